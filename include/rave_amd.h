@@ -1,0 +1,235 @@
+/*
+ * rave_amd.h -- C-ABI of the MI355X-native RAVE encode->decode path.
+ *
+ * Plain C, plain pointers and sizes; no torch or HIP types in any signature
+ * (streams are passed as `void*` holding a hipStream_t, NULL = default stream).
+ * Every entry point returns RAVE_OK (0) or a negative status; the last error
+ * text is available through rave_last_error().  Kernels never allocate:
+ * callers own every buffer (weights, activations, workspace, streaming state).
+ * Calls are asynchronous on the given stream and never synchronise the host.
+ *
+ * What each entry point replaces in the reference (abargum/RAVE @ 2024-10-16):
+ *
+ *   rave_conv1d          cc.Conv1d / cc.ConvTranspose1d forward (third-party
+ *                        cached_conv, non-cached mode: F.pad + conv), fused with
+ *                        the preceding activation module (nn.LeakyReLU(.2),
+ *                        rave/blocks.py:91 / Snake rave/blocks.py:845-853) and
+ *                        the Residual add (rave/blocks.py:44-46).  Call sites:
+ *                        DilatedUnit rave/blocks.py:96-106, EncoderV2
+ *                        :533-584, GeneratorV2 :631-677, NoiseGeneratorV2
+ *                        :257-266.
+ *   rave_pqmf_analysis   CachedPQMF.forward rave/pqmf.py:269-273 (+ reverse_half
+ *                        :13-17, + the band slice of RAVE.encode model.py:613).
+ *   rave_pqmf_synthesis  CachedPQMF.inverse rave/pqmf.py:275-284, optionally fused
+ *                        with GeneratorV2's `x*sigmoid(a) (+noise) -> tanh`
+ *                        epilogue rave/blocks.py:699-707.
+ *   rave_fill_channels   the speaker-embedding concat of RAVE.encode
+ *                        rave/model.py:618-620.
+ *   rave_rvq_encode /    ResidualVectorQuantization.encode / decode
+ *   rave_rvq_decode      rave/quantization.py:302-318.
+ *   rave_plan_*          RAVE.encode / decode / forward rave/model.py:594-634 as
+ *                        one pre-built launch sequence (the module graph).
+ */
+#ifndef RAVE_AMD_H
+#define RAVE_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RAVE_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status */
+enum {
+    RAVE_OK = 0,
+    RAVE_ERR_ARG = -1,          /* invalid argument (ValueError in Python)      */
+    RAVE_ERR_HIP = -2,          /* HIP runtime error (RuntimeError)             */
+    RAVE_ERR_UNSUPPORTED = -3,  /* shape/config the kernels do not implement    */
+    RAVE_ERR_STATE = -4         /* bad handle / plan                            */
+};
+
+/* activation applied to a conv INPUT (fused prologue) */
+enum { RAVE_ACT_NONE = 0, RAVE_ACT_LEAKY = 1, RAVE_ACT_SNAKE = 2 };
+
+const char* rave_last_error(void);
+int rave_abi_version(void);
+/* sizeof of every public struct, in declaration order (ABI self-check) */
+int rave_struct_sizes(int64_t* out, int n);
+
+/* ---------------------------------------------------------------- conv1d
+ * y[b, m, n] = bias[m] + sum_{ci,j} W[m, ci, j] * act(x)[b, ci, n*stride + j*dil - pad_left]
+ *              (+ residual[b, m, n])
+ * with zero padding outside [0, t_in).  Time is contiguous (stride 1) in every
+ * tensor; batch and channel strides are free, so views into larger buffers
+ * (concatenations, streaming history) need no copies.
+ *
+ * transposed = 1: nn.ConvTranspose1d(c_in, c_out, 2r, stride=r) executed in
+ * polyphase form: a 2-tap conv over the input producing r phases per input
+ * position u, written to y[b, co, u*r + q - out_shift] (kept when inside
+ * [0, t_out)).  Offline (padding r//2): pad_left = pad_right = 1,
+ * out_shift = r//2, t_out = t_in*r.  Cached streaming: the input view carries
+ * one history column, pad 0, out_shift 0.
+ */
+typedef struct rave_conv1d_args {
+    int32_t c_in, c_out, kernel, stride, dilation;
+    int32_t pad_left, pad_right;
+    int32_t transposed;     /* 0/1; kernel == 2*stride when set                  */
+    int32_t out_shift;      /* transposed only                                   */
+    int32_t act;            /* RAVE_ACT_*                                        */
+    float   leaky_slope;    /* 0.2                                               */
+    int32_t batch;
+    int32_t t_in;           /* input length (columns of x)                       */
+    int32_t t_out;          /* output length (columns of y)                      */
+    int32_t _pad0;
+    const float* x;       int64_t x_sb, x_sc;
+    float* y;             int64_t y_sb, y_sc;
+    const float* residual; int64_t r_sb, r_sc;   /* NULL = none                  */
+    const float* weight;  /* packed by rave_conv1d_pack_weight                   */
+    const float* bias;    /* c_out floats or NULL                                */
+    const float* alpha;   /* c_in Snake alphas (act == RAVE_ACT_SNAKE)           */
+} rave_conv1d_args;
+
+/* input channels per K-chunk the kernels use for a layer shape */
+int rave_conv1d_chunk(int c_in, int kernel, int stride, int dilation, int transposed);
+/* floats of the packed weight of a layer */
+int64_t rave_conv1d_packed_size(int c_in, int c_out, int kernel, int stride, int dilation,
+                                int transposed);
+/* Host-side repack of a folded torch-layout weight (Conv1d: (c_out, c_in, k);
+ * ConvTranspose1d: (c_in, c_out, k)) into the kernel's K-chunked layout. */
+int rave_conv1d_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
+                            int dilation, int transposed, float* packed);
+int rave_conv1d(const rave_conv1d_args* a, void* stream);
+
+/* ---------------------------------------------------------------- PQMF
+ * analysis: y[b, band, t] = rh(band, t) * sum_j hkf[band, j] * x[b, t*n_band + j - pad_left]
+ * for band < n_out_bands, rh = -1 on odd bands at even t (reverse_half).
+ * hkf: (n_band, taps) analysis filter (taps = 513 for 16 bands).
+ */
+typedef struct rave_pqmf_analysis_args {
+    int32_t n_band, taps, n_out_bands, batch;
+    int32_t t_in, pad_left;     /* t_out = t_in / n_band                          */
+    int32_t t_out, _pad0;
+    const float* x; int64_t x_sb;
+    float* y;       int64_t y_sb, y_sc;
+    const float* hkf;
+} rave_pqmf_analysis_args;
+int rave_pqmf_analysis(const rave_pqmf_analysis_args* a, void* stream);
+
+/* synthesis: in = reverse_half(mode==0 ? x : tanh(x[:n]*sigmoid(x[n:2n]) + noise))
+ * c[m, t] = n_band * sum_{c,k} hki[m, c, k] * in[c, t + k - pad_left]   for t in [0, t_in)
+ * y[b, t*n_band + i] = c[n_band-1-i, t]
+ * x columns [0, x_len) are valid input frames (x_len = 0 means t_in; columns
+ * outside read as zero padding); `frame0` is the global frame index of
+ * column 0 (reverse_half parity).  noise: (B, n_band, x_len) or NULL.
+ * Streaming: point x at the cached history, pad_left = 0, x_len = hist + t_in.
+ */
+typedef struct rave_pqmf_synthesis_args {
+    int32_t n_band, taps, batch, t_in;
+    int32_t pad_left, mode, frame0, x_len;
+    const float* x;     int64_t x_sb, x_sc;
+    const float* noise; int64_t n_sb, n_sc;
+    float* y;           int64_t y_sb;
+    const float* hki;   /* (n_band, n_band, taps) */
+} rave_pqmf_synthesis_args;
+int rave_pqmf_synthesis(const rave_pqmf_synthesis_args* a, void* stream);
+
+/* ---------------------------------------------------------------- misc */
+/* y[b, c, t] = values[c] for c < channels, t < t_len (speaker concat) */
+typedef struct rave_fill_args {
+    int32_t batch, channels, t_len, _pad0;
+    float* y; int64_t y_sb, y_sc;
+    const float* values;
+} rave_fill_args;
+int rave_fill_channels(const rave_fill_args* a, void* stream);
+
+/* y[b, c, t] = x[b, c, t] for c < channels, t < t_len (streaming input staging) */
+typedef struct rave_copy_args {
+    int32_t batch, channels, t_len, _pad0;
+    const float* x; int64_t x_sb, x_sc;
+    float* y;       int64_t y_sb, y_sc;
+} rave_copy_args;
+int rave_copy(const rave_copy_args* a, void* stream);
+
+/* ---------------------------------------------------------------- RVQ
+ * encode: for q in [0, n_q): idx[b, q, t] = argmax_k -(|r|^2 - 2 r.E_q[k] + |E_q[k]|^2),
+ *         r -= E_q[idx];   r starts as z[b, :, t]   (first index on ties)
+ * decode: y[b, :, t] = sum_q E_q[idx[b, q, t]]
+ * codebooks: (n_q, codebook_size, dim) fp32; idx int64.
+ */
+typedef struct rave_rvq_args {
+    int32_t n_q, codebook_size, dim, batch;
+    int32_t t_len, _pad0;
+    const float* codebooks;
+    const float* z;  int64_t z_sb, z_sc;      /* encode input                     */
+    int64_t* idx;    int64_t i_sb, i_sq;      /* (B, n_q, T) int64                */
+    float* y;        int64_t y_sb, y_sc;      /* decode output                    */
+} rave_rvq_args;
+int rave_rvq_encode(const rave_rvq_args* a, void* stream);
+int rave_rvq_decode(const rave_rvq_args* a, void* stream);
+
+/* SHIFT_HISTORY payload (streaming state update): for each (b, c) row of a
+ * buffer with `hist` history columns and `t_new` fresh ones, move the last
+ * `hist` columns to the front.  Rows are independent. */
+typedef struct rave_shift_args {
+    int32_t batch, channels, hist, t_new;
+    float* buf; int64_t sb, sc;
+} rave_shift_args;
+int rave_shift_history(const rave_shift_args* a, void* stream);
+
+/* ---------------------------------------------------------------- plans
+ * A plan is a recorded sequence of the ops above (the module graph of
+ * RAVE.encode/decode).  Pointer fields inside an op's args may be relocated at
+ * run time: a relocation (op, byte offset of the pointer field inside `args`,
+ * slot, byte offset) makes the executor store slots[slot] + byte_offset there,
+ * so one plan serves every call with fresh input/output buffers.
+ */
+enum {
+    RAVE_OP_CONV = 1,
+    RAVE_OP_PQMF_ANALYSIS = 2,
+    RAVE_OP_PQMF_SYNTHESIS = 3,
+    RAVE_OP_FILL = 4,
+    RAVE_OP_RVQ_ENCODE = 5,
+    RAVE_OP_RVQ_DECODE = 6,
+    RAVE_OP_SHIFT_HISTORY = 7,
+    RAVE_OP_COPY = 8
+};
+
+#define RAVE_OP_PAYLOAD 240
+typedef struct rave_plan_op {
+    int32_t kind, _pad0;
+    union {
+        rave_conv1d_args conv;
+        rave_pqmf_analysis_args ana;
+        rave_pqmf_synthesis_args syn;
+        rave_fill_args fill;
+        rave_rvq_args rvq;
+        rave_shift_args shift;
+        rave_copy_args copy;
+        unsigned char raw[RAVE_OP_PAYLOAD];
+    } u;
+} rave_plan_op;
+
+typedef struct rave_reloc {
+    int32_t op, field_offset, slot, _pad0;
+    int64_t byte_offset;
+} rave_reloc;
+
+typedef struct rave_plan rave_plan;
+int rave_plan_create(const rave_plan_op* ops, int n_ops, const rave_reloc* relocs, int n_relocs,
+                     rave_plan** out);
+int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, void* stream);
+int rave_plan_destroy(rave_plan* plan);
+int rave_plan_size(const rave_plan* plan);
+/* Per-op timing with HIP events recorded around every op on the run stream
+ * (measurement only; enable = 0 frees the events).  rave_plan_op_times waits
+ * for the last run and ADDS each op's elapsed milliseconds into ms[0..n). */
+int rave_plan_profile(rave_plan* plan, int enable);
+int rave_plan_op_times(rave_plan* plan, float* ms, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAVE_AMD_H */

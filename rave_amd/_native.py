@@ -1,0 +1,189 @@
+"""ctypes binding of librave_amd.so (include/rave_amd.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` /
+``make -C rave_amd/csrc``.  There is no fallback: if the library is missing
+or its ABI does not match these struct mirrors, importing fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librave_amd.so")
+
+RAVE_OK = 0
+RAVE_ERR_ARG = -1
+RAVE_ERR_HIP = -2
+RAVE_ERR_UNSUPPORTED = -3
+RAVE_ERR_STATE = -4
+
+ACT = {"none": 0, "leaky": 1, "snake": 2}
+
+OP_CONV = 1
+OP_PQMF_ANALYSIS = 2
+OP_PQMF_SYNTHESIS = 3
+OP_FILL = 4
+OP_RVQ_ENCODE = 5
+OP_RVQ_DECODE = 6
+OP_SHIFT_HISTORY = 7
+OP_COPY = 8
+
+i32, i64, f32, vp = C.c_int32, C.c_int64, C.c_float, C.c_void_p
+
+
+class ConvArgs(C.Structure):
+    _fields_ = [("c_in", i32), ("c_out", i32), ("kernel", i32), ("stride", i32), ("dilation", i32),
+                ("pad_left", i32), ("pad_right", i32), ("transposed", i32), ("out_shift", i32),
+                ("act", i32), ("leaky_slope", f32), ("batch", i32), ("t_in", i32), ("t_out", i32),
+                ("_pad0", i32),
+                ("x", vp), ("x_sb", i64), ("x_sc", i64),
+                ("y", vp), ("y_sb", i64), ("y_sc", i64),
+                ("residual", vp), ("r_sb", i64), ("r_sc", i64),
+                ("weight", vp), ("bias", vp), ("alpha", vp)]
+
+
+class AnalysisArgs(C.Structure):
+    _fields_ = [("n_band", i32), ("taps", i32), ("n_out_bands", i32), ("batch", i32),
+                ("t_in", i32), ("pad_left", i32), ("t_out", i32), ("_pad0", i32),
+                ("x", vp), ("x_sb", i64),
+                ("y", vp), ("y_sb", i64), ("y_sc", i64),
+                ("hkf", vp)]
+
+
+class SynthesisArgs(C.Structure):
+    _fields_ = [("n_band", i32), ("taps", i32), ("batch", i32), ("t_in", i32),
+                ("pad_left", i32), ("mode", i32), ("frame0", i32), ("x_len", i32),
+                ("x", vp), ("x_sb", i64), ("x_sc", i64),
+                ("noise", vp), ("n_sb", i64), ("n_sc", i64),
+                ("y", vp), ("y_sb", i64),
+                ("hki", vp)]
+
+
+class FillArgs(C.Structure):
+    _fields_ = [("batch", i32), ("channels", i32), ("t_len", i32), ("_pad0", i32),
+                ("y", vp), ("y_sb", i64), ("y_sc", i64), ("values", vp)]
+
+
+class RvqArgs(C.Structure):
+    _fields_ = [("n_q", i32), ("codebook_size", i32), ("dim", i32), ("batch", i32),
+                ("t_len", i32), ("_pad0", i32),
+                ("codebooks", vp),
+                ("z", vp), ("z_sb", i64), ("z_sc", i64),
+                ("idx", vp), ("i_sb", i64), ("i_sq", i64),
+                ("y", vp), ("y_sb", i64), ("y_sc", i64)]
+
+
+class ShiftArgs(C.Structure):
+    _fields_ = [("batch", i32), ("channels", i32), ("hist", i32), ("t_new", i32),
+                ("buf", vp), ("sb", i64), ("sc", i64)]
+
+
+class CopyArgs(C.Structure):
+    _fields_ = [("batch", i32), ("channels", i32), ("t_len", i32), ("_pad0", i32),
+                ("x", vp), ("x_sb", i64), ("x_sc", i64),
+                ("y", vp), ("y_sb", i64), ("y_sc", i64)]
+
+
+PAYLOAD = 240
+
+
+class PlanOp(C.Structure):
+    _fields_ = [("kind", i32), ("_pad0", i32), ("raw", C.c_ubyte * PAYLOAD)]
+
+
+class Reloc(C.Structure):
+    _fields_ = [("op", i32), ("field_offset", i32), ("slot", i32), ("_pad0", i32),
+                ("byte_offset", i64)]
+
+
+STRUCTS = [ConvArgs, AnalysisArgs, SynthesisArgs, FillArgs, RvqArgs, ShiftArgs, PlanOp, Reloc,
+           CopyArgs]
+
+# every exported symbol of include/rave_amd.h
+EXPORTS = [
+    "rave_last_error", "rave_abi_version", "rave_struct_sizes",
+    "rave_conv1d_chunk", "rave_conv1d_packed_size", "rave_conv1d_pack_weight", "rave_conv1d",
+    "rave_pqmf_analysis", "rave_pqmf_synthesis", "rave_fill_channels", "rave_copy",
+    "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history",
+    "rave_plan_create", "rave_plan_run", "rave_plan_destroy", "rave_plan_size",
+    "rave_plan_profile", "rave_plan_op_times",
+]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"rave_amd native library not built: {LIB_PATH} is missing "
+                          "(run `python -c 'import __graft_entry__ as g; g.build()'` or "
+                          "`make -C rave_amd/csrc`)")
+    lib = C.CDLL(LIB_PATH)
+    lib.rave_last_error.restype = C.c_char_p
+    lib.rave_abi_version.restype = C.c_int
+    lib.rave_struct_sizes.argtypes = [C.POINTER(i64), C.c_int]
+    lib.rave_conv1d_chunk.argtypes = [C.c_int] * 5
+    lib.rave_conv1d_packed_size.argtypes = [C.c_int] * 6
+    lib.rave_conv1d_packed_size.restype = i64
+    lib.rave_conv1d_pack_weight.argtypes = [vp] + [C.c_int] * 6 + [vp]
+    for name, st in [("rave_conv1d", ConvArgs), ("rave_pqmf_analysis", AnalysisArgs),
+                     ("rave_pqmf_synthesis", SynthesisArgs), ("rave_fill_channels", FillArgs),
+                     ("rave_rvq_encode", RvqArgs), ("rave_rvq_decode", RvqArgs),
+                     ("rave_shift_history", ShiftArgs), ("rave_copy", CopyArgs)]:
+        getattr(lib, name).argtypes = [C.POINTER(st), vp]
+    lib.rave_plan_create.argtypes = [C.POINTER(PlanOp), C.c_int, C.POINTER(Reloc), C.c_int,
+                                     C.POINTER(vp)]
+    lib.rave_plan_run.argtypes = [vp, C.POINTER(vp), C.c_int, vp]
+    lib.rave_plan_destroy.argtypes = [vp]
+    lib.rave_plan_size.argtypes = [vp]
+    lib.rave_plan_profile.argtypes = [vp, C.c_int]
+    lib.rave_plan_op_times.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
+    # ABI self-check
+    n = lib.rave_struct_sizes(None, 0)
+    buf = (i64 * n)()
+    lib.rave_struct_sizes(buf, n)
+    native = list(buf)
+    mine = [C.sizeof(s) for s in STRUCTS]
+    if native != mine:
+        raise ImportError(f"rave_amd ABI mismatch: native struct sizes {native} != ctypes {mine}")
+    if lib.rave_abi_version() != 1:
+        raise ImportError("rave_amd ABI version mismatch")
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc == RAVE_OK:
+        return
+    msg = lib.rave_last_error().decode(errors="replace")
+    text = f"{what}: {msg}" if what else msg
+    if rc in (RAVE_ERR_ARG,):
+        raise ValueError(text)
+    if rc == RAVE_ERR_UNSUPPORTED:
+        raise NotImplementedError(text)
+    raise NativeError(f"{text} (status {rc})")
+
+
+def conv_chunk(c_in, kernel, stride, dilation, transposed) -> int:
+    return int(lib.rave_conv1d_chunk(c_in, kernel, stride, dilation, int(transposed)))
+
+
+def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed):
+    """Host repack (numpy float32, torch layout) -> packed numpy float32."""
+    import numpy as np
+    w = np.ascontiguousarray(w, dtype=np.float32)
+    n = int(lib.rave_conv1d_packed_size(c_in, c_out, kernel, stride, dilation, int(transposed)))
+    if n <= 0:
+        raise NotImplementedError(f"unsupported conv shape c_in={c_in} k={kernel} s={stride} d={dilation}")
+    out = np.empty(n, np.float32)
+    check(lib.rave_conv1d_pack_weight(w.ctypes.data, c_in, c_out, kernel, stride, dilation,
+                                      int(transposed), out.ctypes.data), "pack_weight")
+    return out
+
+
+def struct_payload(args: C.Structure):
+    return bytes(C.string_at(C.addressof(args), C.sizeof(args)))

@@ -1,0 +1,158 @@
+// C-ABI glue: error reporting, ABI self-check, and the plan executor that
+// replays a recorded op sequence (the RAVE.encode / decode module graph,
+// rave/model.py:594-634) with per-call pointer relocation.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rave_amd.h"
+
+namespace rave {
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+}  // namespace rave
+
+struct rave_plan {
+    std::vector<rave_plan_op> ops;
+    std::vector<rave_reloc> relocs;
+    std::vector<rave_plan_op> scratch;   // relocated copy used by run()
+    std::vector<hipEvent_t> ev;          // 2 per op when profiling
+    bool ran = false;
+};
+
+extern "C" const char* rave_last_error(void) { return rave::g_err.c_str(); }
+
+extern "C" int rave_abi_version(void) { return RAVE_ABI_VERSION; }
+
+extern "C" int rave_struct_sizes(int64_t* out, int n) {
+    const int64_t sizes[] = {
+        (int64_t)sizeof(rave_conv1d_args),       (int64_t)sizeof(rave_pqmf_analysis_args),
+        (int64_t)sizeof(rave_pqmf_synthesis_args), (int64_t)sizeof(rave_fill_args),
+        (int64_t)sizeof(rave_rvq_args),          (int64_t)sizeof(rave_shift_args),
+        (int64_t)sizeof(rave_plan_op),           (int64_t)sizeof(rave_reloc),
+        (int64_t)sizeof(rave_copy_args),
+    };
+    const int cnt = (int)(sizeof(sizes) / sizeof(sizes[0]));
+    if (!out) return cnt;
+    for (int i = 0; i < n && i < cnt; ++i) out[i] = sizes[i];
+    return cnt;
+}
+
+extern "C" int rave_plan_create(const rave_plan_op* ops, int n_ops, const rave_reloc* relocs,
+                                int n_relocs, rave_plan** out) {
+    if (!out || n_ops < 0 || n_relocs < 0 || (n_ops && !ops) || (n_relocs && !relocs)) {
+        rave::set_error("plan_create: bad arguments");
+        return RAVE_ERR_ARG;
+    }
+    for (int i = 0; i < n_relocs; ++i) {
+        const rave_reloc& r = relocs[i];
+        if (r.op < 0 || r.op >= n_ops || r.field_offset < 0 ||
+            r.field_offset + (int)sizeof(void*) > RAVE_OP_PAYLOAD || (r.field_offset % 8) != 0 ||
+            r.slot < 0) {
+            rave::set_error("plan_create: bad relocation " + std::to_string(i));
+            return RAVE_ERR_ARG;
+        }
+    }
+    rave_plan* p = new rave_plan;
+    p->ops.assign(ops, ops + n_ops);
+    p->relocs.assign(relocs, relocs + n_relocs);
+    p->scratch = p->ops;
+    *out = p;
+    return RAVE_OK;
+}
+
+extern "C" int rave_plan_profile(rave_plan* plan, int enable) {
+    if (!plan) {
+        rave::set_error("plan_profile: null plan");
+        return RAVE_ERR_STATE;
+    }
+    for (hipEvent_t e : plan->ev) (void)hipEventDestroy(e);
+    plan->ev.clear();
+    plan->ran = false;
+    if (enable) {
+        plan->ev.resize(2 * plan->ops.size());
+        for (auto& e : plan->ev) {
+            hipError_t err = hipEventCreate(&e);
+            if (err != hipSuccess) {
+                rave::set_error(std::string("plan_profile: ") + hipGetErrorString(err));
+                return RAVE_ERR_HIP;
+            }
+        }
+    }
+    return RAVE_OK;
+}
+
+extern "C" int rave_plan_op_times(rave_plan* plan, float* ms, int n) {
+    if (!plan || plan->ev.empty() || !plan->ran) {
+        rave::set_error("plan_op_times: profiling not enabled or plan not run");
+        return RAVE_ERR_STATE;
+    }
+    const int nops = (int)plan->ops.size();
+    hipError_t err = hipEventSynchronize(plan->ev[2 * nops - 1]);
+    if (err != hipSuccess) {
+        rave::set_error(std::string("plan_op_times: ") + hipGetErrorString(err));
+        return RAVE_ERR_HIP;
+    }
+    for (int i = 0; i < nops && i < n; ++i) {
+        float t = 0.f;
+        err = hipEventElapsedTime(&t, plan->ev[2 * i], plan->ev[2 * i + 1]);
+        if (err != hipSuccess) {
+            rave::set_error(std::string("plan_op_times: ") + hipGetErrorString(err));
+            return RAVE_ERR_HIP;
+        }
+        ms[i] += t;
+    }
+    return RAVE_OK;
+}
+
+extern "C" int rave_plan_destroy(rave_plan* plan) {
+    if (plan)
+        for (hipEvent_t e : plan->ev) (void)hipEventDestroy(e);
+    delete plan;
+    return RAVE_OK;
+}
+
+extern "C" int rave_plan_size(const rave_plan* plan) { return plan ? (int)plan->ops.size() : -1; }
+
+extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, void* stream) {
+    if (!plan) {
+        rave::set_error("plan_run: null plan");
+        return RAVE_ERR_STATE;
+    }
+    for (const rave_reloc& r : plan->relocs) {
+        if (r.slot >= n_slots || !slots || !slots[r.slot]) {
+            rave::set_error("plan_run: slot " + std::to_string(r.slot) + " not bound");
+            return RAVE_ERR_ARG;
+        }
+        char* base = static_cast<char*>(slots[r.slot]) + r.byte_offset;
+        std::memcpy(plan->scratch[r.op].u.raw + r.field_offset, &base, sizeof(void*));
+    }
+    const bool prof = !plan->ev.empty();
+    for (size_t i = 0; i < plan->scratch.size(); ++i) {
+        const rave_plan_op& op = plan->scratch[i];
+        int rc;
+        if (prof) (void)hipEventRecord(plan->ev[2 * i], static_cast<hipStream_t>(stream));
+        switch (op.kind) {
+            case RAVE_OP_CONV: rc = rave_conv1d(&op.u.conv, stream); break;
+            case RAVE_OP_PQMF_ANALYSIS: rc = rave_pqmf_analysis(&op.u.ana, stream); break;
+            case RAVE_OP_PQMF_SYNTHESIS: rc = rave_pqmf_synthesis(&op.u.syn, stream); break;
+            case RAVE_OP_FILL: rc = rave_fill_channels(&op.u.fill, stream); break;
+            case RAVE_OP_RVQ_ENCODE: rc = rave_rvq_encode(&op.u.rvq, stream); break;
+            case RAVE_OP_RVQ_DECODE: rc = rave_rvq_decode(&op.u.rvq, stream); break;
+            case RAVE_OP_SHIFT_HISTORY: rc = rave_shift_history(&op.u.shift, stream); break;
+            case RAVE_OP_COPY: rc = rave_copy(&op.u.copy, stream); break;
+            default:
+                rave::set_error("plan_run: unknown op kind " + std::to_string(op.kind));
+                return RAVE_ERR_STATE;
+        }
+        if (rc != RAVE_OK) {
+            rave::set_error("plan op " + std::to_string(i) + ": " + rave::g_err);
+            return rc;
+        }
+        if (prof) (void)hipEventRecord(plan->ev[2 * i + 1], static_cast<hipStream_t>(stream));
+    }
+    plan->ran = true;
+    return RAVE_OK;
+}

@@ -1,0 +1,431 @@
+"""``RAVE``: the reference's encode / decode / forward surface on HIP kernels.
+
+Mirrors ``rave.model.RAVE`` (rave/model.py:594-634):
+
+* ``encode(x)``  x (B, 1, T) -> PQMF analysis -> bands[:, :6] -> EncoderV2 ->
+  cat(z, speaker) = (B, latent + 256, T / hop)          (model.py:594-622)
+* ``decode(z)``  GeneratorV2 -> PQMF synthesis -> (B, 1, T)   (model.py:624-629)
+* ``forward(x)`` = decode(encode(x))                          (model.py:631-634)
+
+and, for the discrete config, the nn~ export path of DiscreteScriptedRAVE
+(scripts/export.py:503-517): ``encode_codes`` (encoder -> rvq.encode) and
+``decode_codes`` (rvq.decode -> cat speaker -> decoder -> PQMF inverse).
+
+Every call runs a pre-recorded launch plan (one ctypes call, all launches
+issued from C++ on torch's current stream).  Tensors are torch CUDA tensors;
+PyTorch only provides device memory and the stream.  There is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, List, Mapping, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import pqmf as P
+from .config import RaveConfig, get_padding
+from .graph import ConvNode, build_graph
+from .weights import check_params, conv_weight
+
+
+# ============================================================ device constants
+class Arena:
+    """All constants of a model (packed conv weights, biases, Snake alphas,
+    PQMF kernels, speaker embedding, codebooks) in one device allocation."""
+
+    ALIGN = 64  # floats (256 B)
+
+    def __init__(self):
+        self._parts: List[np.ndarray] = []
+        self.size = 0
+        self.tensor: Optional[torch.Tensor] = None
+
+    def add(self, arr: np.ndarray) -> int:
+        arr = np.ascontiguousarray(arr, np.float32).reshape(-1)
+        off = self.size
+        self._parts.append((off, arr))
+        self.size = off + ((arr.size + self.ALIGN - 1) // self.ALIGN) * self.ALIGN
+        return off
+
+    def upload(self, device) -> None:
+        host = np.zeros(max(self.size, 1), np.float32)
+        for off, arr in self._parts:
+            host[off:off + arr.size] = arr
+        self.tensor = torch.from_numpy(host).to(device)
+        self._parts = []
+
+    def ptr(self, off: int) -> int:
+        return self.tensor.data_ptr() + 4 * off
+
+
+# ============================================================ plans
+@dataclass(frozen=True)
+class View:
+    """A (B, C, T) time-contiguous view: slot 'ws' (workspace), 'arena', or an
+    integer I/O slot bound at run time."""
+    slot: object
+    off: int          # elements from the slot base
+    sb: int
+    sc: int
+    elem: int = 4     # bytes per element
+
+
+class Workspace:
+    """First-fit allocator with liveness-based reuse (sizes in floats)."""
+
+    ALIGN = 64
+
+    def __init__(self):
+        self.free: List[Tuple[int, int]] = []
+        self.top = 0
+
+    def alloc(self, n: int) -> int:
+        n = ((n + self.ALIGN - 1) // self.ALIGN) * self.ALIGN
+        for i, (off, sz) in enumerate(self.free):
+            if sz >= n:
+                if sz == n:
+                    self.free.pop(i)
+                else:
+                    self.free[i] = (off + n, sz - n)
+                return off
+        off = self.top
+        self.top += n
+        return off
+
+    def release(self, off: int, n: int) -> None:
+        n = ((n + self.ALIGN - 1) // self.ALIGN) * self.ALIGN
+        self.free.append((off, n))
+        self.free.sort()
+        merged: List[Tuple[int, int]] = []
+        for o, s in self.free:
+            if merged and merged[-1][0] + merged[-1][1] == o:
+                merged[-1] = (merged[-1][0], merged[-1][1] + s)
+            else:
+                merged.append((o, s))
+        self.free = merged
+
+
+class Plan:
+    """Symbolic op list -> native rave_plan with relocations for I/O slots."""
+
+    def __init__(self, arena: Arena):
+        self.arena = arena
+        self.ws = Workspace()
+        self.sym: List[Tuple[int, type, dict, dict]] = []
+        self.labels: List[str] = []
+        self.flops: List[float] = []
+        self.handle = None
+        self.ws_tensor: Optional[torch.Tensor] = None
+
+    def add(self, kind: int, st: type, scalars: dict, ptrs: Dict[str, Optional[View]],
+            label: str = "", flops: float = 0.0):
+        self.sym.append((kind, st, scalars, ptrs))
+        self.labels.append(label or {N.OP_CONV: "conv", N.OP_PQMF_ANALYSIS: "pqmf_analysis",
+                                     N.OP_PQMF_SYNTHESIS: "pqmf_synthesis", N.OP_FILL: "fill",
+                                     N.OP_RVQ_ENCODE: "rvq_encode", N.OP_RVQ_DECODE: "rvq_decode",
+                                     N.OP_SHIFT_HISTORY: "shift_history"}.get(kind, "op"))
+        self.flops.append(float(flops))
+
+    def finalize(self, device) -> "Plan":
+        self.ws_tensor = torch.empty(max(self.ws.top, 1), dtype=torch.float32, device=device)
+        n = len(self.sym)
+        ops = (N.PlanOp * max(n, 1))()
+        relocs = []
+        for i, (kind, st, scalars, ptrs) in enumerate(self.sym):
+            args = st()
+            for k, v in scalars.items():
+                setattr(args, k, v)
+            for field, view in ptrs.items():
+                if view is None:
+                    setattr(args, field, None)
+                    continue
+                if view.slot == "ws":
+                    setattr(args, field, self.ws_tensor.data_ptr() + view.elem * view.off)
+                elif view.slot == "arena":
+                    setattr(args, field, self.arena.ptr(view.off))
+                else:
+                    setattr(args, field, None)
+                    relocs.append(N.Reloc(i, getattr(st, field).offset, int(view.slot), 0,
+                                          view.elem * view.off))
+            ops[i].kind = kind
+            C.memmove(ops[i].raw, C.addressof(args), C.sizeof(args))
+        rl = (N.Reloc * max(len(relocs), 1))(*relocs)
+        h = C.c_void_p()
+        N.check(N.lib.rave_plan_create(ops, n, rl, len(relocs), C.byref(h)), "plan_create")
+        self.handle = h
+        return self
+
+    def run(self, slots: List[int], stream: Optional[int] = None) -> None:
+        arr = (C.c_void_p * len(slots))(*slots)
+        if stream is None:
+            stream = torch.cuda.current_stream().cuda_stream
+        N.check(N.lib.rave_plan_run(self.handle, arr, len(slots), C.c_void_p(stream)), "plan_run")
+
+    def profile(self, enable: bool = True) -> None:
+        N.check(N.lib.rave_plan_profile(self.handle, int(enable)), "plan_profile")
+
+    def op_times(self, acc: Optional[np.ndarray] = None) -> np.ndarray:
+        """Add the last run's per-op milliseconds (HIP events) into ``acc``."""
+        n = len(self.sym)
+        buf = (C.c_float * n)()
+        if acc is not None:
+            for i in range(n):
+                buf[i] = float(acc[i])
+        N.check(N.lib.rave_plan_op_times(self.handle, buf, n), "plan_op_times")
+        return np.array(list(buf), np.float64)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and N is not None and N.lib is not None:
+            N.lib.rave_plan_destroy(h)
+            self.handle = None
+
+
+# ============================================================ model
+class RAVE:
+    """HIP implementation of RAVE.encode / decode / forward for one config."""
+
+    def __init__(self, cfg: RaveConfig, params: Mapping[str, np.ndarray], speaker: np.ndarray,
+                 device=None, hk: Optional[np.ndarray] = None,
+                 adain_stats: Optional[Mapping] = None):
+        if adain_stats:
+            raise NotImplementedError("AdaIN with learned statistics is not implemented on the "
+                                      "HIP path yet (eval-mode identity is)")
+        check_params(cfg, params)
+        self.cfg = cfg
+        self.graph = build_graph(cfg)
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise ValueError("rave_amd.RAVE runs on the GPU only (device must be cuda)")
+        ar = Arena()
+        self.w_off: Dict[str, Tuple[int, Optional[int], Optional[int]]] = {}
+        for n in self.graph.convs():
+            w = conv_weight(n, params)
+            packed = N.pack_conv_weight(w, n.c_in, n.c_out, n.kernel, n.stride, n.dilation, n.transposed)
+            wo = ar.add(packed)
+            bo = ar.add(params[n.name + ".bias"]) if n.bias else None
+            ao = ar.add(params[n.alpha]) if n.act == "snake" else None
+            self.w_off[n.name] = (wo, bo, ao)
+        self.hk = P.design_bank(cfg.pqmf_attenuation, cfg.n_band) if hk is None else np.asarray(hk, np.float32)
+        hkf, hki = P.kernels(self.hk)
+        self.taps_a, self.taps_s = hkf.shape[-1], hki.shape[-1]
+        self.hkf_off = ar.add(hkf)
+        self.hki_off = ar.add(hki)
+        spk = np.asarray(speaker, np.float32).reshape(-1)
+        if spk.size != cfg.speaker_size:
+            raise ValueError(f"speaker embedding must have {cfg.speaker_size} values")
+        self.spk_off = ar.add(spk)
+        self.cb_off = None
+        if cfg.rvq is not None:
+            cbs = np.stack([np.asarray(params[f"encoder.rvq.layers.{i}._codebook.embed"], np.float32)
+                            for i in range(cfg.rvq.num_quantizers)])
+            self.cb_off = ar.add(cbs)
+        ar.upload(self.device)
+        self.arena = ar
+        self._plans: Dict[tuple, Plan] = {}
+
+    # ------------------------------------------------------------ plan pieces
+    def _conv(self, plan: Plan, n: ConvNode, B: int, t_in: int, src: View, dst: View,
+              res: Optional[View]) -> int:
+        wo, bo, ao = self.w_off[n.name]
+        t_out = n.out_len(t_in)
+        s = dict(c_in=n.c_in, c_out=n.c_out, kernel=n.kernel, stride=n.stride, dilation=n.dilation,
+                 act=N.ACT[n.act], leaky_slope=self.cfg.leaky_slope, batch=B, t_in=t_in, t_out=t_out,
+                 x_sb=src.sb, x_sc=src.sc, y_sb=dst.sb, y_sc=dst.sc,
+                 r_sb=res.sb if res else 0, r_sc=res.sc if res else 0)
+        if n.transposed:
+            s.update(pad_left=1, pad_right=1, transposed=1, out_shift=n.stride // 2)
+        else:
+            s.update(pad_left=n.pad[0], pad_right=n.pad[1], transposed=0, out_shift=0)
+        ptrs = dict(x=src, y=dst, residual=res, weight=View("arena", wo, 0, 0),
+                    bias=View("arena", bo, 0, 0) if bo is not None else None,
+                    alpha=View("arena", ao, 0, 0) if ao is not None else None)
+        if n.transposed:
+            flops = 2.0 * B * n.c_out * t_out * n.c_in * 2          # 2 taps per output sample
+        else:
+            flops = 2.0 * B * n.c_out * t_out * n.c_in * n.kernel
+        plan.add(N.OP_CONV, N.ConvArgs, s, ptrs, label=n.name, flops=flops)
+        return t_out
+
+    def _run_stack(self, plan: Plan, nodes: List[ConvNode], B: int, inputs: Dict[str, Tuple[View, int]],
+                   outputs: Dict[str, View]) -> Dict[str, Tuple[View, int, int]]:
+        """Lay a conv sequence into the plan, allocating workspace tensors with
+        liveness-based reuse.  inputs: name -> (view, T)."""
+        last_use: Dict[str, int] = {}
+        for i, n in enumerate(nodes):
+            last_use[n.src] = i
+            if n.residual:
+                last_use[n.residual] = i
+        tensors: Dict[str, Tuple[View, int, int]] = {k: (v, t, -1) for k, (v, t) in inputs.items()}
+        for i, n in enumerate(nodes):
+            src, t_in, _ = tensors[n.src]
+            t_out = n.out_len(t_in)
+            if n.dst in outputs:
+                dst = outputs[n.dst]
+                size = -1
+            else:
+                size = B * n.c_out * t_out
+                dst = View("ws", plan.ws.alloc(size), n.c_out * t_out, t_out)
+            res = tensors[n.residual][0] if n.residual else None
+            self._conv(plan, n, B, t_in, src, dst, res)
+            tensors[n.dst] = (dst, t_out, size)
+            for name in {n.src, n.residual}:
+                if name and last_use.get(name) == i and name in tensors:
+                    v, _, sz = tensors[name]
+                    if sz > 0 and v.slot == "ws" and name not in outputs:
+                        plan.ws.release(v.off, sz)
+        return tensors
+
+    def _analysis(self, plan: Plan, B: int, T: int, x: View, y: View, n_out: int) -> int:
+        cfg = self.cfg
+        F = T // cfg.n_band
+        pad = get_padding(self.taps_a, causal=cfg.causal)[0]
+        plan.add(N.OP_PQMF_ANALYSIS, N.AnalysisArgs,
+                 dict(n_band=cfg.n_band, taps=self.taps_a, n_out_bands=n_out, batch=B, t_in=T,
+                      pad_left=pad, t_out=F, x_sb=x.sb, y_sb=y.sb, y_sc=y.sc),
+                 dict(x=x, y=y, hkf=View("arena", self.hkf_off, 0, 0)),
+                 flops=2.0 * B * n_out * F * self.taps_a)
+        return F
+
+    def _synthesis(self, plan: Plan, B: int, F: int, x: View, y: View, mode: int,
+                   noise: Optional[View] = None, frame0: int = 0) -> None:
+        cfg = self.cfg
+        pad = get_padding(self.taps_s, causal=cfg.causal)[0]
+        plan.add(N.OP_PQMF_SYNTHESIS, N.SynthesisArgs,
+                 dict(n_band=cfg.n_band, taps=self.taps_s, batch=B, t_in=F, pad_left=pad, mode=mode,
+                      frame0=frame0, x_sb=x.sb, x_sc=x.sc,
+                      n_sb=noise.sb if noise else 0, n_sc=noise.sc if noise else 0, y_sb=y.sb),
+                 dict(x=x, y=y, noise=noise, hki=View("arena", self.hki_off, 0, 0)),
+                 flops=2.0 * B * F * cfg.n_band * cfg.n_band * self.taps_s)
+
+    def _fill_speaker(self, plan: Plan, B: int, Fz: int, z: View) -> None:
+        cfg = self.cfg
+        plan.add(N.OP_FILL, N.FillArgs,
+                 dict(batch=B, channels=cfg.speaker_size, t_len=Fz, y_sb=z.sb, y_sc=z.sc),
+                 dict(y=z, values=View("arena", self.spk_off, 0, 0)))
+
+    # ------------------------------------------------------------ plans
+    def _encode_plan(self, B: int, T: int, codes: bool = False) -> Plan:
+        key = ("enc_codes" if codes else "enc", B, T)
+        if key in self._plans:
+            return self._plans[key]
+        cfg = self.cfg
+        plan = Plan(self.arena)
+        F = T // cfg.n_band
+        Fz = T // cfg.hop
+        bands_sz = B * cfg.enc_bands * F
+        bands = View("ws", plan.ws.alloc(bands_sz), cfg.enc_bands * F, F)
+        self._analysis(plan, B, T, View(0, 0, T, T), bands, cfg.enc_bands)
+        if codes:
+            lat = View("ws", plan.ws.alloc(B * cfg.latent_size * Fz), cfg.latent_size * Fz, Fz)
+        else:
+            zc = cfg.latent_size + cfg.speaker_size
+            lat = View(1, 0, zc * Fz, Fz)
+        self._run_stack(plan, self.graph.encoder, B, {"enc_in": (bands, F)}, {"latent": lat})
+        if codes:
+            rq = cfg.rvq
+            plan.add(N.OP_RVQ_ENCODE, N.RvqArgs,
+                     dict(n_q=rq.num_quantizers, codebook_size=rq.codebook_size, dim=cfg.latent_size,
+                          batch=B, t_len=Fz, z_sb=lat.sb, z_sc=lat.sc,
+                          i_sb=rq.num_quantizers * Fz, i_sq=Fz, y_sb=0, y_sc=0),
+                     dict(codebooks=View("arena", self.cb_off, 0, 0), z=lat,
+                          idx=View(1, 0, 0, 0, elem=8), y=None))
+        else:
+            self._fill_speaker(plan, B, Fz, View(1, cfg.latent_size * Fz, lat.sb, Fz))
+        self._plans[key] = plan.finalize(self.device)
+        return plan
+
+    def _decode_plan(self, B: int, Fz: int, codes: bool = False) -> Plan:
+        key = ("dec_codes" if codes else "dec", B, Fz)
+        if key in self._plans:
+            return self._plans[key]
+        cfg = self.cfg
+        if cfg.noise is not None:
+            raise NotImplementedError("NoiseGeneratorV2 is not on the HIP path yet")
+        plan = Plan(self.arena)
+        zc = cfg.dec_in
+        if codes:
+            rq = cfg.rvq
+            z = View("ws", plan.ws.alloc(B * zc * Fz), zc * Fz, Fz)
+            plan.add(N.OP_RVQ_DECODE, N.RvqArgs,
+                     dict(n_q=rq.num_quantizers, codebook_size=rq.codebook_size, dim=cfg.latent_size,
+                          batch=B, t_len=Fz, z_sb=0, z_sc=0, i_sb=rq.num_quantizers * Fz, i_sq=Fz,
+                          y_sb=z.sb, y_sc=z.sc),
+                     dict(codebooks=View("arena", self.cb_off, 0, 0), z=None,
+                          idx=View(0, 0, 0, 0, elem=8), y=z))
+            self._fill_speaker(plan, B, Fz, View("ws", z.off + cfg.latent_size * Fz, z.sb, Fz))
+        else:
+            z = View(0, 0, zc * Fz, Fz)
+        F = Fz * cfg.hop // cfg.n_band
+        wave = View("ws", plan.ws.alloc(B * cfg.dec_out * F), cfg.dec_out * F, F)
+        self._run_stack(plan, self.graph.decoder, B, {"dec_in": (z, Fz)}, {"wave": wave})
+        T = F * cfg.n_band
+        self._synthesis(plan, B, F, wave, View(1, 0, T, T), 1 if cfg.amplitude_modulation else 0)
+        self._plans[key] = plan.finalize(self.device)
+        return plan
+
+    # ------------------------------------------------------------ public API
+    def _check_audio(self, x: torch.Tensor) -> Tuple[int, int]:
+        if not isinstance(x, torch.Tensor) or x.device.type != "cuda" or x.dtype != torch.float32:
+            raise ValueError("x must be a float32 CUDA tensor")
+        if x.dim() != 3 or x.shape[1] != 1:
+            raise ValueError(f"x must be (B, 1, T), got {tuple(x.shape)}")
+        B, _, T = x.shape
+        if T % self.cfg.hop:
+            raise ValueError(f"T={T} must be a multiple of {self.cfg.hop} (n_band * prod(ratios))")
+        return B, T
+
+    def encode(self, x: torch.Tensor) -> torch.Tensor:
+        B, T = self._check_audio(x)
+        x = x.contiguous()
+        Fz = T // self.cfg.hop
+        z = torch.empty(B, self.cfg.latent_size + self.cfg.speaker_size, Fz, device=x.device)
+        self._encode_plan(B, T).run([x.data_ptr(), z.data_ptr()])
+        return z
+
+    def decode(self, z: torch.Tensor) -> torch.Tensor:
+        if not isinstance(z, torch.Tensor) or z.device.type != "cuda" or z.dtype != torch.float32:
+            raise ValueError("z must be a float32 CUDA tensor")
+        if z.dim() != 3 or z.shape[1] != self.cfg.dec_in:
+            raise ValueError(f"z must be (B, {self.cfg.dec_in}, T), got {tuple(z.shape)}")
+        z = z.contiguous()
+        B, _, Fz = z.shape
+        y = torch.empty(B, 1, Fz * self.cfg.hop, device=z.device)
+        self._decode_plan(B, Fz).run([z.data_ptr(), y.data_ptr()])
+        return y
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.decode(self.encode(x))
+
+    __call__ = forward
+
+    def encode_codes(self, x: torch.Tensor) -> torch.Tensor:
+        """encoder -> rvq.encode: (B, n_q, T/hop) int64 (discrete config)."""
+        if self.cfg.rvq is None:
+            raise ValueError("encode_codes needs a discrete (RVQ) config")
+        B, T = self._check_audio(x)
+        x = x.contiguous()
+        idx = torch.empty(B, self.cfg.rvq.num_quantizers, T // self.cfg.hop, dtype=torch.int64,
+                          device=x.device)
+        self._encode_plan(B, T, codes=True).run([x.data_ptr(), idx.data_ptr()])
+        return idx
+
+    def decode_codes(self, idx: torch.Tensor) -> torch.Tensor:
+        """rvq.decode (indices clamped as DiscreteScriptedRAVE) -> cat speaker ->
+        decoder -> PQMF inverse."""
+        if self.cfg.rvq is None:
+            raise ValueError("decode_codes needs a discrete (RVQ) config")
+        if idx.dtype != torch.int64 or idx.device.type != "cuda" or idx.dim() != 3 \
+                or idx.shape[1] != self.cfg.rvq.num_quantizers:
+            raise ValueError("idx must be an int64 CUDA tensor (B, n_q, T)")
+        idx = idx.contiguous()
+        B, _, Fz = idx.shape
+        y = torch.empty(B, 1, Fz * self.cfg.hop, device=idx.device)
+        self._decode_plan(B, Fz, codes=True).run([idx.data_ptr(), y.data_ptr()])
+        return y
+
+    def forward_codes(self, x: torch.Tensor) -> torch.Tensor:
+        return self.decode_codes(self.encode_codes(x))

@@ -1,0 +1,310 @@
+"""HIP path vs the CPU oracle (and the reference's golden fixtures), through
+the C-ABI.  Runs on an MI355X only (``-m gpu``).
+
+Tolerances: the north star is <= 1e-4 max-abs vs the reference fp32 CPU path
+on model outputs; single layers are checked at 2e-5 relative to max|ref|
+(fp32 accumulation over K <= 3072 against a float64 oracle)."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def maxabs(a, b):
+    return float(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)).max())
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def N():
+    from rave_amd import _native
+    return _native
+
+
+def _golden_hk(golden):
+    return golden("pqmf")["hk"]
+
+
+# ------------------------------------------------------------------ single conv
+CONV_CASES = [
+    # c_in, c_out, k, s, d, transposed, act, residual, B, T
+    (64, 64, 3, 1, 1, 0, "leaky", False, 2, 300),
+    (64, 64, 3, 1, 9, 0, "leaky", False, 3, 1000),
+    (128, 128, 1, 1, 1, 0, "leaky", True, 2, 257),
+    (6, 64, 7, 1, 1, 0, "none", False, 2, 512),
+    (64, 128, 8, 4, 1, 0, "leaky", False, 2, 1024),
+    (256, 512, 4, 2, 1, 0, "snake", False, 2, 64),
+    (1024, 64, 3, 1, 1, 0, "leaky", False, 4, 16),
+    (320, 1024, 3, 1, 1, 0, "none", False, 2, 8),
+    (1024, 512, 4, 2, 1, 1, "leaky", False, 2, 8),
+    (128, 64, 8, 4, 1, 1, "snake", False, 2, 100),
+    (64, 32, 7, 1, 1, 0, "snake", False, 2, 4096),
+    (96, 96, 3, 1, 3, 0, "snake", True, 2, 700),
+    (512, 512, 3, 1, 3, 0, "leaky", False, 16, 128),
+]
+
+
+def run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act):
+    B, _, T = x.shape
+    packed = torch.from_numpy(N.pack_conv_weight(w, c_in, c_out, k, s, d, transposed)).to(dev)
+    xd = torch.from_numpy(x).to(dev)
+    if transposed:
+        t_out = T * s
+    else:
+        t_out = (T + pad[0] + pad[1] - ((k - 1) * d + 1)) // s + 1
+    y = torch.full((B, c_out, t_out), float("nan"), device=dev)
+    bd = torch.from_numpy(b).to(dev) if b is not None else None
+    ad = torch.from_numpy(alpha).to(dev) if alpha is not None else None
+    rd = torch.from_numpy(res).to(dev) if res is not None else None
+    a = N.ConvArgs(c_in=c_in, c_out=c_out, kernel=k, stride=s, dilation=d,
+                   pad_left=1 if transposed else pad[0], pad_right=1 if transposed else pad[1],
+                   transposed=transposed, out_shift=s // 2 if transposed else 0, act=N.ACT[act],
+                   leaky_slope=0.2, batch=B, t_in=T, t_out=t_out,
+                   x=xd.data_ptr(), x_sb=c_in * T, x_sc=T, y=y.data_ptr(), y_sb=c_out * t_out, y_sc=t_out,
+                   residual=rd.data_ptr() if rd is not None else None, r_sb=c_out * t_out, r_sc=t_out,
+                   weight=packed.data_ptr(), bias=bd.data_ptr() if bd is not None else None,
+                   alpha=ad.data_ptr() if ad is not None else None)
+    N.check(N.lib.rave_conv1d(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream)), "conv1d")
+    torch.cuda.synchronize()
+    return y.cpu().numpy()
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[str(c[:8]) for c in CONV_CASES])
+def test_conv_layer(N, dev, case):
+    from oracle.rave_oracle import conv1d, conv_transpose1d, leaky_relu, snake
+    c_in, c_out, k, s, d, transposed, act, has_res, B, T = case
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    x = rng.standard_normal((B, c_in, T)).astype(np.float32)
+    bound = 1 / np.sqrt(c_in * k)
+    if transposed:
+        w = rng.uniform(-bound, bound, (c_in, c_out, k)).astype(np.float32)
+    else:
+        w = rng.uniform(-bound, bound, (c_out, c_in, k)).astype(np.float32)
+    b = rng.uniform(-bound, bound, c_out).astype(np.float32)
+    alpha = (1 + 0.1 * rng.standard_normal((c_in, 1))).astype(np.float32) if act == "snake" else None
+    xa = x.astype(np.float64)
+    if act == "leaky":
+        xa = leaky_relu(xa)
+    elif act == "snake":
+        xa = snake(xa, alpha)
+    if transposed:
+        ref = conv_transpose1d(xa, w, s, s // 2, b)
+        pad = (0, 0)
+    else:
+        p = (k - 1) * d + 1
+        pad = ((p - 1) // 2, p // 2)
+        ref = conv1d(xa, w, b, s, d, pad)
+    res = rng.standard_normal(ref.shape).astype(np.float32) if has_res else None
+    if has_res:
+        ref = ref + res
+    got = run_conv(N, dev, x, w, b, alpha.reshape(-1) if alpha is not None else None, res,
+                   c_in, c_out, k, s, d, pad, transposed, act)
+    assert np.isfinite(got).all()
+    assert maxabs(got, ref) <= 2e-5 * max(1.0, np.abs(ref).max())
+
+
+# ------------------------------------------------------------------ PQMF
+@pytest.mark.parametrize("causal", [False, True])
+def test_pqmf_golden(N, dev, golden, causal):
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE, View, Plan
+    g = golden("pqmf")
+    mode = "causal" if causal else "centered"
+    cfg = rcfg.v2(causal=causal, capacity=8)
+    from rave_amd.weights import init_params
+    m = RAVE(cfg, init_params(cfg), np.zeros(256, np.float32), device=dev, hk=g["hk"])
+    x = torch.from_numpy(g["x"]).to(dev)
+    B, _, T = x.shape
+    F = T // 16
+    y = torch.empty(B, 16, F, device=dev)
+    p = Plan(m.arena)
+    m._analysis(p, B, T, View(0, 0, T, T), View(1, 0, 16 * F, F), 16)
+    p.finalize(dev).run([x.data_ptr(), y.data_ptr()])
+    bands = torch.from_numpy(g["bands"]).to(dev)
+    out = torch.empty(B, 1, bands.shape[-1] * 16, device=dev)
+    p2 = Plan(m.arena)
+    m._synthesis(p2, B, bands.shape[-1], View(0, 0, 16 * bands.shape[-1], bands.shape[-1]),
+                 View(1, 0, out.shape[-1], out.shape[-1]), 0)
+    p2.finalize(dev).run([bands.data_ptr(), out.data_ptr()])
+    torch.cuda.synchronize()
+    ref_a = g[f"analysis_{mode}"]
+    ref_s = g[f"synthesis_{mode}"]
+    assert maxabs(y.cpu().numpy(), ref_a) <= 1e-5 * max(1, np.abs(ref_a).max())
+    assert maxabs(out.cpu().numpy(), ref_s) <= 1e-5 * max(1, np.abs(ref_s).max())
+
+
+# ------------------------------------------------------------------ full model vs golden
+def _model(cfg, g, dev, golden):
+    from rave_amd.model import RAVE
+    from rave_amd.weights import init_params
+    return RAVE(cfg, init_params(cfg, seed=int(g["seed"])), g["speaker"], device=dev,
+                hk=_golden_hk(golden))
+
+
+@pytest.mark.parametrize("name", ["v2", "causal", "discrete"])
+def test_model_golden(dev, golden, name):
+    from rave_amd import config as rcfg
+    cfg = rcfg.get_config(name)
+    g = golden(name)
+    m = _model(cfg, g, dev, golden)
+    x = torch.from_numpy(g["x"]).to(dev)
+    z = m.encode(x)
+    ref_z = g["z_enc"] if name == "discrete" else g["z"]
+    zz = z.cpu().numpy()
+    assert maxabs(zz[:, :cfg.latent_size], ref_z[:, :cfg.latent_size]) < TOL
+    assert maxabs(zz[:, cfg.latent_size:], g["speaker"][None, :, None]) == 0.0
+    y = m.decode(torch.from_numpy(g["z"]).to(dev))
+    torch.cuda.synchronize()
+    assert maxabs(y.cpu().numpy(), g["y"]) < TOL
+
+
+def test_discrete_codes_golden(dev, golden):
+    """rvq.encode indices match the reference except where its own top-2
+    distance gap is below the fp32 tie margin; decode_codes matches."""
+    from rave_amd import config as rcfg
+    from oracle.rave_oracle import Oracle
+    cfg = rcfg.discrete()
+    g = golden("discrete")
+    m = _model(cfg, g, dev, golden)
+    idx = m.encode_codes(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
+    ref = g["rvq_idx"]
+    gap = g["rvq_gap"].reshape(cfg.rvq.num_quantizers, ref.shape[0], ref.shape[2]).transpose(1, 0, 2)
+    mism = idx != ref
+    assert (gap[mism] < 1e-3).all(), (mism.sum(), gap[mism])
+    y = m.decode_codes(torch.from_numpy(ref).to(dev))
+    torch.cuda.synchronize()
+    assert maxabs(y.cpu().numpy(), g["y"]) < TOL
+
+
+def test_rvq_kernels_golden(dev, golden, N):
+    from rave_amd import config as rcfg
+    from rave_amd.weights import init_params
+    g = golden("rvq")
+    cfg = rcfg.discrete()
+    params = init_params(cfg, seed=int(g["seed"]))
+    cbs = np.stack([params[f"encoder.rvq.layers.{i}._codebook.embed"] for i in range(16)])
+    cb = torch.from_numpy(cbs).to(dev)
+    z = torch.from_numpy(g["z"]).to(dev)
+    B, D, T = z.shape
+    idx = torch.empty(B, 16, T, dtype=torch.int64, device=dev)
+    y = torch.empty(B, D, T, device=dev)
+    a = N.RvqArgs(n_q=16, codebook_size=1024, dim=D, batch=B, t_len=T, codebooks=cb.data_ptr(),
+                  z=z.data_ptr(), z_sb=D * T, z_sc=T, idx=idx.data_ptr(), i_sb=16 * T, i_sq=T,
+                  y=y.data_ptr(), y_sb=D * T, y_sc=T)
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    N.check(N.lib.rave_rvq_encode(C.byref(a), st))
+    N.check(N.lib.rave_rvq_decode(C.byref(a), st))
+    torch.cuda.synchronize()
+    got = idx.cpu().numpy()
+    ref = g["idx"]
+    gap = g["gap"].reshape(16, B, T).transpose(1, 0, 2)
+    mism = got != ref
+    assert (gap[mism] < 1e-3).all()
+    assert mism.mean() < 0.01
+    if not mism.any():
+        assert maxabs(y.cpu().numpy(), g["zq"]) < 1e-5
+
+
+# ------------------------------------------------------------------ larger sizes vs oracle
+def test_v2_full_clip_vs_oracle(dev):
+    """One 65536-sample clip (BASELINE config 1 size) against the oracle."""
+    from oracle.rave_oracle import Oracle
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.v2()
+    params, spk = init_params(cfg, 0), init_speaker(cfg, 0)
+    T = 65536
+    n = np.arange(T)
+    x = (0.3 * np.sin(2 * np.pi * 440 * n / 48000)
+         + 0.1 * np.random.default_rng(0).standard_normal(T)).astype(np.float32)[None, None]
+    m = RAVE(cfg, params, spk, device=dev)
+    z = m.encode(torch.from_numpy(x).to(dev))
+    y = m.decode(z)
+    torch.cuda.synchronize()
+    o = Oracle(cfg, params, spk, hk=m.hk)
+    zr = o.encode(x)
+    assert maxabs(z.cpu().numpy(), zr) < TOL
+    yr = o.decode(zr)
+    assert maxabs(y.cpu().numpy(), yr) < TOL
+
+
+def test_batch_independence_and_determinism(dev):
+    """At BASELINE config 2 size (16 x 65536): each clip of the batch equals the
+    same clip run alone (no cross-sample coupling), and reruns are bitwise equal."""
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.v2()
+    m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = (0.1 * torch.randn(16, 1, 65536, generator=g)).to(dev)
+    y1 = m.forward(x)
+    y2 = m.forward(x)
+    y3 = m.forward(x[5:6].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    assert torch.isfinite(y1).all()
+    assert float((y1[5:6] - y3).abs().max()) < 1e-5
+
+
+# ------------------------------------------------------------------ streaming (BASELINE config 3)
+def test_causal_streaming_golden(dev, golden):
+    """Block streaming (2048-sample blocks, persistent caches) reproduces the
+    reference's cached_conv streaming outputs block for block."""
+    from rave_amd import config as rcfg
+    from rave_amd.streaming import StreamingRAVE
+    cfg = rcfg.causal()
+    g = golden("causal_stream")
+    m = _model(cfg, g, dev, golden)
+    blk = int(g["block"])
+    s = StreamingRAVE(m, batch=1, block=blk)
+    x = torch.from_numpy(g["x"]).to(dev)
+    z = torch.from_numpy(g["z"]).to(dev)
+    nb = x.shape[-1] // blk
+    Fz = blk // cfg.hop
+    zs = torch.cat([s.encode(x[..., i * blk:(i + 1) * blk].contiguous()) for i in range(nb)], -1)
+    ys = torch.cat([s.decode(z[..., i * Fz:(i + 1) * Fz].contiguous()) for i in range(nb)], -1)
+    torch.cuda.synchronize()
+    assert maxabs(zs.cpu().numpy(), g["z_stream"]) < TOL
+    assert maxabs(ys.cpu().numpy(), g["y_stream"]) < TOL
+    assert s.decode_delay == 928
+
+
+def test_streaming_matches_oneshot_long(dev):
+    """64 blocks of batch 4: streamed decode == one-shot causal decode delayed by
+    928 samples past the receptive field; streamed encode == one-shot encode."""
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE
+    from rave_amd.streaming import StreamingRAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.causal()
+    m = RAVE(cfg, init_params(cfg, 3), init_speaker(cfg, 3), device=dev)
+    B, blk, nb = 4, 2048, 64
+    gen = torch.Generator().manual_seed(1)
+    x = (0.2 * torch.randn(B, 1, blk * nb, generator=gen)).to(dev)
+    s = StreamingRAVE(m, batch=B, block=blk)
+    zs = torch.cat([s.encode(x[..., i * blk:(i + 1) * blk].contiguous()) for i in range(nb)], -1)
+    z1 = m.encode(x)
+    ys = torch.cat([s.decode(z1[..., i * 2:(i + 1) * 2].contiguous()) for i in range(nb)], -1)
+    y1 = m.decode(z1)
+    torch.cuda.synchronize()
+    assert float((zs - z1).abs().max()) < 1e-4
+    d, warm = 928, 12288
+    assert float((ys[..., d + warm:] - y1[..., warm:-d]).abs().max()) < 1e-4
+    s.reset()
+    ys2 = s.decode(z1[..., :2].contiguous())
+    assert torch.equal(ys2, ys[..., :blk])

@@ -1,0 +1,116 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol that
+include/rave_amd.h declares, its struct layouts match the ctypes mirrors, the
+host-side weight packer lays weights out as the kernels read them, and argument
+validation maps to Python exceptions (no GPU needed: nothing here launches)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle.rave_oracle import conv1d, conv_transpose1d
+from rave_amd import _native as N
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "rave_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rave_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_exports_every_header_symbol():
+    names = header_functions()
+    assert len(names) >= 15
+    for name in names:
+        assert hasattr(N.lib, name), name
+    assert sorted(N.EXPORTS) == names
+
+
+def test_struct_sizes_match():
+    n = N.lib.rave_struct_sizes(None, 0)
+    buf = (C.c_int64 * n)()
+    N.lib.rave_struct_sizes(buf, n)
+    assert list(buf) == [C.sizeof(s) for s in N.STRUCTS]
+    assert C.sizeof(N.PlanOp) == 248
+
+
+def _emulate_packed_conv(packed, x, c_in, c_out, k, s, d, pad, transposed):
+    """Run the GEMM the kernel runs, from the packed layout (kk = j*CI_T + ci)."""
+    ci_t = N.conv_chunk(c_in, k, s, d, transposed)
+    taps = 2 if transposed else k
+    R = s if transposed else 1
+    M = c_out * R
+    Mpad = -(-M // 128) * 128
+    nch = -(-c_in // ci_t)
+    W = packed.reshape(nch, taps, ci_t, Mpad)[..., :M]
+    cs, ds = (1, 1) if transposed else (s, d)
+    pl, pr = (1, 1) if transposed else pad
+    xp = np.pad(x.astype(np.float64), ((0, 0), (0, nch * ci_t - c_in), (pl, pr)))
+    B, _, T = xp.shape
+    U = (T - ((taps - 1) * ds + 1)) // cs + 1
+    y = np.zeros((B, M, U))
+    for c in range(nch):
+        for j in range(taps):
+            xs = xp[:, c * ci_t:(c + 1) * ci_t, j * ds: j * ds + (U - 1) * cs + 1: cs]
+            y += np.einsum("im,bin->bmn", W[c, j], xs)
+    if not transposed:
+        return y
+    out = np.zeros((B, c_out, x.shape[-1] * R))
+    sh = R // 2
+    for m in range(M):
+        co, q = divmod(m, R)
+        for u in range(U):
+            t = u * R + q - sh
+            if 0 <= t < out.shape[-1]:
+                out[:, co, t] = y[:, m, u]
+    return out
+
+
+@pytest.mark.parametrize("c_in,c_out,k,s,d,transposed", [
+    (64, 64, 3, 1, 9, 0), (64, 64, 1, 1, 1, 0), (6, 64, 7, 1, 1, 0), (64, 128, 8, 4, 1, 0),
+    (256, 512, 4, 2, 1, 0), (320, 1024, 3, 1, 1, 0), (64, 32, 7, 1, 1, 0), (96, 96, 3, 1, 3, 0),
+    (1024, 512, 4, 2, 1, 1), (128, 64, 8, 4, 1, 1), (1536, 768, 4, 2, 1, 1)])
+def test_pack_layout(c_in, c_out, k, s, d, transposed):
+    rng = np.random.default_rng(1)
+    T = 40
+    x = rng.standard_normal((2, c_in, T)).astype(np.float32)
+    if transposed:
+        w = rng.standard_normal((c_in, c_out, k)).astype(np.float32)
+        ref = conv_transpose1d(x, w, s, s // 2)
+        pad = (1, 1)
+    else:
+        w = rng.standard_normal((c_out, c_in, k)).astype(np.float32)
+        p = (k - 1) * d + 1
+        pad = ((p - 1) // 2, p // 2)
+        ref = conv1d(x, w, None, s, d, pad)
+    packed = N.pack_conv_weight(w, c_in, c_out, k, s, d, transposed)
+    got = _emulate_packed_conv(packed, x, c_in, c_out, k, s, d, pad, transposed)
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() < 1e-9 * max(1, np.abs(ref).max()) * 1e4
+
+
+def test_validation_errors():
+    a = N.ConvArgs()
+    with pytest.raises(ValueError):
+        N.check(N.lib.rave_conv1d(C.byref(a), None), "conv1d")
+    with pytest.raises(ValueError):
+        N.pack_conv_weight(np.zeros((4, 4, 3), np.float32), 4, 4, 3, 2, 1, 1)  # transposed needs k == 2s
+
+
+def test_plan_create_and_relocation_bounds():
+    ops = (N.PlanOp * 1)()
+    ops[0].kind = N.OP_FILL
+    good = (N.Reloc * 1)(N.Reloc(0, N.FillArgs.y.offset, 0, 0, 0))
+    h = C.c_void_p()
+    N.check(N.lib.rave_plan_create(ops, 1, good, 1, C.byref(h)), "plan_create")
+    assert N.lib.rave_plan_size(h) == 1
+    # unbound slot is reported before anything is launched
+    with pytest.raises(ValueError):
+        N.check(N.lib.rave_plan_run(h, None, 0, None), "plan_run")
+    N.lib.rave_plan_destroy(h)
+    bad = (N.Reloc * 1)(N.Reloc(0, 4, 0, 0, 0))   # misaligned pointer field
+    with pytest.raises(ValueError):
+        N.check(N.lib.rave_plan_create(ops, 1, bad, 1, C.byref(h)), "plan_create")
