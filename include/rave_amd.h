@@ -90,9 +90,14 @@ typedef struct rave_conv1d_args {
     const float* weight;  /* packed by rave_conv1d_pack_weight                   */
     const float* bias;    /* c_out floats or NULL                                */
     const float* alpha;   /* c_in Snake alphas (act == RAVE_ACT_SNAKE)           */
+    float* partial;       /* split-K slab of rave_conv1d_workspace() floats, or
+                             NULL (then the layer runs unsplit)                 */
 } rave_conv1d_args;
 
-/* input channels per K-chunk the kernels use for a layer shape */
+/* Supported layer families (every RAVE conv): kernel 1/3/7 stride 1, kernel 4
+ * stride 2, kernel 8 stride 4, dilation <= 16 on 3-tap convs, and transposed
+ * kernel 2r stride r.  Others return RAVE_ERR_UNSUPPORTED.
+ * input channels per K-chunk the kernels use for a layer shape */
 int rave_conv1d_chunk(int c_in, int kernel, int stride, int dilation, int transposed);
 /* floats of the packed weight of a layer */
 int64_t rave_conv1d_packed_size(int c_in, int c_out, int kernel, int stride, int dilation,
@@ -101,6 +106,8 @@ int64_t rave_conv1d_packed_size(int c_in, int c_out, int kernel, int stride, int
  * ConvTranspose1d: (c_in, c_out, k)) into the kernel's K-chunked layout. */
 int rave_conv1d_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
                             int dilation, int transposed, float* packed);
+/* floats of split-K workspace the launcher would use for these args (0 = none) */
+int64_t rave_conv1d_workspace(const rave_conv1d_args* a);
 int rave_conv1d(const rave_conv1d_args* a, void* stream);
 
 /* ---------------------------------------------------------------- PQMF

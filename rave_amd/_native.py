@@ -40,7 +40,7 @@ class ConvArgs(C.Structure):
                 ("x", vp), ("x_sb", i64), ("x_sc", i64),
                 ("y", vp), ("y_sb", i64), ("y_sc", i64),
                 ("residual", vp), ("r_sb", i64), ("r_sc", i64),
-                ("weight", vp), ("bias", vp), ("alpha", vp)]
+                ("weight", vp), ("bias", vp), ("alpha", vp), ("partial", vp)]
 
 
 class AnalysisArgs(C.Structure):
@@ -104,6 +104,7 @@ STRUCTS = [ConvArgs, AnalysisArgs, SynthesisArgs, FillArgs, RvqArgs, ShiftArgs, 
 EXPORTS = [
     "rave_last_error", "rave_abi_version", "rave_struct_sizes",
     "rave_conv1d_chunk", "rave_conv1d_packed_size", "rave_conv1d_pack_weight", "rave_conv1d",
+    "rave_conv1d_workspace",
     "rave_pqmf_analysis", "rave_pqmf_synthesis", "rave_fill_channels", "rave_copy",
     "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history",
     "rave_plan_create", "rave_plan_run", "rave_plan_destroy", "rave_plan_size",
@@ -128,6 +129,8 @@ def _load():
     lib.rave_conv1d_packed_size.argtypes = [C.c_int] * 6
     lib.rave_conv1d_packed_size.restype = i64
     lib.rave_conv1d_pack_weight.argtypes = [vp] + [C.c_int] * 6 + [vp]
+    lib.rave_conv1d_workspace.argtypes = [C.POINTER(ConvArgs)]
+    lib.rave_conv1d_workspace.restype = i64
     for name, st in [("rave_conv1d", ConvArgs), ("rave_pqmf_analysis", AnalysisArgs),
                      ("rave_pqmf_synthesis", SynthesisArgs), ("rave_fill_channels", FillArgs),
                      ("rave_rvq_encode", RvqArgs), ("rave_rvq_decode", RvqArgs),

@@ -7,20 +7,23 @@
 // module that precedes each conv (LeakyReLU(.2) / Snake) and the Residual add
 // (rave/blocks.py:44-46).
 //
-// GEMM view: Y[m, n] = sum_kk W[m, kk] * X[kk, n] with kk = (ci, tap).
-//  * The K dimension is walked in chunks of CI_T input channels x all taps.
-//  * For each chunk the workgroup stages (a) the weight tile [BK][BM] (packed on
-//    the host so every row is BM contiguous floats) and (b) the input window of
-//    the dilated receptive field: CI_T rows x ((BN-1)*s + (k-1)*d + 1) columns,
-//    read once from HBM (coalesced along time), activation applied, stored in
-//    polyphase order (phase = column mod stride) so the strided B-fragment
-//    reads of one tap are consecutive in LDS (conflict-free ds_read_b32).
-//  * Each tap's B operand is a shifted view of the same LDS window: the halo is
-//    fetched once, not k times.
-//  * 4 waves per workgroup (2x2); each wave owns (BM/2)x(BN/2) of 32x32 MFMA
-//    tiles; exact fp32 (the MFMA is a k-ordered fmaf chain).
-//  * Global loads of chunk c+1 are issued into registers before the MFMAs of
-//    chunk c (register-staged software pipeline).
+// GEMM view: Y[m, n] = sum_kk W[m, kk] * X[kk, n] with kk = (tap, ci).
+//  * K is walked in chunks of CIT input channels x all KT taps (compile-time
+//    per layer family, so the MFMA loop over a chunk is fully unrolled and the
+//    LDS fragment reads use immediate offsets).
+//  * Per chunk the workgroup stages (a) the weight tile [BK][BM] (host-packed:
+//    each row is BM contiguous floats) and (b) the input window of the dilated
+//    receptive field, CIT rows x ((BN-1)*ST + (KT-1)*d + 1) columns, read once
+//    from HBM coalesced along time, activation applied, stored in polyphase
+//    order (phase = column mod stride) so a tap's strided B-fragment reads are
+//    consecutive in LDS.  Every tap reads a shifted view of that one window:
+//    the dilated halo is fetched once, not KT times.
+//  * 4 waves (2x2), each (BM/2)x(BN/2) of 32x32 MFMA tiles; exact fp32 (the
+//    MFMA is a k-ordered fmaf chain).  Global loads of chunk c+1 are issued
+//    into registers before the MFMAs of chunk c.
+//  * Split-K over grid.z for tall-K / short-N layers: each split writes an fp32
+//    partial slab, a second kernel sums the slabs in fixed order (bitwise
+//    deterministic, no atomics) and applies bias / residual / interleave.
 //
 // ConvTranspose1d(C, C', 2r, stride r) runs in polyphase form: the r output
 // phases of input position u are rows m = co*r + q of a 2-tap conv over the
@@ -29,250 +32,485 @@
 
 #include <algorithm>
 #include <cstring>
-#include <vector>
 
 namespace rave {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));   // native vector (HIP float4 is a struct: memcpy -> scratch)
+typedef float f32x4 __attribute__((ext_vector_type(4)));   // native vector (HIP float4 is a struct)
 
 constexpr int kThreads = 256;
-constexpr int kMaxBK = 64;        // taps * CI_T per chunk
-constexpr int kXMax = 5120;       // floats of the staged input window per chunk
-constexpr int kXRegs = kXMax / kThreads;   // 20
-constexpr int kXSlack = kXMax + 1536;     // floats reserved for Xs (covers unconditional stores)
+constexpr int kMaxDil = 16;       // largest dilation of a 3-tap conv the kernels stage
 
 struct ConvKArgs {
     const float* x; const float* w; const float* bias; const float* alpha; const float* res;
-    float* y;
+    float* y; float* partial;
     int64_t x_sb, x_sc, y_sb, y_sc, r_sb, r_sc;
-    int c_in, M, taps, s, log2s, d, pad_l, t_in, U;
-    int ci_t, nchunks, Mpad, XW, XWs, XR;
+    int c_in, M, d, pad_l, t_in, U, B;
+    int nchunks, Mpad, XW;
+    unsigned xw_magic;            // ceil(2^24 / XW): e / XW == (e * magic) >> 24 for e < 2^13
+    int x_bytes, w_bytes;         // buffer-descriptor extents (per batch item / whole packed weight)
+    int y_bytes, r_bytes, bias_rows;
+    int S, cps;                   // splits, chunks per split
     int transposed, R, out_shift, t_y, act;
     float slope;
 };
 
-// --------------------------------------------------------------------- host helpers
-static int ilog2(int v) { int l = 0; while ((1 << l) < v) ++l; return l; }
+// Layer families: (taps, stride, chunk channels).  Every RAVE conv is one of
+// these: k=1 (1x1), k=2 (ConvTranspose polyphase), k=3 (dilated / io),
+// k=4 s=2 (down r=2, noise), k=7 (io), k=8 s=4 (down r=4).
+template <int KT> struct Family;
+template <> struct Family<1> { static constexpr int ST = 1, CIT = 32, DMAX = 1; };
+template <> struct Family<2> { static constexpr int ST = 1, CIT = 32, DMAX = 1; };
+template <> struct Family<3> { static constexpr int ST = 1, CIT = 16, DMAX = kMaxDil; };
+template <> struct Family<4> { static constexpr int ST = 2, CIT = 16, DMAX = 1; };
+template <> struct Family<7> { static constexpr int ST = 1, CIT = 8, DMAX = 1; };
+template <> struct Family<8> { static constexpr int ST = 4, CIT = 8, DMAX = 1; };
 
-// Window length (columns) of the staged input for a BN-column output tile.
-static int window_len(int bn, int s, int taps, int d) { return (bn - 1) * s + (taps - 1) * d + 1; }
+template <int KT, int BN> struct Geo {
+    static constexpr int ST = Family<KT>::ST, CIT = Family<KT>::CIT;
+    static constexpr int BK = KT * CIT;
+    static constexpr int XW_MAX = (BN - 1) * ST + (KT - 1) * Family<KT>::DMAX + 1;
+    static constexpr int XWS = (XW_MAX + ST - 1) / ST;       // per-phase row length
+    static constexpr int XR = XWS * ST;                        // LDS row stride (floats)
+    static constexpr int XREGS = (CIT * XW_MAX + kThreads - 1) / kThreads;
+    // rows reachable by the unconditional staging stores (the window is at
+    // least XW_MIN columns, dilation 1)
+    static constexpr int XW_MIN = (BN - 1) * ST + (KT - 1) + 1;
+    static constexpr int XS_FLOATS = ((XREGS * kThreads - 1) / XW_MIN + 1) * XR;
+};
 
-static int row_stride(int bn, int s, int taps, int d) {
-    int xw = window_len(bn, s, taps, d);
-    int xws = ceil_div(xw, s);
-    return xws * s;
+// Buffer descriptor from wave-uniform inputs (guide T8/T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, int bytes) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const uint64_t u = ((uint64_t)hi << 32) | lo;
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(u), (short)0,
+                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-int chunk_channels(int c_in, int taps, int s, int d) {
-    // largest even CI_T (prefer divisors of c_in) with taps*CI_T <= 64 and the
-    // staged window (at BN = 128) within kXMax floats
-    int xr = row_stride(128, s, taps, d);
-    int best = 0, best_div = 0;
-    int cmax = std::min(kMaxBK / taps, kXMax / xr);
-    int cin_even = (c_in + 1) & ~1;
-    for (int c = 2; c <= cmax && c <= cin_even; c += 2) {
-        best = c;
-        if (cin_even % c == 0) best_div = c;
+// --------------------------------------------------------------------- epilogue
+__device__ __forceinline__ void store_out(const ConvKArgs& a, int b, int m, int n, float v) {
+    if (a.transposed) {
+        const int co = m / a.R;
+        const int q = m - co * a.R;
+        const int t = n * a.R + q - a.out_shift;
+        if (t < 0 || t >= a.t_y) return;
+        if (a.bias) v += a.bias[co];
+        a.y[(int64_t)b * a.y_sb + (int64_t)co * a.y_sc + t] = v;
+    } else {
+        if (a.bias) v += a.bias[m];
+        if (a.res) v += a.res[(int64_t)b * a.r_sb + (int64_t)m * a.r_sc + n];
+        a.y[(int64_t)b * a.y_sb + (int64_t)m * a.y_sc + n] = v;
     }
-    if (best == 0) return 0;
-    // a divisor within 2x of the max is better than padding the last chunk
-    if (best_div * 2 >= best) return best_div;
-    return best;
 }
 
 // --------------------------------------------------------------------- kernel
-template <int BM, int BN>
+// WG = 4 waves.  Each wave owns a 64x64 output tile (2x2 MFMA 32x32 tiles, four
+// independent accumulator chains: 256 MFMA cycles per K-step hide the LDS
+// fragment latency).  The WG tile is (BM/64) x (BN/64) wave tiles; the
+// KS = 4 / (#wave tiles) wave groups split the K-steps of every chunk and are
+// summed through LDS at the end.  LDS is double-buffered: chunk c+1 is staged
+// into the other buffer while chunk c is multiplied (one barrier per chunk).
+template <int BM, int BN, int KT, bool SNAKE>
 __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
-    constexpr int WM = BM / 2, WN = BN / 2;
-    constexpr int TM = WM / 32, TN = WN / 32;
-    constexpr int NA4 = kMaxBK * BM / 4 / kThreads;   // float4 staging regs for A
+    using G = Geo<KT, BN>;
+    constexpr int ST = G::ST, CIT = G::CIT, BK = G::BK, XR = G::XR, XWS = G::XWS;
+    constexpr int WGM = BM / 64, WGN = BN / 64, NWT = WGM * WGN, KS = 4 / NWT;
+    static_assert(NWT * KS == 4, "tile must hold 1, 2 or 4 wave tiles");
+    constexpr int A4 = BK * BM / 4;                        // float4s of one weight chunk
+    constexpr int NA4 = (A4 + kThreads - 1) / kThreads;
+    constexpr int AROWS = NA4 * kThreads * 4 / BM;         // >= BK (slack rows)
+    constexpr int XREGS = G::XREGS;
+    constexpr int BUF = AROWS * BM + G::XS_FLOATS;         // floats per LDS buffer
+    constexpr int HALF = CIT / 2;
+    constexpr int NSTEP = KT * HALF;
 
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int BK = a.ci_t * a.taps;
-    float* As = smem;                 // [BK][BM] (kMaxBK rows reserved)
-    float* Xs = smem + kMaxBK * BM;   // [CI_T][XR] polyphase (kXSlack floats reserved)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int wm0 = (wave >> 1) * WM;
-    const int wn0 = (wave & 1) * WN;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform (scalar branches)
+    const int wt = wave % NWT;          // wave tile
+    const int kg = wave / NWT;          // K group
+    const int wm0 = (wt / WGN) * 64;
+    const int wn0 = (wt % WGN) * 64;
     const int h = lane >> 5;
     const int l32 = lane & 31;
 
     const int n0 = blockIdx.x * BN;
     const int m0 = blockIdx.y * BM;
-    const int b = blockIdx.z;
-    const int in0 = n0 * a.s - a.pad_l;
+    const int b = __builtin_amdgcn_readfirstlane(blockIdx.z / a.S);
+    const int split = __builtin_amdgcn_readfirstlane(blockIdx.z - b * a.S);
+    const int c_begin = split * a.cps;
+    const int c_end = min(a.nchunks, c_begin + a.cps);
+    const int in0 = n0 * ST - a.pad_l;
+    const int XW = a.XW;
+    const int x_elems = CIT * XW;
+    // buffer descriptors: 32-bit voffsets instead of 64-bit addresses per load
+    // (inputs readfirstlane'd so the compiler can PROVE the descriptor uniform;
+    // otherwise every buffer op becomes a waterfall loop)
+    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, a.w_bytes);
+    const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;   // none: v * 1
 
-    const float* xb = a.x + (int64_t)b * a.x_sb;
-
-    floatx16 acc[TM][TN];
+    floatx16 acc[2][2];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const int a_elems4 = BK * BM / 4;
-    const int x_elems = a.ci_t * a.XW;
-
     f32x4 ra[NA4];
-    float rx[kXRegs];
+    float rx[XREGS];
 
+    // Global -> registers.  Unconditional loads from clamped valid addresses,
+    // validity as a select (a load under a per-element branch makes hipcc wait
+    // vmcnt(0) per element); e / XW by a magic multiply, no branches.
     auto load_chunk = [&](int c) __attribute__((always_inline)) {
-        const f32x4* wsrc = reinterpret_cast<const f32x4*>(a.w + (int64_t)c * BK * a.Mpad + m0);
-        // Every load is unconditional from a clamped, valid address; validity is
-        // a select afterwards.  (A load under a per-element branch makes hipcc
-        // wait vmcnt(0) per element and spill the staging array to scratch.)
+        const unsigned wbase = (unsigned)(((unsigned)c * BK * a.Mpad + m0) * 4u);
 #pragma unroll
         for (int i = 0; i < NA4; ++i) {
-            int e = min(tid + i * kThreads, a_elems4 - 1);
-            int row = e / (BM / 4);
-            int col4 = e - row * (BM / 4);
-            ra[i] = wsrc[(int64_t)row * (a.Mpad / 4) + col4];
+            const int e = min(tid + i * kThreads, A4 - 1);
+            const int row = e / (BM / 4);
+            const int col4 = e - row * (BM / 4);
+            ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                wrs, wbase + (unsigned)(row * a.Mpad + col4 * 4) * 4u, 0, 0));
         }
-        const int ci0 = c * a.ci_t;
-        int ci = tid / a.XW;
-        int w = tid - ci * a.XW;
+        const int ci0 = c * CIT;
 #pragma unroll
-        for (int i = 0; i < kXRegs; ++i) {
-            int e = tid + i * kThreads;
-            int cg = ci0 + ci;
-            int t = in0 + w;
-            bool ok = (e < x_elems) && (cg < a.c_in) && (t >= 0) && (t < a.t_in);
-            int cgc = min(cg, a.c_in - 1);
-            int tc = min(max(t, 0), a.t_in - 1);
-            float v = xb[(int64_t)cgc * a.x_sc + tc];
+        for (int i = 0; i < XREGS; ++i) {
+            const int e = tid + i * kThreads;
+            const int ci = (int)(((unsigned)e * a.xw_magic) >> 24);
+            const int w = e - ci * XW;
+            const int cg = ci0 + ci;
+            const int t = in0 + w;
+            const bool ok = (e < x_elems) && (cg < a.c_in) && (t >= 0) && (t < a.t_in);
+            const int cgc = min(cg, a.c_in - 1);
+            const int tc = min(max(t, 0), a.t_in - 1);
+            const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                xrs, (unsigned)(cgc * a.x_sc + tc) * 4u, 0, 0));
             rx[i] = ok ? v : 0.f;
-            w += kThreads;   // XW >= 64, so at most four wraps per step
-            if (w >= a.XW) { w -= a.XW; ++ci; }
-            if (w >= a.XW) { w -= a.XW; ++ci; }
-            if (w >= a.XW) { w -= a.XW; ++ci; }
-            if (w >= a.XW) { w -= a.XW; ++ci; }
         }
     };
 
-    auto store_chunk = [&](int c) __attribute__((always_inline)) {
-        // Unconditional stores: rows past the chunk land in LDS slack (As has
-        // kMaxBK rows, Xs kXSlack floats), so no per-element branches.
+    // Registers -> LDS buffer, activation applied once per staged element.
+    // Stores are unconditional: entries past the chunk land in buffer slack.
+    auto store_chunk = [&](int c, float* buf) __attribute__((always_inline)) {
+        float* As = buf;
+        float* Xs = buf + AROWS * BM;
 #pragma unroll
         for (int i = 0; i < NA4; ++i) {
-            int e = tid + i * kThreads;
-            int row = e / (BM / 4);
-            int col4 = e - row * (BM / 4);
+            const int e = tid + i * kThreads;
+            const int row = e / (BM / 4);
+            const int col4 = e - row * (BM / 4);
             *reinterpret_cast<f32x4*>(As + row * BM + col4 * 4) = ra[i];
         }
-        const int ci0 = c * a.ci_t;
-        int ci = tid / a.XW;
-        int w = tid - ci * a.XW;
+        const int ci0 = c * CIT;
 #pragma unroll
-        for (int i = 0; i < kXRegs; ++i) {
-            {
-                int cg = min(ci0 + ci, a.c_in - 1);
-                float al = (a.act == RAVE_ACT_SNAKE) ? a.alpha[cg] : 0.f;
-                float v = apply_act(rx[i], a.act, a.slope, al);
-                int ph = w & (a.s - 1);
-                int wq = w >> a.log2s;
-                Xs[ci * a.XR + ph * a.XWs + wq] = v;
+        for (int i = 0; i < XREGS; ++i) {
+            const int e = tid + i * kThreads;
+            const int ci = (int)(((unsigned)e * a.xw_magic) >> 24);
+            const int w = e - ci * XW;
+            float v = rx[i];
+            if constexpr (SNAKE) {
+                const float al = a.alpha[min(ci0 + ci, a.c_in - 1)];
+                v = v + (1.0f / (al + 1e-9f)) * sin_squared(al * v);
+            } else {
+                v = v > 0.f ? v : v * slope;
             }
-            w += kThreads;   // XW >= 64, so at most four wraps per step
-            if (w >= a.XW) { w -= a.XW; ++ci; }
-            if (w >= a.XW) { w -= a.XW; ++ci; }
-            if (w >= a.XW) { w -= a.XW; ++ci; }
-            if (w >= a.XW) { w -= a.XW; ++ci; }
+            Xs[ci * XR + (w % ST) * XWS + w / ST] = v;
         }
     };
 
-    load_chunk(0);
-    for (int c = 0; c < a.nchunks; ++c) {
-        __syncthreads();
-        store_chunk(c);
-        __syncthreads();
-        load_chunk(min(c + 1, a.nchunks - 1));   // unconditional (redundant reload on the last chunk)
+    // per-lane LDS offsets of the B fragments of each tap (row h of the pair)
+    int xoff[KT];
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+        const int p = (wn0 + l32) * ST + j * a.d;
+        xoff[j] = h * XR + (p % ST) * XWS + p / ST;
+    }
+    const int aoff = h * BM + wm0 + l32;
 
-        const int half = a.ci_t >> 1;
-        for (int j = 0; j < a.taps; ++j) {
-            const float* Aj = As + (j * a.ci_t + h) * BM + wm0 + l32;
-            int p = (wn0 + l32) * a.s + j * a.d;
-            const float* Xj = Xs + h * a.XR + (p & (a.s - 1)) * a.XWs + (p >> a.log2s);
-#pragma unroll 2
-            for (int c2 = 0; c2 < half; ++c2) {
-                float av[TM], bv[TN];
-#pragma unroll
-                for (int i = 0; i < TM; ++i) av[i] = Aj[c2 * 2 * BM + i * 32];
-#pragma unroll
-                for (int i = 0; i < TN; ++i) bv[i] = Xj[c2 * 2 * a.XR + i * 32];
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int jj = 0; jj < TN; ++jj)
-                        acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[jj], acc[i][jj], 0, 0, 0);
-            }
+    load_chunk(c_begin);
+    store_chunk(c_begin, smem);
+    if (c_begin + 1 < c_end) load_chunk(c_begin + 1);
+    __syncthreads();
+
+    for (int c = c_begin; c < c_end; ++c) {
+        const int cur = (c - c_begin) & 1;
+        float* bcur = smem + cur * BUF;
+        if (c + 1 < c_end) {
+            store_chunk(c + 1, smem + (cur ^ 1) * BUF);   // overlaps the MFMAs below
+            if (c + 2 < c_end) load_chunk(c + 2);
         }
+        const float* As = bcur;
+        const float* Xs = bcur + AROWS * BM;
+#pragma unroll
+        for (int st = 0; st < NSTEP; ++st) {
+            if constexpr (KS > 1) {
+                if (st % KS != kg) continue;        // K-steps of this wave's group
+            }
+            const int j = st / HALF, c2 = st - (st / HALF) * HALF;
+            float fa[2], fb[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) fa[i] = As[aoff + (j * CIT + 2 * c2) * BM + i * 32];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) fb[i] = Xs[xoff[j] + c2 * 2 * XR + i * 32];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj)
+                    acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
+        }
+        __syncthreads();
     }
 
     // ---------------------------------------------------------------- epilogue
-    float* yb = a.y + (int64_t)b * a.y_sb;
-    const float* rb = a.res ? a.res + (int64_t)b * a.r_sb : nullptr;
+    // With KS > 1 every wave parks its partial 64x64 tile in LDS and then
+    // finishes the 32x32 sub-tiles q with q % KS == kg (sum over K groups in
+    // group order).  Stores/loads are branch-free buffer ops: invalid elements
+    // (tile edges, transposed interleave) get offset 0xFFFFFFFF, which the range
+    // check drops (stores) or reads as 0 (loads).
+    constexpr unsigned kOOB = 0xFFFFFFFFu;
+    float* red = smem;   // staging buffers are dead after the last barrier
+    if constexpr (KS > 1) {
+        float* dst = red + (kg * NWT + wt) * 4096;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int jj = 0; jj < TN; ++jj) {
-            const int n = n0 + wn0 + jj * 32 + l32;
-            if (n >= a.U) continue;
+            for (int r = 0; r < 16; ++r) dst[(q * 16 + r) * 64 + lane] = acc[q >> 1][q & 1][r];
+        __syncthreads();
+    }
+    const bool partial = a.S > 1;
+    const __amdgpu_buffer_rsrc_t prs = make_rsrc(
+        partial ? a.partial + ((int64_t)split * a.B + b) * (int64_t)a.M * a.U : a.y,
+        partial ? a.M * a.U * 4 : 0);
+    const __amdgpu_buffer_rsrc_t yrs = make_rsrc(a.y + (int64_t)b * a.y_sb, partial ? 0 : a.y_bytes);
+    const __amdgpu_buffer_rsrc_t brs = make_rsrc(a.bias ? a.bias : a.y, (a.bias && !partial) ? a.bias_rows * 4 : 0);
+    const __amdgpu_buffer_rsrc_t rrs = make_rsrc(
+        a.res ? a.res + (int64_t)b * a.r_sb : a.y, (a.res && !partial) ? a.r_bytes : 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if constexpr (KS > 1) {
+            if (q % KS != kg) continue;            // uniform
+        }
+        const int i = q >> 1, jj = q & 1;
+        const int n = n0 + wn0 + jj * 32 + l32;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if constexpr (KS > 1) {
+                float sum = 0.f;
+#pragma unroll
+                for (int g = 0; g < KS; ++g) sum += red[((g * NWT + wt) * 4096) + (q * 16 + r) * 64 + lane];
+                v[r] = sum;
+            } else {
+                v[r] = acc[i][jj][r];
+            }
+        }
+        if (partial) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m >= a.M) continue;
-                float v = acc[i][jj][r];
-                if (a.transposed) {
-                    const int co = m / a.R;
-                    const int q = m - co * a.R;
-                    const int t = n * a.R + q - a.out_shift;
-                    if (t < 0 || t >= a.t_y) continue;
-                    if (a.bias) v += a.bias[co];
-                    yb[(int64_t)co * a.y_sc + t] = v;
-                } else {
-                    if (a.bias) v += a.bias[m];
-                    if (rb) v += rb[(int64_t)m * a.r_sc + n];
-                    yb[(int64_t)m * a.y_sc + n] = v;
-                }
+                const unsigned off = (m < a.M && n < a.U) ? (unsigned)(m * a.U + n) * 4u : kOOB;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), prs, off, 0, 0);
             }
+            continue;
+        }
+        float bv[16], rv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int brow = a.transposed ? m / a.R : m;
+            bv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, (unsigned)brow * 4u, 0, 0));
+            const unsigned roff = (m < a.M && n < a.U) ? (unsigned)(m * a.r_sc + n) * 4u : kOOB;
+            rv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rrs, roff, 0, 0));
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            unsigned off;
+            if (a.transposed) {
+                const int co = m / a.R;
+                const int t = n * a.R + (m - co * a.R) - a.out_shift;
+                off = (m < a.M && n < a.U && t >= 0 && t < a.t_y) ? (unsigned)(co * a.y_sc + t) * 4u : kOOB;
+            } else {
+                off = (m < a.M && n < a.U) ? (unsigned)(m * a.y_sc + n) * 4u : kOOB;
+            }
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r] + bv[r] + rv[r]),
+                                                  yrs, off, 0, 0);
         }
     }
 }
 
-// --------------------------------------------------------------------- launch
-struct TileCfg { int bm, bn; };
-
-static TileCfg pick_tile(int M, int U, int B) {
-    const TileCfg cands[4] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
-    for (const auto& c : cands) {
-        int64_t wg = (int64_t)ceil_div(M, c.bm) * ceil_div(U, c.bn) * B;
-        double waste = double(ceil_div(M, c.bm) * c.bm) * double(ceil_div(U, c.bn) * c.bn) /
-                       (double(M) * double(U));
-        if (wg >= 512 && waste <= 1.15) return c;
+// Sum the split-K slabs in split order, then the normal epilogue.
+__global__ __launch_bounds__(256) void conv1d_splitk_reduce_kernel(ConvKArgs a) {
+    const int64_t per_b = (int64_t)a.M * a.U;
+    const int64_t total = per_b * a.B;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        float v = 0.f;
+        for (int s = 0; s < a.S; ++s) v += a.partial[(int64_t)s * total + i];
+        const int b = (int)(i / per_b);
+        const int64_t r = i - (int64_t)b * per_b;
+        const int m = (int)(r / a.U);
+        const int n = (int)(r - (int64_t)m * a.U);
+        store_out(a, b, m, n, v);
     }
-    // not enough work for two workgroups per CU: smallest tile
-    return cands[3];
 }
 
-template <int BM, int BN>
-static int launch_tile(ConvKArgs k, int B, hipStream_t st) {
-    k.XW = window_len(BN, k.s, k.taps, k.d);
-    k.XWs = ceil_div(k.XW, k.s);
-    k.XR = k.XWs * k.s;
-    if (k.ci_t * k.XW > kXMax || k.ci_t * k.XR > kXMax + 64 * 4) {
-        set_error("conv1d: staged window exceeds LDS budget");
+// --------------------------------------------------------------------- host side
+static int family_cit(int taps) {
+    switch (taps) {
+        case 1: return Family<1>::CIT;
+        case 2: return Family<2>::CIT;
+        case 3: return Family<3>::CIT;
+        case 4: return Family<4>::CIT;
+        case 7: return Family<7>::CIT;
+        case 8: return Family<8>::CIT;
+        default: return 0;
+    }
+}
+static int family_stride(int taps) {
+    switch (taps) {
+        case 4: return 2;
+        case 8: return 4;
+        default: return 1;
+    }
+}
+
+struct LaunchCfg {
+    int bm, bn, S;
+};
+
+static double pad_waste(int M, int U, int bm, int bn) {
+    return double(ceil_div(M, bm) * bm) * double(ceil_div(U, bn) * bn) / (double(M) * double(U));
+}
+
+// Tile + split-K choice.  Prefer the largest tile (fewest K-groups) that gives
+// >= 2 workgroups per CU with little padding; otherwise the least-padding tile
+// with K split across workgroups until ~2 workgroups per CU.
+static LaunchCfg choose(int M, int U, int B, int nchunks) {
+    const int cand[5][2] = {{128, 128}, {64, 256}, {128, 64}, {64, 128}, {64, 64}};
+    for (auto& c : cand) {
+        int64_t wg = (int64_t)ceil_div(M, c[0]) * ceil_div(U, c[1]) * B;
+        if (wg >= 512 && pad_waste(M, U, c[0], c[1]) <= 1.12) return {c[0], c[1], 1};
+    }
+    LaunchCfg best{64, 64, 1};
+    double bw = 1e30;
+    for (auto& c : cand) {
+        double score = pad_waste(M, U, c[0], c[1]) * (c[0] * c[1] == 4096 ? 1.06 : 1.0);
+        if (score < bw) { bw = score; best = {c[0], c[1], 1}; }
+    }
+    int64_t wg = (int64_t)ceil_div(M, best.bm) * ceil_div(U, best.bn) * B;
+    int S = (int)std::min<int64_t>(16, ceil_div64(512, wg));
+    S = std::min(S, std::max(1, nchunks / 2));
+    best.S = std::max(1, S);
+    return best;
+}
+
+template <int BM, int BN, int KT>
+static int launch_k(ConvKArgs k, hipStream_t st) {
+    using G = Geo<KT, BN>;
+    constexpr int A4 = G::BK * BM / 4;
+    constexpr int NA4 = (A4 + kThreads - 1) / kThreads;
+    constexpr int AROWS = NA4 * kThreads * 4 / BM;
+    constexpr int BUF = AROWS * BM + G::XS_FLOATS;
+    constexpr int NWT = (BM / 64) * (BN / 64);
+    constexpr int RED = (NWT < 4) ? 4 * 64 * 64 : 0;        // K-group reduction area
+    if (k.XW > G::XW_MAX) {
+        set_error("conv1d: dilation too large for the staged window");
         return RAVE_ERR_UNSUPPORTED;
     }
-    size_t lds = (size_t)(kMaxBK * BM + kXSlack) * sizeof(float);
-    dim3 grid(ceil_div(k.U, BN), ceil_div(k.M, BM), B);
-    hipLaunchKernelGGL((conv1d_mfma_kernel<BM, BN>), grid, dim3(kThreads), lds, st, k);
+    const size_t lds = (size_t)std::max(2 * BUF, RED) * sizeof(float);
+    static_assert((size_t)std::max(2 * BUF, RED) * sizeof(float) <= 160 * 1024, "LDS budget");
+    dim3 grid(ceil_div(k.U, BN), ceil_div(k.M, BM), k.B * k.S);
+    auto kern = (k.act == RAVE_ACT_SNAKE) ? conv1d_mfma_kernel<BM, BN, KT, true>
+                                           : conv1d_mfma_kernel<BM, BN, KT, false>;
+    if (lds > 64 * 1024) {
+        // opt in to more than 64 KiB of dynamic LDS (once per instantiation)
+        static bool done[2] = {false, false};
+        bool& d = done[k.act == RAVE_ACT_SNAKE];
+        if (!d) {
+            RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            d = true;
+        }
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, st, k);
     return launch_status("conv1d_mfma_kernel");
+}
+
+template <int KT>
+static int launch_family(ConvKArgs k, const LaunchCfg& c, hipStream_t st) {
+    k.XW = (c.bn - 1) * Family<KT>::ST + (KT - 1) * k.d + 1;
+    k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
+    if (c.bm == 128 && c.bn == 128) return launch_k<128, 128, KT>(k, st);
+    if (c.bm == 64 && c.bn == 256) return launch_k<64, 256, KT>(k, st);
+    if (c.bm == 128 && c.bn == 64) return launch_k<128, 64, KT>(k, st);
+    if (c.bm == 64 && c.bn == 128) return launch_k<64, 128, KT>(k, st);
+    return launch_k<64, 64, KT>(k, st);
+}
+
+// Fill ConvKArgs from the public args; returns status and the tap count.
+static int prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
+    RAVE_CHECK_ARG(a.x && a.y && a.weight, "conv1d: null tensor");
+    RAVE_CHECK_ARG(a.batch > 0 && a.t_in > 0 && a.t_out > 0 && a.c_in > 0 && a.c_out > 0,
+                   "conv1d: empty shape");
+    RAVE_CHECK_ARG(a.act != RAVE_ACT_SNAKE || a.alpha, "conv1d: snake needs alpha");
+    RAVE_CHECK_ARG(a.pad_left >= 0 && a.pad_right >= 0, "conv1d: negative padding");
+    k = ConvKArgs{};
+    k.x = a.x; k.w = a.weight; k.bias = a.bias; k.alpha = a.alpha; k.res = a.residual; k.y = a.y;
+    k.x_sb = a.x_sb; k.x_sc = a.x_sc; k.y_sb = a.y_sb; k.y_sc = a.y_sc; k.r_sb = a.r_sb; k.r_sc = a.r_sc;
+    k.c_in = a.c_in; k.B = a.batch;
+    k.act = a.act; k.slope = a.leaky_slope;
+    k.pad_l = a.pad_left; k.t_in = a.t_in; k.t_y = a.t_out;
+    if (a.transposed) {
+        RAVE_CHECK_ARG(a.kernel == 2 * a.stride, "conv1d: transposed needs kernel == 2*stride");
+        RAVE_CHECK_ARG(a.residual == nullptr, "conv1d: residual unsupported on transposed conv");
+        k.transposed = 1; k.R = a.stride; k.out_shift = a.out_shift;
+        taps = 2; k.d = 1;
+        k.M = a.c_out * a.stride;
+        k.U = a.t_in + a.pad_left + a.pad_right - 1;
+        RAVE_CHECK_ARG(k.U > 0, "conv1d: empty transposed output");
+        RAVE_CHECK_ARG((int64_t)(k.U - 1) * k.R + (k.R - 1) - k.out_shift >= (int64_t)a.t_out - 1,
+                       "conv1d: transposed t_out exceeds computed range");
+    } else {
+        taps = a.kernel;
+        if (family_cit(taps) == 0 || family_stride(taps) != a.stride) {
+            set_error("conv1d: unsupported (kernel, stride) pair; supported: k1/k3/k7 s1, k4 s2, k8 s4");
+            return RAVE_ERR_UNSUPPORTED;
+        }
+        RAVE_CHECK_ARG(a.dilation == 1 || taps == 3, "conv1d: dilation only on 3-tap convs");
+        RAVE_CHECK_ARG(a.dilation >= 1 && a.dilation <= kMaxDil, "conv1d: dilation out of range");
+        k.transposed = 0; k.R = 1; k.out_shift = 0;
+        k.d = a.dilation;
+        k.M = a.c_out;
+        int span = (a.kernel - 1) * a.dilation + 1;
+        int expect = (a.t_in + a.pad_left + a.pad_right - span) / a.stride + 1;
+        RAVE_CHECK_ARG(expect == a.t_out, "conv1d: t_out does not match the conv arithmetic");
+        k.U = a.t_out;
+    }
+    k.nchunks = ceil_div(a.c_in, family_cit(taps));
+    k.Mpad = ceil_div(k.M, 128) * 128;
+    {
+        const int64_t xb = ((int64_t)(a.c_in - 1) * a.x_sc + a.t_in) * 4;
+        const int64_t wb = (int64_t)k.nchunks * family_cit(taps) * taps * k.Mpad * 4;
+        RAVE_CHECK_ARG(xb < (1ll << 31) && wb < (1ll << 31) && a.x_sc >= 0,
+                       "conv1d: tensors beyond 2 GiB per batch item need 64-bit offsets");
+        k.x_bytes = (int)xb;
+        k.w_bytes = (int)wb;
+        const int y_rows = a.c_out;
+        const int64_t yb = ((int64_t)(y_rows - 1) * a.y_sc + a.t_out) * 4;
+        const int64_t rb = a.residual ? ((int64_t)(a.c_out - 1) * a.r_sc + a.t_out) * 4 : 0;
+        RAVE_CHECK_ARG(yb < (1ll << 31) && rb < (1ll << 31), "conv1d: output beyond 2 GiB per batch item");
+        k.y_bytes = (int)yb;
+        k.r_bytes = (int)rb;
+        k.bias_rows = a.c_out;
+    }
+    return RAVE_OK;
 }
 
 }  // namespace rave
@@ -280,10 +518,10 @@ static int launch_tile(ConvKArgs k, int B, hipStream_t st) {
 using namespace rave;
 
 extern "C" int rave_conv1d_chunk(int c_in, int kernel, int stride, int dilation, int transposed) {
-    int taps = transposed ? 2 : kernel;
-    int s = transposed ? 1 : stride;
-    int d = transposed ? 1 : dilation;
-    return chunk_channels(c_in, taps, s, d);
+    (void)c_in; (void)dilation;
+    if (transposed) return kernel == 2 * stride ? family_cit(2) : 0;
+    if (family_cit(kernel) == 0 || family_stride(kernel) != stride) return 0;
+    return family_cit(kernel);
 }
 
 extern "C" int64_t rave_conv1d_packed_size(int c_in, int c_out, int kernel, int stride, int dilation,
@@ -334,49 +572,40 @@ extern "C" int rave_conv1d_pack_weight(const float* w, int c_in, int c_out, int 
     return RAVE_OK;
 }
 
+extern "C" int64_t rave_conv1d_workspace(const rave_conv1d_args* p) {
+    if (!p) return -1;
+    ConvKArgs k;
+    int taps;
+    if (prepare(*p, k, taps) != RAVE_OK) return -1;
+    LaunchCfg c = choose(k.M, k.U, k.B, k.nchunks);
+    if (c.S <= 1) return 0;
+    return (int64_t)c.S * k.B * (int64_t)k.M * k.U;
+}
+
 extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
     RAVE_CHECK_ARG(p, "conv1d: null args");
-    const rave_conv1d_args& a = *p;
-    RAVE_CHECK_ARG(a.x && a.y && a.weight, "conv1d: null tensor");
-    RAVE_CHECK_ARG(a.batch > 0 && a.t_in > 0 && a.t_out > 0 && a.c_in > 0 && a.c_out > 0,
-                   "conv1d: empty shape");
-    RAVE_CHECK_ARG(a.act != RAVE_ACT_SNAKE || a.alpha, "conv1d: snake needs alpha");
-    RAVE_CHECK_ARG(a.pad_left >= 0 && a.pad_right >= 0, "conv1d: negative padding");
-    ConvKArgs k{};
-    k.x = a.x; k.w = a.weight; k.bias = a.bias; k.alpha = a.alpha; k.res = a.residual; k.y = a.y;
-    k.x_sb = a.x_sb; k.x_sc = a.x_sc; k.y_sb = a.y_sb; k.y_sc = a.y_sc; k.r_sb = a.r_sb; k.r_sc = a.r_sc;
-    k.c_in = a.c_in;
-    k.act = a.act; k.slope = a.leaky_slope;
-    k.pad_l = a.pad_left; k.t_in = a.t_in; k.t_y = a.t_out;
-    if (a.transposed) {
-        RAVE_CHECK_ARG(a.kernel == 2 * a.stride, "conv1d: transposed needs kernel == 2*stride");
-        RAVE_CHECK_ARG(a.residual == nullptr, "conv1d: residual unsupported on transposed conv");
-        k.transposed = 1; k.R = a.stride; k.out_shift = a.out_shift;
-        k.taps = 2; k.s = 1; k.log2s = 0; k.d = 1;
-        k.M = a.c_out * a.stride;
-        k.U = a.t_in + a.pad_left + a.pad_right - 1;
-        RAVE_CHECK_ARG(k.U > 0, "conv1d: empty transposed output");
-        RAVE_CHECK_ARG((int64_t)(k.U - 1) * k.R + (k.R - 1) - k.out_shift >= (int64_t)a.t_out - 1,
-                       "conv1d: transposed t_out exceeds computed range");
-    } else {
-        RAVE_CHECK_ARG((a.stride & (a.stride - 1)) == 0, "conv1d: stride must be a power of two");
-        k.transposed = 0; k.R = 1; k.out_shift = 0;
-        k.taps = a.kernel; k.s = a.stride; k.log2s = ilog2(a.stride); k.d = a.dilation;
-        k.M = a.c_out;
-        int span = (a.kernel - 1) * a.dilation + 1;
-        int expect = (a.t_in + a.pad_left + a.pad_right - span) / a.stride + 1;
-        RAVE_CHECK_ARG(expect == a.t_out, "conv1d: t_out does not match the conv arithmetic");
-        k.U = a.t_out;
-    }
-    k.ci_t = rave_conv1d_chunk(a.c_in, a.kernel, a.stride, a.dilation, a.transposed);
-    RAVE_CHECK_ARG(k.ci_t > 0, "conv1d: unsupported layer shape");
-    k.nchunks = ceil_div(a.c_in, k.ci_t);
-    k.Mpad = ceil_div(k.M, 128) * 128;
-
+    ConvKArgs k;
+    int taps;
+    int rc = prepare(*p, k, taps);
+    if (rc != RAVE_OK) return rc;
+    LaunchCfg c = choose(k.M, k.U, k.B, k.nchunks);
+    if (c.S > 1 && p->partial == nullptr) c.S = 1;   // no workspace given: single pass
+    k.cps = ceil_div(k.nchunks, c.S);
+    k.S = ceil_div(k.nchunks, k.cps);                 // no empty splits
+    k.partial = p->partial;
     hipStream_t st = as_stream(stream);
-    TileCfg t = pick_tile(k.M, k.U, a.batch);
-    if (t.bm == 128 && t.bn == 128) return launch_tile<128, 128>(k, a.batch, st);
-    if (t.bm == 64 && t.bn == 128) return launch_tile<64, 128>(k, a.batch, st);
-    if (t.bm == 128 && t.bn == 64) return launch_tile<128, 64>(k, a.batch, st);
-    return launch_tile<64, 64>(k, a.batch, st);
+    switch (taps) {
+        case 1: rc = launch_family<1>(k, c, st); break;
+        case 2: rc = launch_family<2>(k, c, st); break;
+        case 3: rc = launch_family<3>(k, c, st); break;
+        case 4: rc = launch_family<4>(k, c, st); break;
+        case 7: rc = launch_family<7>(k, c, st); break;
+        case 8: rc = launch_family<8>(k, c, st); break;
+        default: set_error("conv1d: unsupported kernel size"); return RAVE_ERR_UNSUPPORTED;
+    }
+    if (rc != RAVE_OK || k.S <= 1) return rc;
+    int64_t total = (int64_t)k.B * k.M * k.U;
+    int blocks = (int)std::min<int64_t>(ceil_div64(total, 256), 4096);
+    hipLaunchKernelGGL(conv1d_splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, k);
+    return launch_status("conv1d_splitk_reduce_kernel");
 }

@@ -17,48 +17,58 @@
 
 namespace rave {
 
-constexpr int kAnaT = 256;     // output frames per workgroup (one per thread)
+constexpr int kAnaT = 128;     // output frames per workgroup (one per thread)
 constexpr int kSynT = 64;      // frames per workgroup
+constexpr int kFrameStride = 20;   // LDS floats per 16-sample frame (16 + 4 pad: conflict-free b128)
 
-__global__ __launch_bounds__(256) void pqmf_analysis_kernel(rave_pqmf_analysis_args a, int xws) {
-    extern __shared__ __attribute__((aligned(16))) float xs[];   // [n_band][xws]
-    const int nb = a.n_band;
+// Analysis (16 bands): window stored frame-major [frame][20] so one ds_read_b128
+// returns 4 consecutive taps of a thread's frame (lane stride 20 dwords keeps a
+// 16-lane group on 64 distinct banks); the filter [band][taps rounded to 4] is
+// read as wave-uniform float4 broadcasts.  NBO (bands produced) is compile-time
+// so the accumulators stay in registers.
+template <int NBO>
+__global__ __launch_bounds__(kAnaT) void pqmf_analysis_kernel(rave_pqmf_analysis_args a, int taps4,
+                                                              int wframes) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* hs = smem;                                  // [NBO][taps4]
+    float* xs = smem + NBO * taps4;                    // [wframes][kFrameStride]
     const int t0 = blockIdx.x * kAnaT;
     const int b = blockIdx.y;
     const float* xb = a.x + (int64_t)b * a.x_sb;
-    const int in0 = t0 * nb - a.pad_left;
-    const int xw = (kAnaT - 1) * nb + a.taps;
-    for (int i = threadIdx.x; i < xw; i += blockDim.x) {
-        int t = in0 + i;
-        float v = (t >= 0 && t < a.t_in) ? xb[t] : 0.f;
-        xs[(i % nb) * xws + i / nb] = v;
+    for (int i = threadIdx.x; i < NBO * taps4; i += kAnaT) {
+        const int k = i / taps4, j = i - k * taps4;
+        hs[i] = j < a.taps ? a.hkf[(int64_t)k * a.taps + j] : 0.f;
+    }
+    const int in0 = t0 * 16 - a.pad_left;
+    for (int i = threadIdx.x; i < wframes * 16; i += kAnaT) {
+        const int t = in0 + i;
+        const float v = (t >= 0 && t < a.t_in) ? xb[t] : 0.f;
+        xs[(i >> 4) * kFrameStride + (i & 15)] = v;
     }
     __syncthreads();
     const int tl = threadIdx.x;
-    const int t = t0 + tl;
-    float acc[16];
+    float acc[NBO];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) acc[k] = 0.f;
-    const int nbo = a.n_out_bands;
-    for (int j0 = 0; j0 < a.taps; j0 += nb) {
-        const int jn = min(nb, a.taps - j0);
-        for (int p = 0; p < jn; ++p) {
-            const float xv = xs[p * xws + tl + j0 / nb];
-            const float* hcol = a.hkf + j0 + p;
+    for (int k = 0; k < NBO; ++k) acc[k] = 0.f;
+    for (int j = 0; j < taps4; j += 4) {
+        const float4 xv = *reinterpret_cast<const float4*>(xs + (tl + (j >> 4)) * kFrameStride + (j & 15));
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (k < nbo) acc[k] = fmaf(hcol[(int64_t)k * a.taps], xv, acc[k]);
+        for (int k = 0; k < NBO; ++k) {
+            const float4 hv = *reinterpret_cast<const float4*>(hs + k * taps4 + j);
+            acc[k] = fmaf(hv.x, xv.x, acc[k]);
+            acc[k] = fmaf(hv.y, xv.y, acc[k]);
+            acc[k] = fmaf(hv.z, xv.z, acc[k]);
+            acc[k] = fmaf(hv.w, xv.w, acc[k]);
         }
     }
+    const int t = t0 + tl;
     if (t >= a.t_out) return;
     float* yb = a.y + (int64_t)b * a.y_sb;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if (k < nbo) {
-            float v = acc[k];
-            if ((k & 1) && !(t & 1)) v = -v;   // reverse_half
-            yb[(int64_t)k * a.y_sc + t] = v;
-        }
+    for (int k = 0; k < NBO; ++k) {
+        float v = acc[k];
+        if ((k & 1) && !(t & 1)) v = -v;   // reverse_half
+        yb[(int64_t)k * a.y_sc + t] = v;
     }
 }
 
@@ -127,15 +137,19 @@ using namespace rave;
 extern "C" int rave_pqmf_analysis(const rave_pqmf_analysis_args* p, void* stream) {
     RAVE_CHECK_ARG(p && p->x && p->y && p->hkf, "pqmf_analysis: null pointer");
     const rave_pqmf_analysis_args& a = *p;
-    RAVE_CHECK_ARG(a.n_band > 0 && a.n_band <= 16 && a.n_out_bands > 0 && a.n_out_bands <= a.n_band,
-                   "pqmf_analysis: n_band must be in [1, 16]");
-    RAVE_CHECK_ARG(a.taps > 0 && a.taps <= 2048, "pqmf_analysis: bad taps");
+    RAVE_CHECK_ARG(a.n_band == 16, "pqmf_analysis: kernel is built for 16 bands");
+    RAVE_CHECK_ARG(a.n_out_bands == 6 || a.n_out_bands == 16,
+                   "pqmf_analysis: n_out_bands must be 6 (RAVE.encode) or 16");
+    RAVE_CHECK_ARG(a.taps > 0 && a.taps <= 1024, "pqmf_analysis: bad taps");
     RAVE_CHECK_ARG(a.batch > 0 && a.t_in > 0 && a.t_out > 0, "pqmf_analysis: empty shape");
-    int xw = (kAnaT - 1) * a.n_band + a.taps;
-    int xws = ceil_div(xw, a.n_band) + 1;
-    size_t lds = (size_t)a.n_band * xws * sizeof(float);
+    const int taps4 = (a.taps + 3) & ~3;
+    const int wframes = kAnaT + taps4 / 16 + 1;
+    size_t lds = (size_t)(a.n_out_bands * taps4 + wframes * kFrameStride) * sizeof(float);
     dim3 grid(ceil_div(a.t_out, kAnaT), a.batch);
-    hipLaunchKernelGGL(pqmf_analysis_kernel, grid, dim3(256), lds, as_stream(stream), a, xws);
+    if (a.n_out_bands == 6)
+        hipLaunchKernelGGL(pqmf_analysis_kernel<6>, grid, dim3(kAnaT), lds, as_stream(stream), a, taps4, wframes);
+    else
+        hipLaunchKernelGGL(pqmf_analysis_kernel<16>, grid, dim3(kAnaT), lds, as_stream(stream), a, taps4, wframes);
     return launch_status("pqmf_analysis_kernel");
 }
 

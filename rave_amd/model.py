@@ -108,17 +108,40 @@ class Workspace:
         self.free = merged
 
 
+def splitk_floats(scalars: dict, has_res: bool = False) -> int:
+    """Split-K slab floats the native launcher wants for a conv (0 = unsplit)."""
+    a = N.ConvArgs(**scalars)
+    a.x = a.y = a.weight = 16          # placeholders: only shapes are inspected
+    a.residual = 16 if has_res else None
+    n = int(N.lib.rave_conv1d_workspace(C.byref(a)))
+    if n < 0:
+        N.check(N.RAVE_ERR_ARG, "conv1d_workspace")
+    return n
+
+
 class Plan:
     """Symbolic op list -> native rave_plan with relocations for I/O slots."""
 
     def __init__(self, arena: Arena):
         self.arena = arena
         self.ws = Workspace()
+        self.splitk_off = -1
         self.sym: List[Tuple[int, type, dict, dict]] = []
         self.labels: List[str] = []
         self.flops: List[float] = []
         self.handle = None
         self.ws_tensor: Optional[torch.Tensor] = None
+        self._splitk: List[View] = []
+        self.splitk_max = 0
+
+    def splitk_view(self, floats: int) -> Optional[View]:
+        """One shared split-K slab (dead after each conv's reduce), sized at
+        finalize time to the largest request."""
+        if floats <= 0:
+            return None
+        self.splitk_max = max(self.splitk_max, floats)
+        v = View("splitk", 0, 0, 0)
+        return v
 
     def add(self, kind: int, st: type, scalars: dict, ptrs: Dict[str, Optional[View]],
             label: str = "", flops: float = 0.0):
@@ -130,6 +153,11 @@ class Plan:
         self.flops.append(float(flops))
 
     def finalize(self, device) -> "Plan":
+        # The slab is live at different points of the plan than any tensor, so it
+        # must not come from the free list (regions free at the END of planning
+        # are in use mid-plan): bump-allocate past everything.
+        splitk_off = self.splitk_off = self.ws.top
+        self.ws.top += ((self.splitk_max + Workspace.ALIGN - 1) // Workspace.ALIGN) * Workspace.ALIGN
         self.ws_tensor = torch.empty(max(self.ws.top, 1), dtype=torch.float32, device=device)
         n = len(self.sym)
         ops = (N.PlanOp * max(n, 1))()
@@ -144,6 +172,8 @@ class Plan:
                     continue
                 if view.slot == "ws":
                     setattr(args, field, self.ws_tensor.data_ptr() + view.elem * view.off)
+                elif view.slot == "splitk":
+                    setattr(args, field, self.ws_tensor.data_ptr() + 4 * splitk_off)
                 elif view.slot == "arena":
                     setattr(args, field, self.arena.ptr(view.off))
                 else:
@@ -243,6 +273,7 @@ class RAVE:
         ptrs = dict(x=src, y=dst, residual=res, weight=View("arena", wo, 0, 0),
                     bias=View("arena", bo, 0, 0) if bo is not None else None,
                     alpha=View("arena", ao, 0, 0) if ao is not None else None)
+        ptrs["partial"] = plan.splitk_view(splitk_floats(s, res is not None))
         if n.transposed:
             flops = 2.0 * B * n.c_out * t_out * n.c_in * 2          # 2 taps per output sample
         else:

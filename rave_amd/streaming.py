@@ -32,7 +32,7 @@ import torch
 from . import _native as N
 from .config import get_padding
 from .graph import ConvNode
-from .model import RAVE, Plan, View
+from .model import RAVE, Plan, View, splitk_floats
 
 
 def _need(n: ConvNode) -> int:
@@ -100,6 +100,7 @@ class StreamingRAVE:
         ptrs = dict(x=x, y=y, residual=res, weight=View("arena", wo, 0, 0),
                     bias=View("arena", bo, 0, 0) if bo is not None else None,
                     alpha=View("arena", ao, 0, 0) if ao is not None else None)
+        ptrs["partial"] = plan.splitk_view(splitk_floats(s, res is not None))
         plan.add(N.OP_CONV, N.ConvArgs, s, ptrs, label=n.name)
 
     def _shift_all(self, plan: Plan, bufs) -> None:

@@ -57,7 +57,7 @@ CONV_CASES = [
 ]
 
 
-def run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act):
+def run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act, split=True):
     B, _, T = x.shape
     packed = torch.from_numpy(N.pack_conv_weight(w, c_in, c_out, k, s, d, transposed)).to(dev)
     xd = torch.from_numpy(x).to(dev)
@@ -77,13 +77,21 @@ def run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed,
                    residual=rd.data_ptr() if rd is not None else None, r_sb=c_out * t_out, r_sc=t_out,
                    weight=packed.data_ptr(), bias=bd.data_ptr() if bd is not None else None,
                    alpha=ad.data_ptr() if ad is not None else None)
+    ws = None
+    if split:
+        nws = N.lib.rave_conv1d_workspace(C.byref(a))
+        assert nws >= 0
+        if nws > 0:
+            ws = torch.full((nws,), float("nan"), device=dev)
+            a.partial = ws.data_ptr()
     N.check(N.lib.rave_conv1d(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream)), "conv1d")
     torch.cuda.synchronize()
     return y.cpu().numpy()
 
 
+@pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("case", CONV_CASES, ids=[str(c[:8]) for c in CONV_CASES])
-def test_conv_layer(N, dev, case):
+def test_conv_layer(N, dev, case, split):
     from oracle.rave_oracle import conv1d, conv_transpose1d, leaky_relu, snake
     c_in, c_out, k, s, d, transposed, act, has_res, B, T = case
     rng = np.random.default_rng(hash(case) & 0xFFFF)
@@ -111,7 +119,7 @@ def test_conv_layer(N, dev, case):
     if has_res:
         ref = ref + res
     got = run_conv(N, dev, x, w, b, alpha.reshape(-1) if alpha is not None else None, res,
-                   c_in, c_out, k, s, d, pad, transposed, act)
+                   c_in, c_out, k, s, d, pad, transposed, act, split)
     assert np.isfinite(got).all()
     assert maxabs(got, ref) <= 2e-5 * max(1.0, np.abs(ref).max())
 

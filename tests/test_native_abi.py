@@ -96,8 +96,16 @@ def test_validation_errors():
     a = N.ConvArgs()
     with pytest.raises(ValueError):
         N.check(N.lib.rave_conv1d(C.byref(a), None), "conv1d")
-    with pytest.raises(ValueError):
+    with pytest.raises(NotImplementedError):
         N.pack_conv_weight(np.zeros((4, 4, 3), np.float32), 4, 4, 3, 2, 1, 1)  # transposed needs k == 2s
+    with pytest.raises(NotImplementedError):
+        N.pack_conv_weight(np.zeros((4, 4, 5), np.float32), 4, 4, 5, 1, 1, 0)  # no 5-tap family
+    # workspace query validates like the launcher
+    a = N.ConvArgs(c_in=64, c_out=64, kernel=3, stride=1, dilation=1, pad_left=1, pad_right=1,
+                   batch=1, t_in=100, t_out=99, x=16, y=16, weight=16)
+    assert N.lib.rave_conv1d_workspace(C.byref(a)) == -1   # t_out inconsistent
+    a.t_out = 100
+    assert N.lib.rave_conv1d_workspace(C.byref(a)) >= 0
 
 
 def test_plan_create_and_relocation_bounds():
@@ -114,3 +122,22 @@ def test_plan_create_and_relocation_bounds():
     bad = (N.Reloc * 1)(N.Reloc(0, 4, 0, 0, 0))   # misaligned pointer field
     with pytest.raises(ValueError):
         N.check(N.lib.rave_plan_create(ops, 1, bad, 1, C.byref(h)), "plan_create")
+
+
+def test_workspace_splitk_slab_disjoint():
+    """The split-K slab never aliases a planned tensor (regression: it was
+    taken from the end-of-plan free list, which overlaps mid-plan tensors)."""
+    from rave_amd.model import Plan
+
+    class _Arena:
+        def ptr(self, off):
+            return 4096 + 4 * off
+    p = Plan(_Arena())
+    a = p.ws.alloc(1000)
+    b = p.ws.alloc(3000)
+    p.ws.release(a, 1000)          # free at the end of planning, live mid-plan
+    p.ws.release(b, 3000)
+    p.splitk_view(500)
+    p.add(N.OP_FILL, N.FillArgs, dict(batch=1, channels=1, t_len=1), dict(y=None, values=None))
+    p.finalize("cpu")
+    assert p.splitk_off >= b + 3000
