@@ -104,17 +104,11 @@ def main():
     B, T = a.batch, a.samples
     Fz = T // cfg.hop
     x = torch.from_numpy(synth_batch(B, T, 1000 * rank)).to(dev)
-    zc = cfg.latent_size + cfg.speaker_size
-    z_all = torch.empty(world * B, zc, Fz, device=dev)
+    from rave_amd.distributed import ShardedRunner
+    runner = ShardedRunner(model)          # encode -> RCCL all-gather of latents -> decode
 
     def step():
-        z = model.encode(x)
-        if world > 1:
-            dist.all_gather_into_tensor(z_all, z)     # RCCL over xGMI
-            zl = z_all[rank * B:(rank + 1) * B]
-        else:
-            zl = z
-        return model.decode(zl)
+        return runner.step(x)[1]
 
     for _ in range(a.warmup):
         step()
