@@ -66,12 +66,15 @@ int rave_struct_sizes(int64_t* out, int n);
  * tensor; batch and channel strides are free, so views into larger buffers
  * (concatenations, streaming history) need no copies.
  *
- * transposed = 1: nn.ConvTranspose1d(c_in, c_out, 2r, stride=r) executed in
- * polyphase form: a 2-tap conv over the input producing r phases per input
- * position u, written to y[b, co, u*r + q - out_shift] (kept when inside
- * [0, t_out)).  Offline (padding r//2): pad_left = pad_right = 1,
- * out_shift = r//2, t_out = t_in*r.  Cached streaming: the input view carries
- * one history column, pad 0, out_shift 0.
+ * transposed = 1: nn.ConvTranspose1d(c_in, c_out, 2r, stride=r) in polyphase
+ * form.  Output t = u*r + q (u in [0, t_in - pad_left)) for every phase q is a
+ * 2-tap conv of the input: with P = out_shift, phases q < r-P read (x[u-1],
+ * x[u]) and phases q >= r-P read (x[u], x[u+1]); the two phase groups are
+ * separate row blocks of one GEMM, so no output column is wasted.
+ *   offline (torch padding r//2): pad_left = 0, out_shift = r/2, t_out = t_in*r
+ *   cached streaming (overlap-add cache): the input view starts with one history
+ *   column, pad_left = 1, out_shift = 0, t_out = (t_in - 1)*r
+ * pad_right is ignored; the weight must be packed with the same out_shift.
  */
 typedef struct rave_conv1d_args {
     int32_t c_in, c_out, kernel, stride, dilation;
@@ -92,6 +95,8 @@ typedef struct rave_conv1d_args {
     const float* alpha;   /* c_in Snake alphas (act == RAVE_ACT_SNAKE)           */
     float* partial;       /* split-K slab of rave_conv1d_workspace() floats, or
                              NULL (then the layer runs unsplit)                 */
+    unsigned long long* stamps;   /* diagnostic builds only (-DRAVE_STAMPS): 8 clock
+                                     stamps per workgroup; ignored otherwise      */
 } rave_conv1d_args;
 
 /* Supported layer families (every RAVE conv): kernel 1/3/7 stride 1, kernel 4
@@ -105,7 +110,7 @@ int64_t rave_conv1d_packed_size(int c_in, int c_out, int kernel, int stride, int
 /* Host-side repack of a folded torch-layout weight (Conv1d: (c_out, c_in, k);
  * ConvTranspose1d: (c_in, c_out, k)) into the kernel's K-chunked layout. */
 int rave_conv1d_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
-                            int dilation, int transposed, float* packed);
+                            int dilation, int transposed, int out_shift, float* packed);
 /* floats of split-K workspace the launcher would use for these args (0 = none) */
 int64_t rave_conv1d_workspace(const rave_conv1d_args* a);
 int rave_conv1d(const rave_conv1d_args* a, void* stream);

@@ -11,6 +11,10 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librave_amd.so")
+# Kernel-tuning hook only: tools/ may point this at the -DRAVE_STAMPS diagnostic
+# build (rave_amd/librave_amd_diag.so).  The product always loads LIB_PATH.
+if os.environ.get("RAVE_AMD_DIAG_LIB") == "1":
+    LIB_PATH = os.path.join(_HERE, "librave_amd_diag.so")
 
 RAVE_OK = 0
 RAVE_ERR_ARG = -1
@@ -40,7 +44,7 @@ class ConvArgs(C.Structure):
                 ("x", vp), ("x_sb", i64), ("x_sc", i64),
                 ("y", vp), ("y_sb", i64), ("y_sc", i64),
                 ("residual", vp), ("r_sb", i64), ("r_sc", i64),
-                ("weight", vp), ("bias", vp), ("alpha", vp), ("partial", vp)]
+                ("weight", vp), ("bias", vp), ("alpha", vp), ("partial", vp), ("stamps", vp)]
 
 
 class AnalysisArgs(C.Structure):
@@ -128,7 +132,7 @@ def _load():
     lib.rave_conv1d_chunk.argtypes = [C.c_int] * 5
     lib.rave_conv1d_packed_size.argtypes = [C.c_int] * 6
     lib.rave_conv1d_packed_size.restype = i64
-    lib.rave_conv1d_pack_weight.argtypes = [vp] + [C.c_int] * 6 + [vp]
+    lib.rave_conv1d_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
     lib.rave_conv1d_workspace.argtypes = [C.POINTER(ConvArgs)]
     lib.rave_conv1d_workspace.restype = i64
     for name, st in [("rave_conv1d", ConvArgs), ("rave_pqmf_analysis", AnalysisArgs),
@@ -175,8 +179,12 @@ def conv_chunk(c_in, kernel, stride, dilation, transposed) -> int:
     return int(lib.rave_conv1d_chunk(c_in, kernel, stride, dilation, int(transposed)))
 
 
-def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed):
-    """Host repack (numpy float32, torch layout) -> packed numpy float32."""
+def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift=None):
+    """Host repack (numpy float32, torch layout) -> packed numpy float32.
+    ``out_shift`` (ConvTranspose only): stride//2 for torch padding r//2 (default),
+    0 for the cached streaming form."""
+    if out_shift is None:
+        out_shift = stride // 2 if transposed else 0
     import numpy as np
     w = np.ascontiguousarray(w, dtype=np.float32)
     n = int(lib.rave_conv1d_packed_size(c_in, c_out, kernel, stride, dilation, int(transposed)))
@@ -184,7 +192,7 @@ def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed):
         raise NotImplementedError(f"unsupported conv shape c_in={c_in} k={kernel} s={stride} d={dilation}")
     out = np.empty(n, np.float32)
     check(lib.rave_conv1d_pack_weight(w.ctypes.data, c_in, c_out, kernel, stride, dilation,
-                                      int(transposed), out.ctypes.data), "pack_weight")
+                                      int(transposed), int(out_shift), out.ctypes.data), "pack_weight")
     return out
 
 

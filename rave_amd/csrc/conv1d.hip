@@ -50,8 +50,13 @@ struct ConvKArgs {
     unsigned xw_magic;            // ceil(2^24 / XW): e / XW == (e * magic) >> 24 for e < 2^13
     int x_bytes, w_bytes;         // buffer-descriptor extents (per batch item / whole packed weight)
     int y_bytes, r_bytes, bias_rows;
+#ifdef RAVE_STAMPS
+    unsigned long long* stamps;   // diagnostic build only: 8 per workgroup
+#endif
     int S, cps;                   // splits, chunks per split
     int transposed, R, out_shift, t_y, act;
+    int split_row, pad_g1, q0;    // ConvT phase groups: rows < split_row use pad_l, others pad_g1;
+                                  // q0 = phases in group 0 (= R - out_shift)
     float slope;
 };
 
@@ -90,12 +95,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, int 
 }
 
 // --------------------------------------------------------------------- epilogue
+// ConvT row m -> (output channel, phase).  Rows [0, split_row) hold phases
+// [0, q0) of every channel, rows [split_row, M) phases [q0, R).
+__device__ __forceinline__ void convt_row(const ConvKArgs& a, int m, int& co, int& q) {
+    if (m < a.split_row) {
+        co = m / a.q0;
+        q = m - co * a.q0;
+    } else {
+        const int mm = m - a.split_row, p = a.R - a.q0;
+        co = mm / p;
+        q = a.q0 + (mm - co * p);
+    }
+}
+
 __device__ __forceinline__ void store_out(const ConvKArgs& a, int b, int m, int n, float v) {
     if (a.transposed) {
-        const int co = m / a.R;
-        const int q = m - co * a.R;
-        const int t = n * a.R + q - a.out_shift;
-        if (t < 0 || t >= a.t_y) return;
+        int co, q;
+        convt_row(a, m, co, q);
+        const int t = n * a.R + q;
+        if (t >= a.t_y) return;
         if (a.bias) v += a.bias[co];
         a.y[(int64_t)b * a.y_sb + (int64_t)co * a.y_sc + t] = v;
     } else {
@@ -129,6 +147,16 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
 
     const int tid = threadIdx.x;
+#ifdef RAVE_STAMPS
+    const int wg_lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    auto stamp = [&](int k) {
+        if (tid == 0) {
+            a.stamps[wg_lin * 8 + k] = __builtin_amdgcn_s_memtime();
+            if (k == 0) a.stamps[wg_lin * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+        }
+    };
+    stamp(0);
+#endif
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform (scalar branches)
     const int wt = wave % NWT;          // wave tile
@@ -144,7 +172,7 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
     const int split = __builtin_amdgcn_readfirstlane(blockIdx.z - b * a.S);
     const int c_begin = split * a.cps;
     const int c_end = min(a.nchunks, c_begin + a.cps);
-    const int in0 = n0 * ST - a.pad_l;
+    const int in0 = n0 * ST - ((m0 < a.split_row) ? a.pad_l : a.pad_g1);   // ConvT phase groups
     const int XW = a.XW;
     const int x_elems = CIT * XW;
     // buffer descriptors: 32-bit voffsets instead of 64-bit addresses per load
@@ -237,6 +265,9 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
     store_chunk(c_begin, smem);
     if (c_begin + 1 < c_end) load_chunk(c_begin + 1);
     __syncthreads();
+#ifdef RAVE_STAMPS
+    stamp(1);
+#endif
 
     for (int c = c_begin; c < c_end; ++c) {
         const int cur = (c - c_begin) & 1;
@@ -274,6 +305,9 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
     // (tile edges, transposed interleave) get offset 0xFFFFFFFF, which the range
     // check drops (stores) or reads as 0 (loads).
     constexpr unsigned kOOB = 0xFFFFFFFFu;
+#ifdef RAVE_STAMPS
+    stamp(2);
+#endif
     float* red = smem;   // staging buffers are dead after the last barrier
     if constexpr (KS > 1) {
         float* dst = red + (kg * NWT + wt) * 4096;
@@ -323,7 +357,11 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int brow = a.transposed ? m / a.R : m;
+            int brow = m;
+            if (a.transposed) {
+                int qq;
+                convt_row(a, m, brow, qq);
+            }
             bv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, (unsigned)brow * 4u, 0, 0));
             const unsigned roff = (m < a.M && n < a.U) ? (unsigned)(m * a.r_sc + n) * 4u : kOOB;
             rv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rrs, roff, 0, 0));
@@ -333,9 +371,10 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
             const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
             unsigned off;
             if (a.transposed) {
-                const int co = m / a.R;
-                const int t = n * a.R + (m - co * a.R) - a.out_shift;
-                off = (m < a.M && n < a.U && t >= 0 && t < a.t_y) ? (unsigned)(co * a.y_sc + t) * 4u : kOOB;
+                int co, q;
+                convt_row(a, m, co, q);
+                const int t = n * a.R + q;
+                off = (m < a.M && n < a.U && t < a.t_y) ? (unsigned)(co * a.y_sc + t) * 4u : kOOB;
             } else {
                 off = (m < a.M && n < a.U) ? (unsigned)(m * a.y_sc + n) * 4u : kOOB;
             }
@@ -343,6 +382,9 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
                                                   yrs, off, 0, 0);
         }
     }
+#ifdef RAVE_STAMPS
+    stamp(3);
+#endif
 }
 
 // Sum the split-K slabs in split order, then the normal epilogue.
@@ -392,15 +434,20 @@ static double pad_waste(int M, int U, int bm, int bn) {
 // Tile + split-K choice.  Prefer the largest tile (fewest K-groups) that gives
 // >= 2 workgroups per CU with little padding; otherwise the least-padding tile
 // with K split across workgroups until ~2 workgroups per CU.
-static LaunchCfg choose(int M, int U, int B, int nchunks) {
-    const int cand[5][2] = {{128, 128}, {64, 256}, {128, 64}, {64, 128}, {64, 64}};
-    for (auto& c : cand) {
+static LaunchCfg choose(int M, int U, int B, int nchunks, int split_row = 1 << 30) {
+    const int all[5][2] = {{128, 128}, {64, 256}, {128, 64}, {64, 128}, {64, 64}};
+    int cand[5][2], nc = 0;
+    for (auto& c : all)   // a tile may not straddle the ConvT phase-group boundary
+        if (split_row >= M || split_row % c[0] == 0) { cand[nc][0] = c[0]; cand[nc][1] = c[1]; ++nc; }
+    for (int ci = 0; ci < nc; ++ci) {
+        const int* c = cand[ci];
         int64_t wg = (int64_t)ceil_div(M, c[0]) * ceil_div(U, c[1]) * B;
         if (wg >= 512 && pad_waste(M, U, c[0], c[1]) <= 1.12) return {c[0], c[1], 1};
     }
     LaunchCfg best{64, 64, 1};
     double bw = 1e30;
-    for (auto& c : cand) {
+    for (int ci = 0; ci < nc; ++ci) {
+        const int* c = cand[ci];
         double score = pad_waste(M, U, c[0], c[1]) * (c[0] * c[1] == 4096 ? 1.06 : 1.0);
         if (score < bw) { bw = score; best = {c[0], c[1], 1}; }
     }
@@ -468,15 +515,22 @@ static int prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
     k.act = a.act; k.slope = a.leaky_slope;
     k.pad_l = a.pad_left; k.t_in = a.t_in; k.t_y = a.t_out;
     if (a.transposed) {
-        RAVE_CHECK_ARG(a.kernel == 2 * a.stride, "conv1d: transposed needs kernel == 2*stride");
+        RAVE_CHECK_ARG(a.kernel == 2 * a.stride && a.stride % 2 == 0,
+                       "conv1d: transposed needs kernel == 2*stride, even stride");
         RAVE_CHECK_ARG(a.residual == nullptr, "conv1d: residual unsupported on transposed conv");
+        RAVE_CHECK_ARG(a.out_shift == 0 || a.out_shift == a.stride / 2,
+                       "conv1d: transposed out_shift must be 0 (cached) or stride/2 (padding r//2)");
+        RAVE_CHECK_ARG(a.pad_left == 0 || a.pad_left == 1, "conv1d: transposed pad_left = history columns (0/1)");
         k.transposed = 1; k.R = a.stride; k.out_shift = a.out_shift;
         taps = 2; k.d = 1;
         k.M = a.c_out * a.stride;
-        k.U = a.t_in + a.pad_left + a.pad_right - 1;
-        RAVE_CHECK_ARG(k.U > 0, "conv1d: empty transposed output");
-        RAVE_CHECK_ARG((int64_t)(k.U - 1) * k.R + (k.R - 1) - k.out_shift >= (int64_t)a.t_out - 1,
-                       "conv1d: transposed t_out exceeds computed range");
+        k.q0 = a.stride - a.out_shift;               // phases whose taps are (u-1, u)
+        k.split_row = a.c_out * k.q0;
+        k.pad_l = 1 - a.pad_left;                    // group 0 window starts at u-1
+        k.pad_g1 = -a.pad_left;                      // group 1 window starts at u
+        k.U = a.t_in - a.pad_left;
+        RAVE_CHECK_ARG(k.U > 0, "conv1d: empty transposed input");
+        RAVE_CHECK_ARG((int64_t)k.U * k.R == a.t_out, "conv1d: transposed t_out must be (t_in - pad_left) * stride");
     } else {
         taps = a.kernel;
         if (family_cit(taps) == 0 || family_stride(taps) != a.stride) {
@@ -486,6 +540,7 @@ static int prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
         RAVE_CHECK_ARG(a.dilation == 1 || taps == 3, "conv1d: dilation only on 3-tap convs");
         RAVE_CHECK_ARG(a.dilation >= 1 && a.dilation <= kMaxDil, "conv1d: dilation out of range");
         k.transposed = 0; k.R = 1; k.out_shift = 0;
+        k.split_row = 1 << 30; k.pad_g1 = a.pad_left; k.q0 = 1;
         k.d = a.dilation;
         k.M = a.c_out;
         int span = (a.kernel - 1) * a.dilation + 1;
@@ -536,16 +591,22 @@ extern "C" int64_t rave_conv1d_packed_size(int c_in, int c_out, int kernel, int 
 }
 
 extern "C" int rave_conv1d_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
-                                       int dilation, int transposed, float* packed) {
+                                       int dilation, int transposed, int out_shift, float* packed) {
     RAVE_CHECK_ARG(w && packed, "pack_weight: null pointer");
     RAVE_CHECK_ARG(c_in > 0 && c_out > 0 && kernel > 0 && stride > 0 && dilation > 0,
                    "pack_weight: bad shape");
-    RAVE_CHECK_ARG(!transposed || kernel == 2 * stride, "pack_weight: transposed needs kernel == 2*stride");
     int ci_t = rave_conv1d_chunk(c_in, kernel, stride, dilation, transposed);
-    RAVE_CHECK_ARG(ci_t > 0, "pack_weight: unsupported layer shape");
+    if (ci_t <= 0) {
+        set_error("pack_weight: unsupported layer shape");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    RAVE_CHECK_ARG(!transposed || out_shift == 0 || out_shift == stride / 2,
+                   "pack_weight: transposed out_shift must be 0 or stride/2");
     int taps = transposed ? 2 : kernel;
     int R = transposed ? stride : 1;
     int M = c_out * R;
+    int q0 = R - (transposed ? out_shift : 0);       // ConvT phases in row group 0
+    int split_row = c_out * q0;
     int64_t Mpad = (int64_t)ceil_div(M, 128) * 128;
     int nchunks = ceil_div(c_in, ci_t);
     int BK = ci_t * taps;
@@ -559,9 +620,15 @@ extern "C" int rave_conv1d_pack_weight(const float* w, int c_in, int c_out, int 
                 for (int m = 0; m < M; ++m) {
                     float v;
                     if (transposed) {
-                        int co = m / R, q = m % R;
-                        // tap 0 multiplies x[u-1] -> kernel index q + r; tap 1 x[u] -> q
-                        int kidx = (j == 0) ? q + R : q;
+                        // output t = u*R + q; with P = out_shift:
+                        //   q <  R-P : y = W[q+P+R] x[u-1] + W[q+P] x[u]     (taps u-1, u)
+                        //   q >= R-P : y = W[q+P]   x[u]   + W[q+P-R] x[u+1] (taps u, u+1)
+                        int co, q;
+                        if (m < split_row) { co = m / q0; q = m % q0; }
+                        else { int p = R - q0; co = (m - split_row) / p; q = q0 + (m - split_row) % p; }
+                        int kidx;
+                        if (q < q0) kidx = (j == 0) ? q + out_shift + R : q + out_shift;
+                        else kidx = (j == 0) ? q + out_shift : q + out_shift - R;
                         v = w[((int64_t)ci * c_out + co) * kernel + kidx];
                     } else {
                         v = w[((int64_t)m * c_in + ci) * kernel + j];
@@ -577,7 +644,7 @@ extern "C" int64_t rave_conv1d_workspace(const rave_conv1d_args* p) {
     ConvKArgs k;
     int taps;
     if (prepare(*p, k, taps) != RAVE_OK) return -1;
-    LaunchCfg c = choose(k.M, k.U, k.B, k.nchunks);
+    LaunchCfg c = choose(k.M, k.U, k.B, k.nchunks, k.split_row);
     if (c.S <= 1) return 0;
     return (int64_t)c.S * k.B * (int64_t)k.M * k.U;
 }
@@ -588,11 +655,14 @@ extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
     int taps;
     int rc = prepare(*p, k, taps);
     if (rc != RAVE_OK) return rc;
-    LaunchCfg c = choose(k.M, k.U, k.B, k.nchunks);
+    LaunchCfg c = choose(k.M, k.U, k.B, k.nchunks, k.split_row);
     if (c.S > 1 && p->partial == nullptr) c.S = 1;   // no workspace given: single pass
     k.cps = ceil_div(k.nchunks, c.S);
     k.S = ceil_div(k.nchunks, k.cps);                 // no empty splits
     k.partial = p->partial;
+#ifdef RAVE_STAMPS
+    k.stamps = p->stamps;
+#endif
     hipStream_t st = as_stream(stream);
     switch (taps) {
         case 1: rc = launch_family<1>(k, c, st); break;

@@ -232,10 +232,14 @@ class RAVE:
             raise ValueError("rave_amd.RAVE runs on the GPU only (device must be cuda)")
         ar = Arena()
         self.w_off: Dict[str, Tuple[int, Optional[int], Optional[int]]] = {}
+        self.w_off_stream: Dict[str, int] = {}
         for n in self.graph.convs():
             w = conv_weight(n, params)
             packed = N.pack_conv_weight(w, n.c_in, n.c_out, n.kernel, n.stride, n.dilation, n.transposed)
             wo = ar.add(packed)
+            if n.transposed:   # cached (streaming) form: overlap-add cache, no r//2 crop
+                self.w_off_stream[n.name] = ar.add(N.pack_conv_weight(
+                    w, n.c_in, n.c_out, n.kernel, n.stride, n.dilation, True, out_shift=0))
             bo = ar.add(params[n.name + ".bias"]) if n.bias else None
             ao = ar.add(params[n.alpha]) if n.act == "snake" else None
             self.w_off[n.name] = (wo, bo, ao)
@@ -267,7 +271,7 @@ class RAVE:
                  x_sb=src.sb, x_sc=src.sc, y_sb=dst.sb, y_sc=dst.sc,
                  r_sb=res.sb if res else 0, r_sc=res.sc if res else 0)
         if n.transposed:
-            s.update(pad_left=1, pad_right=1, transposed=1, out_shift=n.stride // 2)
+            s.update(pad_left=0, pad_right=0, transposed=1, out_shift=n.stride // 2)
         else:
             s.update(pad_left=n.pad[0], pad_right=n.pad[1], transposed=0, out_shift=0)
         ptrs = dict(x=src, y=dst, residual=res, weight=View("arena", wo, 0, 0),

@@ -91,9 +91,12 @@ class StreamingRAVE:
             r, h_r, _ = bufs[n.residual]
             res = View("ws", r.off + h_r, r.sb, r.sc)
         wo, bo, ao = m.w_off[n.name]
+        if n.transposed:
+            wo = m.w_off_stream[n.name]      # packed for the cached form (out_shift 0)
         t_in = need + t_src
         s = dict(c_in=n.c_in, c_out=n.c_out, kernel=n.kernel, stride=n.stride, dilation=n.dilation,
-                 pad_left=0, pad_right=0, transposed=int(n.transposed), out_shift=0,
+                 pad_left=1 if n.transposed else 0, pad_right=0, transposed=int(n.transposed),
+                 out_shift=0,
                  act=N.ACT[n.act], leaky_slope=self.cfg.leaky_slope, batch=self.B, t_in=t_in,
                  t_out=t_dst, x_sb=x.sb, x_sc=x.sc, y_sb=y.sb, y_sc=y.sc,
                  r_sb=res.sb if res else 0, r_sc=res.sc if res else 0)

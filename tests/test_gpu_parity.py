@@ -70,7 +70,7 @@ def run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed,
     ad = torch.from_numpy(alpha).to(dev) if alpha is not None else None
     rd = torch.from_numpy(res).to(dev) if res is not None else None
     a = N.ConvArgs(c_in=c_in, c_out=c_out, kernel=k, stride=s, dilation=d,
-                   pad_left=1 if transposed else pad[0], pad_right=1 if transposed else pad[1],
+                   pad_left=0 if transposed else pad[0], pad_right=0 if transposed else pad[1],
                    transposed=transposed, out_shift=s // 2 if transposed else 0, act=N.ACT[act],
                    leaky_slope=0.2, batch=B, t_in=T, t_out=t_out,
                    x=xd.data_ptr(), x_sb=c_in * T, x_sc=T, y=y.data_ptr(), y_sb=c_out * t_out, y_sc=t_out,

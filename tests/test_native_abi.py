@@ -37,8 +37,10 @@ def test_struct_sizes_match():
     assert C.sizeof(N.PlanOp) == 248
 
 
-def _emulate_packed_conv(packed, x, c_in, c_out, k, s, d, pad, transposed):
-    """Run the GEMM the kernel runs, from the packed layout (kk = j*CI_T + ci)."""
+def _emulate_packed_conv(packed, x, c_in, c_out, k, s, d, pad, transposed, out_shift=None):
+    """Run the GEMM the kernel runs, from the packed layout (kk = tap*CI_T + ci).
+    ConvTranspose: rows [0, split) are phases q < r-P with window offset -1,
+    rows [split, M) phases q >= r-P with offset 0; output t = u*r + q."""
     ci_t = N.conv_chunk(c_in, k, s, d, transposed)
     taps = 2 if transposed else k
     R = s if transposed else 1
@@ -46,33 +48,40 @@ def _emulate_packed_conv(packed, x, c_in, c_out, k, s, d, pad, transposed):
     Mpad = -(-M // 128) * 128
     nch = -(-c_in // ci_t)
     W = packed.reshape(nch, taps, ci_t, Mpad)[..., :M]
-    cs, ds = (1, 1) if transposed else (s, d)
-    pl, pr = (1, 1) if transposed else pad
-    xp = np.pad(x.astype(np.float64), ((0, 0), (0, nch * ci_t - c_in), (pl, pr)))
-    B, _, T = xp.shape
-    U = (T - ((taps - 1) * ds + 1)) // cs + 1
-    y = np.zeros((B, M, U))
-    for c in range(nch):
-        for j in range(taps):
-            xs = xp[:, c * ci_t:(c + 1) * ci_t, j * ds: j * ds + (U - 1) * cs + 1: cs]
-            y += np.einsum("im,bin->bmn", W[c, j], xs)
+    xc = np.pad(x.astype(np.float64), ((0, 0), (0, nch * ci_t - c_in), (0, 0)))
+    B, _, T = x.shape
     if not transposed:
+        xp = np.pad(xc, ((0, 0), (0, 0), pad))
+        U = (xp.shape[-1] - ((taps - 1) * d + 1)) // s + 1
+        y = np.zeros((B, M, U))
+        for c in range(nch):
+            for j in range(taps):
+                xs = xp[:, c * ci_t:(c + 1) * ci_t, j * d: j * d + (U - 1) * s + 1: s]
+                y += np.einsum("im,bin->bmn", W[c, j], xs)
         return y
-    out = np.zeros((B, c_out, x.shape[-1] * R))
-    sh = R // 2
+    P = R // 2 if out_shift is None else out_shift
+    q0 = R - P
+    split = c_out * q0
+    xp = np.pad(xc, ((0, 0), (0, 0), (1, 1)))        # x[-1] and x[T] are zero
+    out = np.zeros((B, c_out, T * R))
     for m in range(M):
-        co, q = divmod(m, R)
-        for u in range(U):
-            t = u * R + q - sh
-            if 0 <= t < out.shape[-1]:
-                out[:, co, t] = y[:, m, u]
+        if m < split:
+            co, q, off = m // q0, m % q0, -1
+        else:
+            co, q, off = (m - split) // (R - q0), q0 + (m - split) % (R - q0), 0
+        acc = np.zeros((B, T))
+        for c in range(nch):
+            for j in range(taps):
+                xs = xp[:, c * ci_t:(c + 1) * ci_t, 1 + off + j: 1 + off + j + T]
+                acc += np.einsum("i,bit->bt", W[c, j, :, m], xs)
+        out[:, co, q::R] = acc
     return out
 
 
 @pytest.mark.parametrize("c_in,c_out,k,s,d,transposed", [
     (64, 64, 3, 1, 9, 0), (64, 64, 1, 1, 1, 0), (6, 64, 7, 1, 1, 0), (64, 128, 8, 4, 1, 0),
     (256, 512, 4, 2, 1, 0), (320, 1024, 3, 1, 1, 0), (64, 32, 7, 1, 1, 0), (96, 96, 3, 1, 3, 0),
-    (1024, 512, 4, 2, 1, 1), (128, 64, 8, 4, 1, 1), (1536, 768, 4, 2, 1, 1)])
+    (64, 48, 4, 2, 1, 1), (32, 16, 8, 4, 1, 1), (96, 40, 4, 2, 1, 1)])
 def test_pack_layout(c_in, c_out, k, s, d, transposed):
     rng = np.random.default_rng(1)
     T = 40
@@ -80,7 +89,7 @@ def test_pack_layout(c_in, c_out, k, s, d, transposed):
     if transposed:
         w = rng.standard_normal((c_in, c_out, k)).astype(np.float32)
         ref = conv_transpose1d(x, w, s, s // 2)
-        pad = (1, 1)
+        pad = (0, 0)
     else:
         w = rng.standard_normal((c_out, c_in, k)).astype(np.float32)
         p = (k - 1) * d + 1
@@ -141,3 +150,17 @@ def test_workspace_splitk_slab_disjoint():
     p.add(N.OP_FILL, N.FillArgs, dict(batch=1, channels=1, t_len=1), dict(y=None, values=None))
     p.finalize("cpu")
     assert p.splitk_off >= b + 3000
+
+
+@pytest.mark.parametrize("c_in,c_out,r", [(64, 32, 2), (32, 16, 4)])
+def test_pack_layout_transposed_cached_form(c_in, c_out, r):
+    """out_shift = 0 (cached_conv's overlap-add form): output = the uncropped
+    transposed conv's first T*r samples (cache = zeros)."""
+    rng = np.random.default_rng(2)
+    T = 20
+    x = rng.standard_normal((2, c_in, T)).astype(np.float32)
+    w = rng.standard_normal((c_in, c_out, 2 * r)).astype(np.float32)
+    ref = conv_transpose1d(x, w, r, 0)[..., :T * r]
+    packed = N.pack_conv_weight(w, c_in, c_out, 2 * r, r, 1, 1, out_shift=0)
+    got = _emulate_packed_conv(packed, x, c_in, c_out, 2 * r, r, 1, (0, 0), 1, out_shift=0)
+    assert np.abs(got - ref).max() < 1e-9 * max(1, np.abs(ref).max()) * 1e4

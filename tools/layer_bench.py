@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Time single conv layers of the v2 graph in isolation (HIP events), for
+kernel tuning and per-layer PMC profiling:
+
+    python tools/layer_bench.py [--layers k3_64,k1_64,...] [--iters 50] [--batch 16]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from rave_amd import _native as N  # noqa: E402
+
+# name: (c_in, c_out, k, s, d, transposed, act, residual, t_in per clip)
+LAYERS = {
+    "k3_64": (64, 64, 3, 1, 9, 0, "leaky", False, 4096),
+    "k1_64": (64, 64, 1, 1, 1, 0, "leaky", True, 4096),
+    "k3_128": (128, 128, 3, 1, 3, 0, "leaky", False, 1024),
+    "k1_128": (128, 128, 1, 1, 1, 0, "leaky", True, 1024),
+    "k3_256": (256, 256, 3, 1, 3, 0, "leaky", False, 256),
+    "k1_256": (256, 256, 1, 1, 1, 0, "leaky", True, 256),
+    "k3_512": (512, 512, 3, 1, 3, 0, "leaky", False, 128),
+    "k1_512": (512, 512, 1, 1, 1, 0, "leaky", True, 128),
+    "down4_64": (64, 128, 8, 4, 1, 0, "leaky", False, 4096),
+    "down2_256": (256, 512, 4, 2, 1, 0, "leaky", False, 256),
+    "convT2_1024": (1024, 512, 4, 2, 1, 1, "leaky", False, 64),
+    "convT4_128": (128, 64, 8, 4, 1, 1, "leaky", False, 1024),
+    "enc_out": (1024, 64, 3, 1, 1, 0, "leaky", False, 64),
+    "dec_in": (320, 1024, 3, 1, 1, 0, "none", False, 64),
+    "wave": (64, 32, 7, 1, 1, 0, "leaky", False, 4096),
+}
+
+
+STAMPS = os.environ.get("RAVE_AMD_DIAG_LIB") == "1"
+
+
+def run(name, B, iters, dev):
+    ci, co, k, s, d, tr, act, has_res, T = LAYERS[name]
+    rng = np.random.default_rng(0)
+    w = rng.uniform(-0.05, 0.05, (ci, co, k) if tr else (co, ci, k)).astype(np.float32)
+    packed = torch.from_numpy(N.pack_conv_weight(w, ci, co, k, s, d, tr)).to(dev)
+    x = torch.randn(B, ci, T, device=dev)
+    if tr:
+        t_out, pl, pr = T * s, 0, 0
+    else:
+        p = (k - 1) * d + 1
+        pl, pr = (p - 1) // 2, p // 2
+        t_out = (T + pl + pr - p) // s + 1
+    y = torch.empty(B, co, t_out, device=dev)
+    res = torch.randn(B, co, t_out, device=dev) if has_res else None
+    bias = torch.randn(co, device=dev)
+    a = N.ConvArgs(c_in=ci, c_out=co, kernel=k, stride=s, dilation=d, pad_left=pl, pad_right=pr,
+                   transposed=tr, out_shift=s // 2 if tr else 0, act=N.ACT[act], leaky_slope=0.2,
+                   batch=B, t_in=T, t_out=t_out, x=x.data_ptr(), x_sb=ci * T, x_sc=T,
+                   y=y.data_ptr(), y_sb=co * t_out, y_sc=t_out,
+                   residual=res.data_ptr() if res is not None else None, r_sb=co * t_out, r_sc=t_out,
+                   weight=packed.data_ptr(), bias=bias.data_ptr())
+    stamps = None
+    if STAMPS:
+        stamps = torch.zeros(8 * 200000, dtype=torch.int64, device=dev)
+        a.stamps = stamps.data_ptr()
+    nws = N.lib.rave_conv1d_workspace(C.byref(a))
+    ws = torch.empty(max(nws, 1), device=dev)
+    if nws > 0:
+        a.partial = ws.data_ptr()
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for _ in range(3):
+        N.check(N.lib.rave_conv1d(C.byref(a), st))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        N.check(N.lib.rave_conv1d(C.byref(a), st))
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    taps = 2 if tr else k
+    fl = 2.0 * B * co * t_out * ci * taps
+    print(f"{name:12s} B={B} ws={nws:>9d}  {ms * 1e3:8.2f} us  {fl / ms / 1e9:7.2f} TFLOP/s", flush=True)
+    if stamps is not None:
+        stamps.zero_()
+        N.check(N.lib.rave_conv1d(C.byref(a), st))
+        torch.cuda.synchronize()
+        s_ = stamps.view(-1, 8).cpu().numpy()
+        s_ = s_[s_[:, 7] != 0].astype(np.float64)
+        pro, main, epi, tot = (s_[:, 1] - s_[:, 0], s_[:, 2] - s_[:, 1], s_[:, 3] - s_[:, 2], s_[:, 3] - s_[:, 0])
+        rt = (s_[:, 7] - s_[:, 7].min()) * 10.0 / 1e3   # us (100 MHz)
+        q = lambda v: f"{np.median(v):8.0f} [{np.percentile(v, 10):7.0f},{np.percentile(v, 90):7.0f}]"
+        print(f"   WGs={len(s_)}  cycles median [p10,p90]: prologue {q(pro)} main {q(main)} "
+              f"epilogue {q(epi)} total {q(tot)}; WG start spread {rt.max():.1f} us", flush=True)
+    return ms
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", default=",".join(LAYERS))
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=16)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    for name in a.layers.split(","):
+        run(name, a.batch, a.iters, dev)
+
+
+if __name__ == "__main__":
+    main()
