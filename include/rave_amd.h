@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 1
+#define RAVE_ABI_VERSION 2
 
 /* ---------------------------------------------------------------- status */
 enum {
@@ -130,7 +130,10 @@ typedef struct rave_pqmf_analysis_args {
 } rave_pqmf_analysis_args;
 int rave_pqmf_analysis(const rave_pqmf_analysis_args* a, void* stream);
 
-/* synthesis: in = reverse_half(mode==0 ? x : tanh(x[:n]*sigmoid(x[n:2n]) + noise))
+/* synthesis: in = reverse_half(mode 0: x
+ *                                mode 1: tanh(x[:n]*sigmoid(x[n:2n]) + noise)   (amplitude modulation)
+ *                                mode 2: tanh(x[:n] + noise))
+ * (modes 1/2 are GeneratorV2's epilogue, rave/blocks.py:699-707; noise may be NULL)
  * c[m, t] = n_band * sum_{c,k} hki[m, c, k] * in[c, t + k - pad_left]   for t in [0, t_in)
  * y[b, t*n_band + i] = c[n_band-1-i, t]
  * x columns [0, x_len) are valid input frames (x_len = 0 means t_in; columns
@@ -191,6 +194,51 @@ typedef struct rave_shift_args {
 } rave_shift_args;
 int rave_shift_history(const rave_shift_args* a, void* stream);
 
+/* ---------------------------------------------------------------- noise synthesizer
+ * NoiseGeneratorV2's filter stage (rave/blocks.py:281-291, rave/core.py:66-67,95-129),
+ * after its conv stack:  for every (b, frame f, band j)
+ *   A[k]  = 2 * sigmoid(amp[b, j*noise_bands + k, f] - 5)^2.3 + 1e-7     k < noise_bands
+ *   ir    = irfft(A) (fs = 2*(noise_bands-1) taps), Hann-windowed and centred by the
+ *           roll/pad/roll of amp_to_impulse_response, length `target`
+ *   y[b, j, f*target + i] = sum_{m<=i} (2*u[b, f, j, m] - 1) * ir[i - m]   i < target
+ *           (the second half of fft_convolve's zero-padded circular product)
+ * u: (B, frames, n_band, target) U[0,1) samples (torch.rand_like(ir)); u_sb its
+ * batch stride, inner dims contiguous.  Requires target >= fs, target <= 32.
+ */
+typedef struct rave_noise_args {
+    int32_t batch, frames, n_band, noise_bands;
+    int32_t target, _pad0;
+    const float* amp; int64_t a_sb, a_sc;     /* (B, n_band*noise_bands, frames) */
+    const float* u;   int64_t u_sb;
+    float* y;         int64_t y_sb, y_sc;     /* (B, n_band, frames*target)      */
+} rave_noise_args;
+int rave_noise_synth(const rave_noise_args* a, void* stream);
+
+/* ---------------------------------------------------------------- AdaIN
+ * AdaptiveInstanceNormalization.forward in eval mode (rave/blocks.py:856-919) over
+ * the module's own buffers, kept on the device:
+ *   stats:    (4, max_batch, channels) = mean_x, std_x, mean_y, std_y   (row = row0 + b)
+ *   counters: float[2] = num_update_x, num_update_y
+ * mode 0 (transfer):  y = transfer(x) if num_update_x and num_update_y else x
+ * mode 1 (learn_x):   mean_x/std_x[row] += (stat(x) - ·)/(num_update_x + 1); num_update_x += 1;
+ *                     then as mode 0
+ * mode 2 (learn_y):   mean_y/std_y[row] += (stat(x) - ·)/(num_update_y + 1); num_update_y += 1;
+ *                     y = x
+ * stat = mean / unbiased std over t; transfer(x) = (x - mean_x)/(std_x + 1e-5)*std_y + mean_y.
+ * `ticket` is a zeroed uint32 the kernel uses to bump the counter once per call
+ * (it is left zeroed).  y may alias x.
+ */
+typedef struct rave_adain_args {
+    int32_t batch, channels, t_len, mode;
+    int32_t max_batch, row0;
+    const float* x; int64_t x_sb, x_sc;
+    float* y;       int64_t y_sb, y_sc;
+    float* stats;
+    float* counters;
+    uint32_t* ticket;
+} rave_adain_args;
+int rave_adain(const rave_adain_args* a, void* stream);
+
 /* ---------------------------------------------------------------- plans
  * A plan is a recorded sequence of the ops above (the module graph of
  * RAVE.encode/decode).  Pointer fields inside an op's args may be relocated at
@@ -206,7 +254,9 @@ enum {
     RAVE_OP_RVQ_ENCODE = 5,
     RAVE_OP_RVQ_DECODE = 6,
     RAVE_OP_SHIFT_HISTORY = 7,
-    RAVE_OP_COPY = 8
+    RAVE_OP_COPY = 8,
+    RAVE_OP_NOISE = 9,
+    RAVE_OP_ADAIN = 10
 };
 
 #define RAVE_OP_PAYLOAD 240
@@ -220,6 +270,8 @@ typedef struct rave_plan_op {
         rave_rvq_args rvq;
         rave_shift_args shift;
         rave_copy_args copy;
+        rave_noise_args noise;
+        rave_adain_args adain;
         unsigned char raw[RAVE_OP_PAYLOAD];
     } u;
 } rave_plan_op;

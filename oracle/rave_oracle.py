@@ -174,6 +174,8 @@ class Oracle:
         self.hk = qmf_bank(cfg.pqmf_attenuation, cfg.n_band) if hk is None else np.asarray(hk, np.float32)
         self.hkf, self.hki = pqmf_filters(self.hk)
         self.adain_stats = adain_stats or {}
+        self.learn_x = False
+        self.learn_y = False
         self.trace: Dict[str, np.ndarray] = {}
         self.record = False
 
@@ -200,12 +202,44 @@ class Oracle:
         return y
 
     def _adain(self, x, name):
+        """AdaptiveInstanceNormalization.forward, eval mode (rave/blocks.py:896-919).
+
+        ``adain_stats[name]`` holds the module's buffers (mean_x, std_x, mean_y,
+        std_y: (MAX_BATCH, C, 1); num_update_x/y) and is updated in place like
+        the reference's; ``self.learn_x`` / ``self.learn_y`` are the learn flags
+        (set on every module at once, as nn~'s attributes do).  Without state
+        the module is the identity."""
         st = self.adain_stats.get(name)
         if st is None:
-            return x   # eval, no learned stats: identity (rave/blocks.py:896-919)
+            return x
         bs = x.shape[0]
-        x = (x - st["mean_x"][:bs]) / (st["std_x"][:bs] + 1e-5)
-        return x * st["std_y"][:bs] + st["mean_y"][:bs]
+
+        def update(key, src, count):
+            tgt = st[key]
+            tgt[:bs] = tgt[:bs] + (src - tgt[:bs]) / (count + 1)
+
+        if self.learn_y:
+            n = float(st.get("num_update_y", 0.0))
+            update("mean_y", x.mean(-1, keepdims=True), n)
+            update("std_y", x.std(-1, ddof=1, keepdims=True), n)
+            st["num_update_y"] = n + 1
+            return x
+        if self.learn_x:
+            n = float(st.get("num_update_x", 0.0))
+            update("mean_x", x.mean(-1, keepdims=True), n)
+            update("std_x", x.std(-1, ddof=1, keepdims=True), n)
+            st["num_update_x"] = n + 1
+        if float(st.get("num_update_x", 1.0)) and float(st.get("num_update_y", 1.0)):
+            x = (x - st["mean_x"][:bs]) / (st["std_x"][:bs] + 1e-5)
+            x = x * st["std_y"][:bs] + st["mean_y"][:bs]
+        return x
+
+    @staticmethod
+    def fresh_adain_state(modules, max_batch: int = 64):
+        """Reference-initialised buffers (rave/blocks.py:858-868) for (name, C) pairs."""
+        return {n: {"mean_x": np.zeros((max_batch, c, 1)), "std_x": np.ones((max_batch, c, 1)),
+                    "mean_y": np.zeros((max_batch, c, 1)), "std_y": np.ones((max_batch, c, 1)),
+                    "num_update_x": 0.0, "num_update_y": 0.0} for n, c in modules}
 
     def _dilated_residual(self, x, res, d):
         unit = f"{res}.aligned.branches.0.net"

@@ -32,6 +32,9 @@ OP_RVQ_ENCODE = 5
 OP_RVQ_DECODE = 6
 OP_SHIFT_HISTORY = 7
 OP_COPY = 8
+OP_NOISE = 9
+OP_ADAIN = 10
+ABI_VERSION = 2
 
 i32, i64, f32, vp = C.c_int32, C.c_int64, C.c_float, C.c_void_p
 
@@ -89,6 +92,22 @@ class CopyArgs(C.Structure):
                 ("y", vp), ("y_sb", i64), ("y_sc", i64)]
 
 
+class NoiseArgs(C.Structure):
+    _fields_ = [("batch", i32), ("frames", i32), ("n_band", i32), ("noise_bands", i32),
+                ("target", i32), ("_pad0", i32),
+                ("amp", vp), ("a_sb", i64), ("a_sc", i64),
+                ("u", vp), ("u_sb", i64),
+                ("y", vp), ("y_sb", i64), ("y_sc", i64)]
+
+
+class AdainArgs(C.Structure):
+    _fields_ = [("batch", i32), ("channels", i32), ("t_len", i32), ("mode", i32),
+                ("max_batch", i32), ("row0", i32),
+                ("x", vp), ("x_sb", i64), ("x_sc", i64),
+                ("y", vp), ("y_sb", i64), ("y_sc", i64),
+                ("stats", vp), ("counters", vp), ("ticket", vp)]
+
+
 PAYLOAD = 240
 
 
@@ -102,7 +121,7 @@ class Reloc(C.Structure):
 
 
 STRUCTS = [ConvArgs, AnalysisArgs, SynthesisArgs, FillArgs, RvqArgs, ShiftArgs, PlanOp, Reloc,
-           CopyArgs]
+           CopyArgs, NoiseArgs, AdainArgs]
 
 # every exported symbol of include/rave_amd.h
 EXPORTS = [
@@ -110,7 +129,7 @@ EXPORTS = [
     "rave_conv1d_chunk", "rave_conv1d_packed_size", "rave_conv1d_pack_weight", "rave_conv1d",
     "rave_conv1d_workspace",
     "rave_pqmf_analysis", "rave_pqmf_synthesis", "rave_fill_channels", "rave_copy",
-    "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history",
+    "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
     "rave_plan_create", "rave_plan_run", "rave_plan_destroy", "rave_plan_size",
     "rave_plan_profile", "rave_plan_op_times",
 ]
@@ -138,7 +157,8 @@ def _load():
     for name, st in [("rave_conv1d", ConvArgs), ("rave_pqmf_analysis", AnalysisArgs),
                      ("rave_pqmf_synthesis", SynthesisArgs), ("rave_fill_channels", FillArgs),
                      ("rave_rvq_encode", RvqArgs), ("rave_rvq_decode", RvqArgs),
-                     ("rave_shift_history", ShiftArgs), ("rave_copy", CopyArgs)]:
+                     ("rave_shift_history", ShiftArgs), ("rave_copy", CopyArgs),
+                     ("rave_noise_synth", NoiseArgs), ("rave_adain", AdainArgs)]:
         getattr(lib, name).argtypes = [C.POINTER(st), vp]
     lib.rave_plan_create.argtypes = [C.POINTER(PlanOp), C.c_int, C.POINTER(Reloc), C.c_int,
                                      C.POINTER(vp)]
@@ -155,7 +175,7 @@ def _load():
     mine = [C.sizeof(s) for s in STRUCTS]
     if native != mine:
         raise ImportError(f"rave_amd ABI mismatch: native struct sizes {native} != ctypes {mine}")
-    if lib.rave_abi_version() != 1:
+    if lib.rave_abi_version() != ABI_VERSION:
         raise ImportError("rave_amd ABI version mismatch")
     return lib
 

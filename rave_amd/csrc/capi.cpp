@@ -32,7 +32,8 @@ extern "C" int rave_struct_sizes(int64_t* out, int n) {
         (int64_t)sizeof(rave_pqmf_synthesis_args), (int64_t)sizeof(rave_fill_args),
         (int64_t)sizeof(rave_rvq_args),          (int64_t)sizeof(rave_shift_args),
         (int64_t)sizeof(rave_plan_op),           (int64_t)sizeof(rave_reloc),
-        (int64_t)sizeof(rave_copy_args),
+        (int64_t)sizeof(rave_copy_args),         (int64_t)sizeof(rave_noise_args),
+        (int64_t)sizeof(rave_adain_args),
     };
     const int cnt = (int)(sizeof(sizes) / sizeof(sizes[0]));
     if (!out) return cnt;
@@ -143,6 +144,8 @@ extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, v
             case RAVE_OP_RVQ_DECODE: rc = rave_rvq_decode(&op.u.rvq, stream); break;
             case RAVE_OP_SHIFT_HISTORY: rc = rave_shift_history(&op.u.shift, stream); break;
             case RAVE_OP_COPY: rc = rave_copy(&op.u.copy, stream); break;
+            case RAVE_OP_NOISE: rc = rave_noise_synth(&op.u.noise, stream); break;
+            case RAVE_OP_ADAIN: rc = rave_adain(&op.u.adain, stream); break;
             default:
                 rave::set_error("plan_run: unknown op kind " + std::to_string(op.kind));
                 return RAVE_ERR_STATE;

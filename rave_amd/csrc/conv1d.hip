@@ -96,7 +96,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, int 
 
 // --------------------------------------------------------------------- epilogue
 // ConvT row m -> (output channel, phase).  Rows [0, split_row) hold phases
-// [0, q0) of every channel, rows [split_row, M) phases [q0, R).
+// [0, q0) of every channel (rows up to the 64-aligned group-1 start are
+// padding: co >= c_out), rows [split_row, M) phases [q0, R).
 __device__ __forceinline__ void convt_row(const ConvKArgs& a, int m, int& co, int& q) {
     if (m < a.split_row) {
         co = m / a.q0;
@@ -113,7 +114,7 @@ __device__ __forceinline__ void store_out(const ConvKArgs& a, int b, int m, int 
         int co, q;
         convt_row(a, m, co, q);
         const int t = n * a.R + q;
-        if (t >= a.t_y) return;
+        if (t >= a.t_y || co >= a.bias_rows) return;    // bias_rows = c_out
         if (a.bias) v += a.bias[co];
         a.y[(int64_t)b * a.y_sb + (int64_t)co * a.y_sc + t] = v;
     } else {
@@ -374,7 +375,7 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
                 int co, q;
                 convt_row(a, m, co, q);
                 const int t = n * a.R + q;
-                off = (m < a.M && n < a.U && t < a.t_y) ? (unsigned)(co * a.y_sc + t) * 4u : kOOB;
+                off = (co < a.bias_rows && n < a.U && t < a.t_y) ? (unsigned)(co * a.y_sc + t) * 4u : kOOB;
             } else {
                 off = (m < a.M && n < a.U) ? (unsigned)(m * a.y_sc + n) * 4u : kOOB;
             }
@@ -421,6 +422,13 @@ static int family_stride(int taps) {
         case 8: return 4;
         default: return 1;
     }
+}
+
+// First row of ConvT phase group 1: c_out*q0, rounded up to the 64-row tile
+// so that no tile straddles the two window offsets (no group 1: all rows).
+static inline int convt_group1_row(int c_out, int R, int q0) {
+    const int g0 = c_out * q0;
+    return q0 == R ? g0 : ceil_div(g0, 64) * 64;
 }
 
 struct LaunchCfg {
@@ -523,9 +531,9 @@ static int prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
         RAVE_CHECK_ARG(a.pad_left == 0 || a.pad_left == 1, "conv1d: transposed pad_left = history columns (0/1)");
         k.transposed = 1; k.R = a.stride; k.out_shift = a.out_shift;
         taps = 2; k.d = 1;
-        k.M = a.c_out * a.stride;
         k.q0 = a.stride - a.out_shift;               // phases whose taps are (u-1, u)
-        k.split_row = a.c_out * k.q0;
+        k.split_row = convt_group1_row(a.c_out, a.stride, k.q0);
+        k.M = k.split_row + a.c_out * (a.stride - k.q0);
         k.pad_l = 1 - a.pad_left;                    // group 0 window starts at u-1
         k.pad_g1 = -a.pad_left;                      // group 1 window starts at u
         k.U = a.t_in - a.pad_left;
@@ -584,7 +592,10 @@ extern "C" int64_t rave_conv1d_packed_size(int c_in, int c_out, int kernel, int 
     int ci_t = rave_conv1d_chunk(c_in, kernel, stride, dilation, transposed);
     if (ci_t <= 0) return -1;
     int taps = transposed ? 2 : kernel;
-    int M = transposed ? c_out * stride : c_out;
+    // transposed: the larger of the two row layouts (out_shift 0 / stride/2)
+    int M = transposed ? std::max(c_out * stride, convt_group1_row(c_out, stride, stride - stride / 2) +
+                                                      c_out * (stride / 2))
+                       : c_out;
     int64_t Mpad = (int64_t)ceil_div(M, 128) * 128;
     int64_t nchunks = ceil_div(c_in, ci_t);
     return nchunks * ci_t * taps * Mpad;
@@ -604,9 +615,9 @@ extern "C" int rave_conv1d_pack_weight(const float* w, int c_in, int c_out, int 
                    "pack_weight: transposed out_shift must be 0 or stride/2");
     int taps = transposed ? 2 : kernel;
     int R = transposed ? stride : 1;
-    int M = c_out * R;
     int q0 = R - (transposed ? out_shift : 0);       // ConvT phases in row group 0
-    int split_row = c_out * q0;
+    int split_row = transposed ? convt_group1_row(c_out, R, q0) : 1 << 30;
+    int M = transposed ? split_row + c_out * (R - q0) : c_out;
     int64_t Mpad = (int64_t)ceil_div(M, 128) * 128;
     int nchunks = ceil_div(c_in, ci_t);
     int BK = ci_t * taps;
@@ -626,6 +637,7 @@ extern "C" int rave_conv1d_pack_weight(const float* w, int c_in, int c_out, int 
                         int co, q;
                         if (m < split_row) { co = m / q0; q = m % q0; }
                         else { int p = R - q0; co = (m - split_row) / p; q = q0 + (m - split_row) % p; }
+                        if (co >= c_out) { row[m] = 0.f; continue; }   // group-0 padding rows
                         int kidx;
                         if (q < q0) kidx = (j == 0) ? q + out_shift + R : q + out_shift;
                         else kidx = (j == 0) ? q + out_shift : q + out_shift - R;

@@ -97,9 +97,11 @@ __global__ __launch_bounds__(256) void pqmf_synthesis_kernel(rave_pqmf_synthesis
         float v = 0.f;
         if (f >= 0 && f < x_len) {
             v = xb[(int64_t)c * a.x_sc + f];
-            if (a.mode == 1) {
-                float amp = xb[(int64_t)(c + nb) * a.x_sc + f];
-                v = v * (1.0f / (1.0f + expf(-amp)));
+            if (a.mode != 0) {
+                if (a.mode == 1) {
+                    float amp = xb[(int64_t)(c + nb) * a.x_sc + f];
+                    v = v * (1.0f / (1.0f + expf(-amp)));
+                }
                 if (nzb) v = v + nzb[(int64_t)c * a.n_sc + f];
                 v = tanhf(v);
             }
@@ -159,7 +161,7 @@ extern "C" int rave_pqmf_synthesis(const rave_pqmf_synthesis_args* p, void* stre
     RAVE_CHECK_ARG(a.n_band == 16, "pqmf_synthesis: kernel is built for 16 bands");
     RAVE_CHECK_ARG(a.taps > 0 && a.taps <= 64, "pqmf_synthesis: bad taps");
     RAVE_CHECK_ARG(a.batch > 0 && a.t_in > 0, "pqmf_synthesis: empty shape");
-    RAVE_CHECK_ARG(a.mode == 0 || a.mode == 1, "pqmf_synthesis: mode must be 0 or 1");
+    RAVE_CHECK_ARG(a.mode >= 0 && a.mode <= 2, "pqmf_synthesis: mode must be 0, 1 or 2");
     int hrow = a.n_band * a.taps + 1;
     size_t lds = (size_t)(a.n_band * hrow + a.n_band * (kSynT + a.taps - 1)) * sizeof(float);
     dim3 grid(ceil_div(a.t_in, kSynT), a.batch);

@@ -63,6 +63,9 @@ class ShardedRunner:
 
     def step(self, x_local: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         rank, size = world()
+        if getattr(self.model, "adain", None) is not None:
+            # AdaIN buffer rows follow the global batch index (rave/blocks.py:886-891)
+            self.model.adain_row0 = rank * x_local.shape[0]
         z = self.model.encode(x_local)
         if size > 1:
             shape = (size * z.shape[0],) + tuple(z.shape[1:])

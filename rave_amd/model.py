@@ -26,6 +26,7 @@ import torch
 
 from . import _native as N
 from . import pqmf as P
+from .adain import AdainState
 from .config import RaveConfig, get_padding
 from .graph import ConvNode, build_graph
 from .weights import check_params, conv_weight
@@ -64,8 +65,9 @@ class Arena:
 # ============================================================ plans
 @dataclass(frozen=True)
 class View:
-    """A (B, C, T) time-contiguous view: slot 'ws' (workspace), 'arena', or an
-    integer I/O slot bound at run time."""
+    """A (B, C, T) time-contiguous view: slot 'ws' (workspace), 'arena', 'abs'
+    (``off`` is an absolute device address in bytes, elem 1), or an integer I/O
+    slot bound at run time."""
     slot: object
     off: int          # elements from the slot base
     sb: int
@@ -111,7 +113,7 @@ class Workspace:
 def splitk_floats(scalars: dict, has_res: bool = False) -> int:
     """Split-K slab floats the native launcher wants for a conv (0 = unsplit)."""
     a = N.ConvArgs(**scalars)
-    a.x = a.y = a.weight = 16          # placeholders: only shapes are inspected
+    a.x = a.y = a.weight = a.alpha = 16   # placeholders: only shapes are inspected
     a.residual = 16 if has_res else None
     n = int(N.lib.rave_conv1d_workspace(C.byref(a)))
     if n < 0:
@@ -149,7 +151,8 @@ class Plan:
         self.labels.append(label or {N.OP_CONV: "conv", N.OP_PQMF_ANALYSIS: "pqmf_analysis",
                                      N.OP_PQMF_SYNTHESIS: "pqmf_synthesis", N.OP_FILL: "fill",
                                      N.OP_RVQ_ENCODE: "rvq_encode", N.OP_RVQ_DECODE: "rvq_decode",
-                                     N.OP_SHIFT_HISTORY: "shift_history"}.get(kind, "op"))
+                                     N.OP_SHIFT_HISTORY: "shift_history", N.OP_COPY: "copy",
+                                     N.OP_NOISE: "noise_synth", N.OP_ADAIN: "adain"}.get(kind, "op"))
         self.flops.append(float(flops))
 
     def finalize(self, device) -> "Plan":
@@ -176,6 +179,8 @@ class Plan:
                     setattr(args, field, self.ws_tensor.data_ptr() + 4 * splitk_off)
                 elif view.slot == "arena":
                     setattr(args, field, self.arena.ptr(view.off))
+                elif view.slot == "abs":
+                    setattr(args, field, view.off)
                 else:
                     setattr(args, field, None)
                     relocs.append(N.Reloc(i, getattr(st, field).offset, int(view.slot), 0,
@@ -221,9 +226,6 @@ class RAVE:
     def __init__(self, cfg: RaveConfig, params: Mapping[str, np.ndarray], speaker: np.ndarray,
                  device=None, hk: Optional[np.ndarray] = None,
                  adain_stats: Optional[Mapping] = None):
-        if adain_stats:
-            raise NotImplementedError("AdaIN with learned statistics is not implemented on the "
-                                      "HIP path yet (eval-mode identity is)")
         check_params(cfg, params)
         self.cfg = cfg
         self.graph = build_graph(cfg)
@@ -243,6 +245,7 @@ class RAVE:
             bo = ar.add(params[n.name + ".bias"]) if n.bias else None
             ao = ar.add(params[n.alpha]) if n.act == "snake" else None
             self.w_off[n.name] = (wo, bo, ao)
+        self.noise_target = int(np.prod(cfg.noise.ratios)) if cfg.noise is not None else 0
         self.hk = P.design_bank(cfg.pqmf_attenuation, cfg.n_band) if hk is None else np.asarray(hk, np.float32)
         hkf, hki = P.kernels(self.hk)
         self.taps_a, self.taps_s = hkf.shape[-1], hki.shape[-1]
@@ -260,6 +263,35 @@ class RAVE:
         ar.upload(self.device)
         self.arena = ar
         self._plans: Dict[tuple, Plan] = {}
+        # AdaIN buffers (rave/blocks.py:856-919): identity until statistics are
+        # loaded or learned; ``adain_row0`` is the first buffer row this
+        # process's batch uses (batch shards of a data-parallel job).
+        self.adain: Optional[AdainState] = None
+        self.adain_row0 = 0
+        if cfg.adain:
+            self.adain = AdainState(self.graph.adain_modules, self.device)
+            if adain_stats:
+                self.adain.load(adain_stats)
+        elif adain_stats:
+            raise ValueError("adain_stats given for a config without AdaIN")
+
+    def _adain_key(self) -> tuple:
+        return self.adain.key() + (self.adain_row0,) if self.adain is not None else ()
+
+    def _adain_op(self, plan: Plan, name: str, B: int, C: int, T: int, x: View) -> None:
+        """AdaIN in place on the residual unit's input (it is both the unit's
+        conv input and its residual, and has no other reader)."""
+        ad = self.adain
+        if self.adain_row0 + B > ad.max_batch:
+            raise ValueError(f"AdaIN statistics hold {ad.max_batch} batch rows "
+                             f"(cc.MAX_BATCH_SIZE); batch {B} at row {self.adain_row0} exceeds them")
+        st, cnt, tk = ad.ptrs(name)
+        plan.add(N.OP_ADAIN, N.AdainArgs,
+                 dict(batch=B, channels=C, t_len=T, mode=ad.mode, max_batch=ad.max_batch,
+                      row0=self.adain_row0, x_sb=x.sb, x_sc=x.sc, y_sb=x.sb, y_sc=x.sc),
+                 dict(x=x, y=x, stats=View("abs", st, 0, 0, elem=1),
+                      counters=View("abs", cnt, 0, 0, elem=1), ticket=View("abs", tk, 0, 0, elem=1)),
+                 label=name)
 
     # ------------------------------------------------------------ plan pieces
     def _conv(self, plan: Plan, n: ConvNode, B: int, t_in: int, src: View, dst: View,
@@ -297,6 +329,8 @@ class RAVE:
         tensors: Dict[str, Tuple[View, int, int]] = {k: (v, t, -1) for k, (v, t) in inputs.items()}
         for i, n in enumerate(nodes):
             src, t_in, _ = tensors[n.src]
+            if n.adain and self.adain is not None and self.adain.active:
+                self._adain_op(plan, n.adain, B, n.c_in, t_in, src)
             t_out = n.out_len(t_in)
             if n.dst in outputs:
                 dst = outputs[n.dst]
@@ -344,7 +378,7 @@ class RAVE:
 
     # ------------------------------------------------------------ plans
     def _encode_plan(self, B: int, T: int, codes: bool = False) -> Plan:
-        key = ("enc_codes" if codes else "enc", B, T)
+        key = ("enc_codes" if codes else "enc", B, T) + self._adain_key()
         if key in self._plans:
             return self._plans[key]
         cfg = self.cfg
@@ -374,12 +408,10 @@ class RAVE:
         return plan
 
     def _decode_plan(self, B: int, Fz: int, codes: bool = False) -> Plan:
-        key = ("dec_codes" if codes else "dec", B, Fz)
+        key = ("dec_codes" if codes else "dec", B, Fz) + self._adain_key()
         if key in self._plans:
             return self._plans[key]
         cfg = self.cfg
-        if cfg.noise is not None:
-            raise NotImplementedError("NoiseGeneratorV2 is not on the HIP path yet")
         plan = Plan(self.arena)
         zc = cfg.dec_in
         if codes:
@@ -396,9 +428,26 @@ class RAVE:
             z = View(0, 0, zc * Fz, Fz)
         F = Fz * cfg.hop // cfg.n_band
         wave = View("ws", plan.ws.alloc(B * cfg.dec_out * F), cfg.dec_out * F, F)
-        self._run_stack(plan, self.graph.decoder, B, {"dec_in": (z, Fz)}, {"wave": wave})
+        outputs = {"wave": wave}
+        noise = None
+        if cfg.noise is not None:
+            nz = cfg.noise
+            Fn = F // self.noise_target
+            na = cfg.n_band * nz.noise_bands
+            outputs["noise_amp"] = View("ws", plan.ws.alloc(B * na * Fn), na * Fn, Fn)
+        self._run_stack(plan, self.graph.decoder + self.graph.noise, B, {"dec_in": (z, Fz)}, outputs)
+        if cfg.noise is not None:
+            # NoiseGeneratorV2 filter stage; the uniform noise is I/O slot 2
+            noise = View("ws", plan.ws.alloc(B * cfg.n_band * F), cfg.n_band * F, F)
+            amp = outputs["noise_amp"]
+            plan.add(N.OP_NOISE, N.NoiseArgs,
+                     dict(batch=B, frames=Fn, n_band=cfg.n_band, noise_bands=nz.noise_bands,
+                          target=self.noise_target, a_sb=amp.sb, a_sc=amp.sc,
+                          u_sb=Fn * cfg.n_band * self.noise_target, y_sb=noise.sb, y_sc=noise.sc),
+                     dict(amp=amp, u=View(2, 0, 0, 0), y=noise))
         T = F * cfg.n_band
-        self._synthesis(plan, B, F, wave, View(1, 0, T, T), 1 if cfg.amplitude_modulation else 0)
+        self._synthesis(plan, B, F, wave, View(1, 0, T, T), 1 if cfg.amplitude_modulation else 2,
+                        noise=noise)
         self._plans[key] = plan.finalize(self.device)
         return plan
 
@@ -421,7 +470,30 @@ class RAVE:
         self._encode_plan(B, T).run([x.data_ptr(), z.data_ptr()])
         return z
 
-    def decode(self, z: torch.Tensor) -> torch.Tensor:
+    def noise_shape(self, B: int, Fz: int) -> Tuple[int, int, int, int]:
+        """Shape of NoiseGeneratorV2's uniform noise (torch.rand_like(ir),
+        rave/blocks.py:287): (B, frames, n_band, target_size)."""
+        F = Fz * self.cfg.hop // self.cfg.n_band
+        return (B, F // self.noise_target, self.cfg.n_band, self.noise_target)
+
+    def _noise_slot(self, B: int, Fz: int, noise_u: Optional[torch.Tensor], dev) -> List[int]:
+        if self.cfg.noise is None:
+            if noise_u is not None:
+                raise ValueError("noise_u given for a config without a noise synthesizer")
+            return []
+        shape = self.noise_shape(B, Fz)
+        if noise_u is None:
+            noise_u = torch.rand(shape, device=dev)      # rand_like on the device RNG
+        elif (noise_u.dtype != torch.float32 or noise_u.device.type != "cuda"
+              or tuple(noise_u.shape) != shape):
+            raise ValueError(f"noise_u must be a float32 CUDA tensor of shape {shape}")
+        self._noise_keep = noise_u = noise_u.contiguous()
+        return [noise_u.data_ptr()]
+
+    def decode(self, z: torch.Tensor, noise_u: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """GeneratorV2 -> PQMF inverse.  For a noise config, ``noise_u`` (U[0,1),
+        ``noise_shape``) replaces the reference's torch.rand_like draw; when
+        omitted it is drawn on the device."""
         if not isinstance(z, torch.Tensor) or z.device.type != "cuda" or z.dtype != torch.float32:
             raise ValueError("z must be a float32 CUDA tensor")
         if z.dim() != 3 or z.shape[1] != self.cfg.dec_in:
@@ -429,11 +501,12 @@ class RAVE:
         z = z.contiguous()
         B, _, Fz = z.shape
         y = torch.empty(B, 1, Fz * self.cfg.hop, device=z.device)
-        self._decode_plan(B, Fz).run([z.data_ptr(), y.data_ptr()])
+        slots = [z.data_ptr(), y.data_ptr()] + self._noise_slot(B, Fz, noise_u, z.device)
+        self._decode_plan(B, Fz).run(slots)
         return y
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.decode(self.encode(x))
+    def forward(self, x: torch.Tensor, noise_u: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return self.decode(self.encode(x), noise_u)
 
     __call__ = forward
 
@@ -459,7 +532,8 @@ class RAVE:
         idx = idx.contiguous()
         B, _, Fz = idx.shape
         y = torch.empty(B, 1, Fz * self.cfg.hop, device=idx.device)
-        self._decode_plan(B, Fz, codes=True).run([idx.data_ptr(), y.data_ptr()])
+        slots = [idx.data_ptr(), y.data_ptr()] + self._noise_slot(B, Fz, None, idx.device)
+        self._decode_plan(B, Fz, codes=True).run(slots)
         return y
 
     def forward_codes(self, x: torch.Tensor) -> torch.Tensor:

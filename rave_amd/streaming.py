@@ -53,6 +53,9 @@ class StreamingRAVE:
             raise ValueError("streaming requires a causal config (causal.gin)")
         if cfg.noise is not None:
             raise NotImplementedError("streaming noise synthesis is not implemented")
+        if model.adain is not None and model.adain.active:
+            raise NotImplementedError("streaming with learned AdaIN statistics is not implemented "
+                                      "(the identity AdaIN of a fresh model is)")
         if block % cfg.hop:
             raise ValueError(f"block must be a multiple of {cfg.hop}")
         self.model, self.cfg, self.B, self.block = model, cfg, batch, block
@@ -168,7 +171,7 @@ class StreamingRAVE:
         w, hw, tw = bufs["wave"]
         plan.add(N.OP_PQMF_SYNTHESIS, N.SynthesisArgs,
                  dict(n_band=cfg.n_band, taps=m.taps_s, batch=B, t_in=self.F, pad_left=0,
-                      mode=1 if cfg.amplitude_modulation else 0, frame0=-hw, x_len=hw + self.F,
+                      mode=1 if cfg.amplitude_modulation else 2, frame0=-hw, x_len=hw + self.F,
                       x_sb=w.sb, x_sc=w.sc, n_sb=0, n_sc=0, y_sb=self.block),
                  dict(x=View("ws", w.off, w.sb, w.sc), y=View(1, 0, self.block, self.block),
                       noise=None, hki=View("arena", m.hki_off, 0, 0)))

@@ -339,6 +339,50 @@ def gen_streaming(mods, cfg, out, seed=0, n_blocks=12, block=2048):
     return res
 
 
+def gen_adain(mods, cfg, out, fname="v3_adain.npz", batch=2, t=8192, seed=0):
+    """AdaIN style transfer in eval mode (rave/blocks.py:856-919), driven the
+    way nn~'s learn_source / learn_target attributes drive it: learn the target
+    statistics on x_tgt, learn the source statistics on x_src (the transfer
+    turns on in that same call), transfer with frozen statistics, then learn the
+    source again on a smaller batch (the buffers' [:bs] rows).  Every call is a
+    full encode -> decode (AdaIN sits in both EncoderV2 and GeneratorV2)."""
+    m = build_reference(mods, cfg, cached=False)
+    params = init_params(cfg, seed=seed)
+    load_params(m, cfg, params)
+    speaker = torch.from_numpy(init_speaker(cfg, seed=seed))
+    n = np.arange(t)
+    rng = np.random.Generator(np.random.PCG64(100))
+    x_tgt = torch.from_numpy((0.8 * np.sin(2 * np.pi * 3000 * n / 48000)[None, None, :]
+                              * np.linspace(0.2, 1.0, batch)[:, None, None]
+                              + 0.3 * rng.standard_normal((batch, 1, t))).astype(np.float32))
+    x_src = torch.from_numpy(synth_audio(batch, t, seed0=200))
+    ada = [mod for mod in m.modules() if isinstance(mod, mods["blocks"].AdaptiveInstanceNormalization)]
+    names = [n for n, mod in m.named_modules() if isinstance(mod, mods["blocks"].AdaptiveInstanceNormalization)]
+
+    def set_learn(lx, ly):
+        for mod in ada:
+            mod.learn_x.fill_(float(lx))
+            mod.learn_y.fill_(float(ly))
+
+    res = {"x_tgt": x_tgt.numpy(), "x_src": x_src.numpy(), "speaker": speaker.numpy(),
+           "seed": np.int64(seed), "names": np.array(names)}
+    steps = [("learn_y", (0, 1), x_tgt), ("learn_x", (1, 0), x_src), ("transfer", (0, 0), x_src),
+             ("learn_x_bs1", (1, 0), x_src[:1])]
+    with torch.no_grad():
+        for i, (tag, (lx, ly), x) in enumerate(steps):
+            set_learn(lx, ly)
+            z = ref_encode(m, cfg, x, speaker)
+            y = ref_decode(m, z)
+            res[f"step{i}/z"] = z.numpy()
+            res[f"step{i}/y"] = y.numpy()
+    res["steps"] = np.array([s[0] for s in steps])
+    for n, mod in zip(names, ada):
+        for b in ("mean_x", "std_x", "mean_y", "std_y", "num_update_x", "num_update_y"):
+            res[f"final/{n}.{b}"] = getattr(mod, b).numpy().copy()
+    np.savez_compressed(os.path.join(out, fname), **res)
+    return res
+
+
 def check_residual_semantics(mods):
     """The reference's tests/test_residual.py logic (streaming == one-shot,
     delay-shifted) run against the cached_conv restatement."""
@@ -380,9 +424,14 @@ def check_residual_semantics(mods):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
+    ap.add_argument("--only", default=None, help="regenerate one fixture group (e.g. adain)")
     a = ap.parse_args()
     torch.set_num_threads(8)
     mods = install_shims()
+    if a.only == "adain":
+        gen_adain(mods, rcfg.v3(), a.out)
+        gen_adain(mods, rcfg.v3(capacity=8), a.out, fname="v3_adain_small.npz", t=4096)
+        return
     manifest = {"generator": "tests/golden/make_golden.py",
                 "reference": "abargum/RAVE @ 2024-10-16 (path-imported, see docstring)",
                 "torch": torch.__version__}
@@ -400,6 +449,8 @@ def main():
     gen_model(mods, rcfg.v3_noise(), a.out, "v3_noise.npz")
     gen_model(mods, rcfg.v3_noise(capacity=8), a.out, "v3_noise_small_layers.npz", batch=1, t=4096,
               per_layer=True)
+    gen_adain(mods, rcfg.v3(), a.out)
+    gen_adain(mods, rcfg.v3(capacity=8), a.out, fname="v3_adain_small.npz", t=4096)
 
     files = sorted(f for f in os.listdir(a.out) if f.endswith(".npz"))
     manifest["files"] = {f: hashlib.sha256(open(os.path.join(a.out, f), "rb").read()).hexdigest()[:16]

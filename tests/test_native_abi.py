@@ -44,7 +44,11 @@ def _emulate_packed_conv(packed, x, c_in, c_out, k, s, d, pad, transposed, out_s
     ci_t = N.conv_chunk(c_in, k, s, d, transposed)
     taps = 2 if transposed else k
     R = s if transposed else 1
-    M = c_out * R
+    P = R // 2 if out_shift is None else out_shift
+    q0 = R - P
+    # group 1 starts on a 64-row tile boundary (rows in between are padding)
+    split = c_out * q0 if (not transposed or q0 == R) else -(-c_out * q0 // 64) * 64
+    M = split + c_out * (R - q0) if transposed else c_out
     Mpad = -(-M // 128) * 128
     nch = -(-c_in // ci_t)
     W = packed.reshape(nch, taps, ci_t, Mpad)[..., :M]
@@ -59,14 +63,14 @@ def _emulate_packed_conv(packed, x, c_in, c_out, k, s, d, pad, transposed, out_s
                 xs = xp[:, c * ci_t:(c + 1) * ci_t, j * d: j * d + (U - 1) * s + 1: s]
                 y += np.einsum("im,bin->bmn", W[c, j], xs)
         return y
-    P = R // 2 if out_shift is None else out_shift
-    q0 = R - P
-    split = c_out * q0
     xp = np.pad(xc, ((0, 0), (0, 0), (1, 1)))        # x[-1] and x[T] are zero
     out = np.zeros((B, c_out, T * R))
     for m in range(M):
         if m < split:
             co, q, off = m // q0, m % q0, -1
+            if co >= c_out:
+                assert not W[..., m].any()           # padding rows are zero
+                continue
         else:
             co, q, off = (m - split) // (R - q0), q0 + (m - split) % (R - q0), 0
         acc = np.zeros((B, T))
@@ -164,3 +168,27 @@ def test_pack_layout_transposed_cached_form(c_in, c_out, r):
     packed = N.pack_conv_weight(w, c_in, c_out, 2 * r, r, 1, 1, out_shift=0)
     got = _emulate_packed_conv(packed, x, c_in, c_out, 2 * r, r, 1, (0, 0), 1, out_shift=0)
     assert np.abs(got - ref).max() < 1e-9 * max(1, np.abs(ref).max()) * 1e4
+
+
+def test_adain_state_roundtrip():
+    """AdaIN buffers: reference init, load/state_dict under the reference's
+    names, learn flags -> kernel mode (learn_y wins, as forward checks it first)."""
+    import torch
+    from rave_amd.adain import AdainState
+    st = AdainState([("a", 4), ("b", 8)], torch.device("cpu"))
+    assert not st.active and st.mode == 0
+    sd = st.state_dict()
+    assert sd["a.mean_x"].shape == (64, 4, 1) and (sd["b.std_y"] == 1).all()
+    rng = np.random.default_rng(0)
+    new = {"b.mean_y": rng.standard_normal((64, 8, 1)), "b.num_update_y": np.array([3.0])}
+    st.load(new)
+    assert st.active
+    sd = st.state_dict()
+    assert np.allclose(sd["b.mean_y"], new["b.mean_y"]) and sd["b.num_update_y"][0] == 3.0
+    assert (sd["a.mean_y"] == 0).all()
+    st.set_learn(learn_x=True, learn_y=True)
+    assert st.mode == 2
+    st.set_learn(learn_y=False)
+    assert st.mode == 1
+    st.reset_y()
+    assert (st.state_dict()["b.mean_y"] == 0).all() and st.state_dict()["b.num_update_y"][0] == 0

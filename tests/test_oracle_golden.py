@@ -118,3 +118,36 @@ def test_causal_streaming_is_delayed_oneshot(golden):
     assert maxabs(g["z_stream"], g["z_oneshot"]) < 1e-5
     o = _oracle(rcfg.causal(), g)
     assert maxabs(o.decode(g["z"]), g["y_oneshot"]) < TOL
+
+
+def adain_sequence(g):
+    """(tag, learn_x, learn_y, x) of the AdaIN fixture's call sequence."""
+    flags = {"learn_y": (False, True), "learn_x": (True, False), "transfer": (False, False),
+             "learn_x_bs1": (True, False)}
+    xs = {"learn_y": g["x_tgt"], "learn_x": g["x_src"], "transfer": g["x_src"],
+          "learn_x_bs1": g["x_src"][:1]}
+    return [(str(t),) + flags[str(t)] + (xs[str(t)],) for t in g["steps"]]
+
+
+@pytest.mark.parametrize("name,cfg", [("v3_adain_small", rcfg.v3(capacity=8)),
+                                      ("v3_adain", rcfg.v3())])
+def test_adain_style_transfer(golden, name, cfg):
+    """learn_y -> learn_x -> transfer -> learn_x(bs=1), buffers updated in place."""
+    from rave_amd.graph import build_graph
+    g = golden(name)
+    o = _oracle(cfg, g)
+    mods = build_graph(cfg).adain_modules
+    assert [n for n, _ in mods] == [str(n) for n in g["names"]]
+    o.adain_stats = Oracle.fresh_adain_state(mods)
+    for i, (tag, lx, ly, x) in enumerate(adain_sequence(g)):
+        o.learn_x, o.learn_y = lx, ly
+        z = o.encode(x)
+        assert rel(z, g[f"step{i}/z"]) < TOL, tag
+        y = o.decode(z)
+        assert maxabs(y, g[f"step{i}/y"]) < TOL, tag
+    for n, _ in mods:
+        st = o.adain_stats[n]
+        for b in ("mean_x", "std_x", "mean_y", "std_y"):
+            assert rel(st[b], g[f"final/{n}.{b}"]) < 1e-4, (n, b)
+        assert st["num_update_x"] == float(g[f"final/{n}.num_update_x"][0])
+        assert st["num_update_y"] == float(g[f"final/{n}.num_update_y"][0])
