@@ -34,6 +34,23 @@ PEAK_FP32_TFLOPS = 157.3      # MI355X dense FP32 (vector = MFMA), MI355X_MICROA
 SR = 48000
 
 
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "conv_traffic.json")
+
+
+def traffic_per_op(config: str, B: int, T: int):
+    """HBM bytes per conv op from the committed rocprofv3 PMC passes
+    (tools/profile_round.sh -> tools/rocprof_summary.py), for this exact
+    workload only; null otherwise."""
+    try:
+        with open(TRAFFIC_FILE) as fh:
+            t = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if t.get("workload") != [config, B, T]:
+        return None
+    return t.get("bytes_per_op")
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -110,9 +127,12 @@ def main():
     def step():
         return runner.step(x)[1]
 
+    pe = model._encode_plan(B, T)
+    pd = model._decode_plan(B, Fz)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    profile = not a.no_profile
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -134,38 +154,45 @@ def main():
 
     # ---------------------------------------------------------- roofline (HIP events per op)
     roof = None
-    if not a.no_profile:
-        pe = model._encode_plan(B, T)
-        pd = model._decode_plan(B, Fz)
-        pe.profile(True)
-        pd.profile(True)
-        te = np.zeros(len(pe.sym))
-        td = np.zeros(len(pd.sym))
+    if profile:
+        # Per-op timing over a second pass of the same K steps: the events ride
+        # inside the kernels' own dispatch packets (hipExtLaunchKernelGGL, no
+        # marker packets, no host syncs).  Kept out of the timed pass above,
+        # whose wall time the event bookkeeping would stretch (~15 %).
+        pe.profile(a.steps)
+        pd.profile(a.steps)
         for _ in range(a.steps):
-            z = model.encode(x)
-            te = pe.op_times(te)
-            model.decode(z)
-            td = pd.op_times(td)
-        pe.profile(False)
-        pd.profile(False)
+            step()
+        torch.cuda.synchronize()
+        te, ne = pe.op_times()
+        td, nd = pd.op_times()
+        pe.profile(0)
+        pd.profile(0)
+        if ne != a.steps or nd != a.steps:
+            raise RuntimeError(f"profiled {ne}/{nd} runs, expected {a.steps}")
         te /= a.steps
         td /= a.steps
         conv_ms = conv_fl = 0.0
         rows = []
+        from rave_amd import _native as N
+        n_conv = 0
         for plan, tm in ((pe, te), (pd, td)):
-            for lab, fl, ms in zip(plan.labels, plan.flops, tm):
+            for sym, lab, fl, ms in zip(plan.sym, plan.labels, plan.flops, tm):
                 rows.append((lab, fl, ms))
-                if lab not in ("pqmf_analysis", "pqmf_synthesis", "fill"):
+                if sym[0] == N.OP_CONV:
                     conv_ms += ms
                     conv_fl += fl
-        n_conv = sum(1 for r in rows if r[0] not in ("pqmf_analysis", "pqmf_synthesis", "fill"))
+                    n_conv += 1
         achieved = conv_fl / (conv_ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
-                "kernel": "conv1d_mfma_kernel (all %d conv launches of one step, fp32 MFMA 32x32x2)" % n_conv,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                "traffic": traffic_per_op(cfg.name, B, T),
+                "kernel": "conv1d_mfma_kernel (+ its split-K reduce): all %d conv ops of one step, "
+                          "fp32 MFMA 32x32x2" % n_conv,
                 "flop_per_launch_avg": conv_fl / max(n_conv, 1),
                 "avg_launch_ms": conv_ms / max(n_conv, 1),
-                "event_ms_per_step": round(float(te.sum() + td.sum()), 4)}
+                "event_ms_per_step": round(float(te.sum() + td.sum()), 4),
+                "timing": "HIP events inside the conv dispatches, K steps after the timed pass"}
         if rank == 0:
             log(f"{'op':58s} {'GFLOP':>8s} {'ms':>8s} {'TFLOP/s':>8s}")
             for lab, fl, ms in rows:

@@ -287,9 +287,13 @@ int rave_plan_create(const rave_plan_op* ops, int n_ops, const rave_reloc* reloc
 int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, void* stream);
 int rave_plan_destroy(rave_plan* plan);
 int rave_plan_size(const rave_plan* plan);
-/* Per-op timing with HIP events recorded around every op on the run stream
- * (measurement only; enable = 0 frees the events).  rave_plan_op_times waits
- * for the last run and ADDS each op's elapsed milliseconds into ms[0..n). */
+/* Per-op timing (measurement only).  rave_plan_profile(plan, runs) arms event
+ * sets for up to `runs` consecutive runs (0 frees them); the events ride inside
+ * the op's own kernel dispatches (first kernel start -> last kernel end), so
+ * timed runs need no host synchronisation and get no extra packets.
+ * rave_plan_op_times waits for the recorded runs, ADDS each op's elapsed
+ * milliseconds summed over them into ms[0..n), re-arms, and returns the number
+ * of runs summed (>= 0) or an error status. */
 int rave_plan_profile(rave_plan* plan, int enable);
 int rave_plan_op_times(rave_plan* plan, float* ms, int n);
 

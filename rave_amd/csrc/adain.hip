@@ -97,6 +97,6 @@ extern "C" int rave_adain(const rave_adain_args* p, void* stream) {
     RAVE_CHECK_ARG(a.mode == 0 || a.ticket, "adain: learning modes need the ticket word");
     RAVE_CHECK_ARG(a.row0 >= 0 && a.row0 + a.batch <= a.max_batch,
                    "adain: batch exceeds the statistics buffers (cc.MAX_BATCH_SIZE rows)");
-    hipLaunchKernelGGL(adain_kernel, dim3(a.channels, a.batch), dim3(kAdaThreads), 0, as_stream(stream), a);
+    launch(adain_kernel, dim3(a.channels, a.batch), dim3(kAdaThreads), 0, as_stream(stream), a);
     return launch_status("adain_kernel");
 }

@@ -7,19 +7,21 @@
 #include <string>
 #include <vector>
 
-#include "../../include/rave_amd.h"
+#include "common.h"
 
 namespace rave {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
+thread_local OpEvents g_op_events;
 }  // namespace rave
 
 struct rave_plan {
     std::vector<rave_plan_op> ops;
     std::vector<rave_reloc> relocs;
     std::vector<rave_plan_op> scratch;   // relocated copy used by run()
-    std::vector<hipEvent_t> ev;          // 2 per op when profiling
-    bool ran = false;
+    std::vector<hipEvent_t> ev;          // 2 per op per armed run when profiling
+    int runs_cap = 0;                    // armed runs
+    int runs = 0;                        // runs recorded since the last op_times
 };
 
 extern "C" const char* rave_last_error(void) { return rave::g_err.c_str(); }
@@ -64,16 +66,17 @@ extern "C" int rave_plan_create(const rave_plan_op* ops, int n_ops, const rave_r
     return RAVE_OK;
 }
 
-extern "C" int rave_plan_profile(rave_plan* plan, int enable) {
-    if (!plan) {
-        rave::set_error("plan_profile: null plan");
+extern "C" int rave_plan_profile(rave_plan* plan, int runs) {
+    if (!plan || runs < 0) {
+        rave::set_error("plan_profile: null plan or negative run count");
         return RAVE_ERR_STATE;
     }
     for (hipEvent_t e : plan->ev) (void)hipEventDestroy(e);
     plan->ev.clear();
-    plan->ran = false;
-    if (enable) {
-        plan->ev.resize(2 * plan->ops.size());
+    plan->runs_cap = 0;
+    plan->runs = 0;
+    if (runs > 0) {
+        plan->ev.resize(2 * plan->ops.size() * (size_t)runs);
         for (auto& e : plan->ev) {
             hipError_t err = hipEventCreate(&e);
             if (err != hipSuccess) {
@@ -81,31 +84,33 @@ extern "C" int rave_plan_profile(rave_plan* plan, int enable) {
                 return RAVE_ERR_HIP;
             }
         }
+        plan->runs_cap = runs;
     }
     return RAVE_OK;
 }
 
 extern "C" int rave_plan_op_times(rave_plan* plan, float* ms, int n) {
-    if (!plan || plan->ev.empty() || !plan->ran) {
-        rave::set_error("plan_op_times: profiling not enabled or plan not run");
+    if (!plan || plan->ev.empty()) {
+        rave::set_error("plan_op_times: profiling not enabled");
         return RAVE_ERR_STATE;
     }
     const int nops = (int)plan->ops.size();
-    hipError_t err = hipEventSynchronize(plan->ev[2 * nops - 1]);
-    if (err != hipSuccess) {
-        rave::set_error(std::string("plan_op_times: ") + hipGetErrorString(err));
-        return RAVE_ERR_HIP;
-    }
-    for (int i = 0; i < nops && i < n; ++i) {
-        float t = 0.f;
-        err = hipEventElapsedTime(&t, plan->ev[2 * i], plan->ev[2 * i + 1]);
+    const int runs = plan->runs;
+    for (int r = 0; r < runs; ++r) {
+        hipEvent_t* ev = plan->ev.data() + (size_t)2 * nops * r;
+        hipError_t err = hipEventSynchronize(ev[2 * nops - 1]);
+        for (int i = 0; i < nops && i < n && err == hipSuccess; ++i) {
+            float t = 0.f;
+            err = hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]);
+            ms[i] += t;
+        }
         if (err != hipSuccess) {
             rave::set_error(std::string("plan_op_times: ") + hipGetErrorString(err));
             return RAVE_ERR_HIP;
         }
-        ms[i] += t;
     }
-    return RAVE_OK;
+    plan->runs = 0;
+    return runs;
 }
 
 extern "C" int rave_plan_destroy(rave_plan* plan) {
@@ -130,11 +135,12 @@ extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, v
         char* base = static_cast<char*>(slots[r.slot]) + r.byte_offset;
         std::memcpy(plan->scratch[r.op].u.raw + r.field_offset, &base, sizeof(void*));
     }
-    const bool prof = !plan->ev.empty();
+    const bool prof = plan->runs < plan->runs_cap;   // armed and not yet full
+    hipEvent_t* ev = prof ? plan->ev.data() + (size_t)2 * plan->scratch.size() * plan->runs : nullptr;
     for (size_t i = 0; i < plan->scratch.size(); ++i) {
         const rave_plan_op& op = plan->scratch[i];
         int rc;
-        if (prof) (void)hipEventRecord(plan->ev[2 * i], static_cast<hipStream_t>(stream));
+        if (prof) rave::g_op_events = {ev[2 * i], ev[2 * i + 1]};
         switch (op.kind) {
             case RAVE_OP_CONV: rc = rave_conv1d(&op.u.conv, stream); break;
             case RAVE_OP_PQMF_ANALYSIS: rc = rave_pqmf_analysis(&op.u.ana, stream); break;
@@ -150,12 +156,18 @@ extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, v
                 rave::set_error("plan_run: unknown op kind " + std::to_string(op.kind));
                 return RAVE_ERR_STATE;
         }
+        if (prof) {
+            if (rave::g_op_events.start) {   // the op launched nothing: record an empty interval
+                (void)hipEventRecord(ev[2 * i], static_cast<hipStream_t>(stream));
+                (void)hipEventRecord(ev[2 * i + 1], static_cast<hipStream_t>(stream));
+            }
+            rave::g_op_events = {};
+        }
         if (rc != RAVE_OK) {
             rave::set_error("plan op " + std::to_string(i) + ": " + rave::g_err);
             return rc;
         }
-        if (prof) (void)hipEventRecord(plan->ev[2 * i + 1], static_cast<hipStream_t>(stream));
     }
-    plan->ran = true;
+    if (prof) ++plan->runs;
     return RAVE_OK;
 }

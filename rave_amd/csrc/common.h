@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -40,6 +41,28 @@ inline int launch_status(const char* what) {
 }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Per-op timing hook of the plan executor (rave_plan_profile).  While set, the
+// op's launches carry the events inside their own dispatch packets
+// (hipExtLaunchKernelGGL): the first launch takes the start event, every launch
+// re-records the stop event, so the op's time is first-kernel start to
+// last-kernel end with no marker packets between kernels.
+struct OpEvents {
+    hipEvent_t start = nullptr;
+    hipEvent_t stop = nullptr;
+};
+extern thread_local OpEvents g_op_events;
+
+template <typename K, typename... Args>
+inline void launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st, Args... args) {
+    OpEvents& e = g_op_events;
+    if (e.stop) {
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, st, e.start, e.stop, 0, args...);
+        e.start = nullptr;
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+    }
+}
 
 constexpr int ceil_div(int a, int b) { return (a + b - 1) / b; }
 constexpr int64_t ceil_div64(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -494,7 +494,7 @@ static int launch_k(ConvKArgs k, hipStream_t st) {
             d = true;
         }
     }
-    hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, st, k);
+    launch(kern, grid, dim3(kThreads), lds, st, k);
     return launch_status("conv1d_mfma_kernel");
 }
 
@@ -688,6 +688,6 @@ extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
     if (rc != RAVE_OK || k.S <= 1) return rc;
     int64_t total = (int64_t)k.B * k.M * k.U;
     int blocks = (int)std::min<int64_t>(ceil_div64(total, 256), 4096);
-    hipLaunchKernelGGL(conv1d_splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, k);
+    launch(conv1d_splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, k);
     return launch_status("conv1d_splitk_reduce_kernel");
 }

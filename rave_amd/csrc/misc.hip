@@ -168,7 +168,7 @@ extern "C" int rave_fill_channels(const rave_fill_args* p, void* stream) {
     RAVE_CHECK_ARG(p->batch > 0 && p->channels > 0 && p->t_len > 0, "fill_channels: empty shape");
     int64_t total = (int64_t)p->channels * p->t_len;
     int blocks = (int)std::min<int64_t>(ceil_div64(total, 256), 1024);
-    hipLaunchKernelGGL(fill_channels_kernel, dim3(blocks, p->batch), dim3(256), 0, as_stream(stream), *p);
+    launch(fill_channels_kernel, dim3(blocks, p->batch), dim3(256), 0, as_stream(stream), *p);
     return launch_status("fill_channels_kernel");
 }
 
@@ -177,7 +177,7 @@ extern "C" int rave_copy(const rave_copy_args* p, void* stream) {
     RAVE_CHECK_ARG(p->batch > 0 && p->channels > 0 && p->t_len > 0, "copy: empty shape");
     int64_t total = (int64_t)p->channels * p->t_len;
     int blocks = (int)std::min<int64_t>(ceil_div64(total, 256), 1024);
-    hipLaunchKernelGGL(copy_kernel, dim3(blocks, p->batch), dim3(256), 0, as_stream(stream), *p);
+    launch(copy_kernel, dim3(blocks, p->batch), dim3(256), 0, as_stream(stream), *p);
     return launch_status("copy_kernel");
 }
 
@@ -186,7 +186,7 @@ extern "C" int rave_shift_history(const rave_shift_args* p, void* stream) {
     RAVE_CHECK_ARG(p->t_new >= 1 && p->hist >= 0, "shift_history: bad sizes");
     if (p->hist == 0) return RAVE_OK;
     int rows = p->batch * p->channels;
-    hipLaunchKernelGGL(shift_history_kernel, dim3(ceil_div(rows, 256)), dim3(256), 0, as_stream(stream), *p);
+    launch(shift_history_kernel, dim3(ceil_div(rows, 256)), dim3(256), 0, as_stream(stream), *p);
     return launch_status("shift_history_kernel");
 }
 
@@ -197,8 +197,8 @@ extern "C" int rave_rvq_encode(const rave_rvq_args* p, void* stream) {
     int n_frames = p->batch * p->t_len;
     dim3 grid(ceil_div(n_frames, kFT));
     switch (p->dim) {
-        case 128: hipLaunchKernelGGL(rvq_encode_kernel<128>, grid, dim3(kRvqThreads), 0, as_stream(stream), *p, n_frames); break;
-        case 64: hipLaunchKernelGGL(rvq_encode_kernel<64>, grid, dim3(kRvqThreads), 0, as_stream(stream), *p, n_frames); break;
+        case 128: launch(rvq_encode_kernel<128>, grid, dim3(kRvqThreads), 0, as_stream(stream), *p, n_frames); break;
+        case 64: launch(rvq_encode_kernel<64>, grid, dim3(kRvqThreads), 0, as_stream(stream), *p, n_frames); break;
         default: set_error("rvq_encode: dim must be 64 or 128"); return RAVE_ERR_UNSUPPORTED;
     }
     return launch_status("rvq_encode_kernel");
@@ -209,6 +209,6 @@ extern "C" int rave_rvq_decode(const rave_rvq_args* p, void* stream) {
     RAVE_CHECK_ARG(p->n_q > 0 && p->dim > 0 && p->batch > 0 && p->t_len > 0, "rvq_decode: empty shape");
     int64_t total = (int64_t)p->dim * p->t_len;
     int blocks = (int)std::min<int64_t>(ceil_div64(total, 256), 1024);
-    hipLaunchKernelGGL(rvq_decode_kernel, dim3(blocks, p->batch), dim3(256), 0, as_stream(stream), *p);
+    launch(rvq_decode_kernel, dim3(blocks, p->batch), dim3(256), 0, as_stream(stream), *p);
     return launch_status("rvq_decode_kernel");
 }

@@ -85,11 +85,11 @@ extern "C" int rave_noise_synth(const rave_noise_args* p, void* stream) {
     RAVE_CHECK_ARG(a.target >= 2 * (a.noise_bands - 1), "noise_synth: target must be >= 2*(noise_bands-1)");
     dim3 grid(ceil_div(a.frames, kNoiseThreads), a.n_band, a.batch);
     if (a.noise_bands == 5 && a.target == 8)
-        hipLaunchKernelGGL((noise_synth_kernel<5, 8>), grid, dim3(kNoiseThreads), 0, as_stream(stream), a);
+        launch((noise_synth_kernel<5, 8>), grid, dim3(kNoiseThreads), 0, as_stream(stream), a);
     else if (a.noise_bands == 5 && a.target == 16)
-        hipLaunchKernelGGL((noise_synth_kernel<5, 16>), grid, dim3(kNoiseThreads), 0, as_stream(stream), a);
+        launch((noise_synth_kernel<5, 16>), grid, dim3(kNoiseThreads), 0, as_stream(stream), a);
     else if (a.noise_bands == 9 && a.target == 16)
-        hipLaunchKernelGGL((noise_synth_kernel<9, 16>), grid, dim3(kNoiseThreads), 0, as_stream(stream), a);
+        launch((noise_synth_kernel<9, 16>), grid, dim3(kNoiseThreads), 0, as_stream(stream), a);
     else {
         set_error("noise_synth: supported (noise_bands, target) are (5, 8), (5, 16), (9, 16)");
         return RAVE_ERR_UNSUPPORTED;

@@ -149,9 +149,9 @@ extern "C" int rave_pqmf_analysis(const rave_pqmf_analysis_args* p, void* stream
     size_t lds = (size_t)(a.n_out_bands * taps4 + wframes * kFrameStride) * sizeof(float);
     dim3 grid(ceil_div(a.t_out, kAnaT), a.batch);
     if (a.n_out_bands == 6)
-        hipLaunchKernelGGL(pqmf_analysis_kernel<6>, grid, dim3(kAnaT), lds, as_stream(stream), a, taps4, wframes);
+        launch(pqmf_analysis_kernel<6>, grid, dim3(kAnaT), lds, as_stream(stream), a, taps4, wframes);
     else
-        hipLaunchKernelGGL(pqmf_analysis_kernel<16>, grid, dim3(kAnaT), lds, as_stream(stream), a, taps4, wframes);
+        launch(pqmf_analysis_kernel<16>, grid, dim3(kAnaT), lds, as_stream(stream), a, taps4, wframes);
     return launch_status("pqmf_analysis_kernel");
 }
 
@@ -165,6 +165,6 @@ extern "C" int rave_pqmf_synthesis(const rave_pqmf_synthesis_args* p, void* stre
     int hrow = a.n_band * a.taps + 1;
     size_t lds = (size_t)(a.n_band * hrow + a.n_band * (kSynT + a.taps - 1)) * sizeof(float);
     dim3 grid(ceil_div(a.t_in, kSynT), a.batch);
-    hipLaunchKernelGGL(pqmf_synthesis_kernel, grid, dim3(256), lds, as_stream(stream), a, hrow);
+    launch(pqmf_synthesis_kernel, grid, dim3(256), lds, as_stream(stream), a, hrow);
     return launch_status("pqmf_synthesis_kernel");
 }

@@ -199,18 +199,22 @@ class Plan:
             stream = torch.cuda.current_stream().cuda_stream
         N.check(N.lib.rave_plan_run(self.handle, arr, len(slots), C.c_void_p(stream)), "plan_run")
 
-    def profile(self, enable: bool = True) -> None:
-        N.check(N.lib.rave_plan_profile(self.handle, int(enable)), "plan_profile")
+    def profile(self, runs: int = 1) -> None:
+        """Arm per-op timing for the next ``runs`` runs (0 disarms)."""
+        N.check(N.lib.rave_plan_profile(self.handle, int(runs)), "plan_profile")
 
-    def op_times(self, acc: Optional[np.ndarray] = None) -> np.ndarray:
-        """Add the last run's per-op milliseconds (HIP events) into ``acc``."""
+    def op_times(self, acc: Optional[np.ndarray] = None) -> Tuple[np.ndarray, int]:
+        """(per-op milliseconds summed over the recorded runs, added into ``acc``;
+        number of runs).  Re-arms the recorder."""
         n = len(self.sym)
         buf = (C.c_float * n)()
         if acc is not None:
             for i in range(n):
                 buf[i] = float(acc[i])
-        N.check(N.lib.rave_plan_op_times(self.handle, buf, n), "plan_op_times")
-        return np.array(list(buf), np.float64)
+        runs = N.lib.rave_plan_op_times(self.handle, buf, n)
+        if runs < 0:
+            N.check(runs, "plan_op_times")
+        return np.array(list(buf), np.float64), runs
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -291,7 +295,7 @@ class RAVE:
                       row0=self.adain_row0, x_sb=x.sb, x_sc=x.sc, y_sb=x.sb, y_sc=x.sc),
                  dict(x=x, y=x, stats=View("abs", st, 0, 0, elem=1),
                       counters=View("abs", cnt, 0, 0, elem=1), ticket=View("abs", tk, 0, 0, elem=1)),
-                 label=name)
+                 label="adain:" + name)
 
     # ------------------------------------------------------------ plan pieces
     def _conv(self, plan: Plan, n: ConvNode, B: int, t_in: int, src: View, dst: View,

@@ -1,0 +1,37 @@
+#!/bin/bash
+# One profiling pass of bench.py on the GPU box (run through gpurun):
+#   1. the plain bench line (with the CPU baseline),
+#   2. rocprofv3 --kernel-trace --stats of the same command (per-kernel times),
+#   3./4. separate --pmc FETCH_SIZE / WRITE_SIZE passes (HBM traffic; the two
+#      counters do not fit one gfx950 pass),
+# then tools/rocprof_summary.py.  Every GPU step has its own time limit and the
+# script stops at the first failure.
+set -e -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r01}
+OUT=$R/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+BENCH="$R/bench.py --steps 10 --warmup 3"
+timeout -k 10 300 python3 $BENCH > "$OUT/bench.json" 2> "$OUT/bench.err"
+echo "bench: $(cat $OUT/bench.json)"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
+    python3 $BENCH --no-cpu-baseline > "$OUT/bench_kt.json" 2> "$OUT/bench_kt.err"
+echo "kernel-trace pass done"
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run -- \
+    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
+echo "fetch pass done"
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run -- \
+    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile > "$OUT/bench_write.json" 2> "$OUT/bench_write.err"
+echo "write pass done"
+KT=$(find "$OUT/kt" -name '*kernel_trace.csv' | head -n 1)
+FE=$(find "$OUT/fetch" -name '*counter_collection.csv' | head -n 1)
+WR=$(find "$OUT/write" -name '*counter_collection.csv' | head -n 1)
+python3 "$R/tools/rocprof_summary.py" --trace "$KT" --fetch "$FE" --write "$WR" \
+    --bench "$OUT/bench_kt.json" --out "$OUT/summary.json" --traffic-out "$OUT/conv_traffic.json"
+find "$OUT" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
+# counter CSVs are large; keep the conv rows only
+for f in "$FE" "$WR"; do
+    head -n 1 "$f" > "$f.conv"; grep conv1d "$f" >> "$f.conv" || true; rm -f "$f"
+done
+ls -la "$OUT"
