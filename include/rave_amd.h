@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 2
+#define RAVE_ABI_VERSION 3
 
 /* ---------------------------------------------------------------- status */
 enum {
@@ -239,6 +239,30 @@ typedef struct rave_adain_args {
 } rave_adain_args;
 int rave_adain(const rave_adain_args* a, void* stream);
 
+/* ---------------------------------------------------------------- fused residual unit
+ * Residual(DilatedUnit(C, k=3, d)) in one kernel (rave/blocks.py:32-46, 84-113):
+ *   y = x + W2 . act(W1 *_d act(x) + b1) + b2
+ * W1: (C, C, 3) dilation d, padding (pad_left, 2d - pad_left) -- centered d, causal 2d;
+ * W2: (C, C, 1).  act is the unit's activation (LeakyReLU slope / Snake with
+ * alpha0 before W1 and alpha2 before W2).  weight = rave_unit_pack_weight
+ * layout (rave_unit_packed_size floats).  C in {64, 128, 256, 512}; other
+ * widths return RAVE_ERR_UNSUPPORTED (callers use two rave_conv1d calls).
+ * y must not alias x.
+ */
+typedef struct rave_unit_args {
+    int32_t channels, batch, t_len, dilation;
+    int32_t pad_left, act;
+    float leaky_slope; int32_t _pad0;
+    const float* x; int64_t x_sb, x_sc;
+    float* y;       int64_t y_sb, y_sc;
+    const float* weight;
+    const float* bias1; const float* bias2;
+    const float* alpha0; const float* alpha2;
+} rave_unit_args;
+int64_t rave_unit_packed_size(int channels);
+int rave_unit_pack_weight(const float* w1, const float* w2, int channels, float* packed);
+int rave_residual_unit(const rave_unit_args* a, void* stream);
+
 /* ---------------------------------------------------------------- plans
  * A plan is a recorded sequence of the ops above (the module graph of
  * RAVE.encode/decode).  Pointer fields inside an op's args may be relocated at
@@ -256,7 +280,8 @@ enum {
     RAVE_OP_SHIFT_HISTORY = 7,
     RAVE_OP_COPY = 8,
     RAVE_OP_NOISE = 9,
-    RAVE_OP_ADAIN = 10
+    RAVE_OP_ADAIN = 10,
+    RAVE_OP_UNIT = 11
 };
 
 #define RAVE_OP_PAYLOAD 240
@@ -272,6 +297,7 @@ typedef struct rave_plan_op {
         rave_copy_args copy;
         rave_noise_args noise;
         rave_adain_args adain;
+        rave_unit_args unit;
         unsigned char raw[RAVE_OP_PAYLOAD];
     } u;
 } rave_plan_op;

@@ -34,7 +34,8 @@ OP_SHIFT_HISTORY = 7
 OP_COPY = 8
 OP_NOISE = 9
 OP_ADAIN = 10
-ABI_VERSION = 2
+OP_UNIT = 11
+ABI_VERSION = 3
 
 i32, i64, f32, vp = C.c_int32, C.c_int64, C.c_float, C.c_void_p
 
@@ -108,6 +109,14 @@ class AdainArgs(C.Structure):
                 ("stats", vp), ("counters", vp), ("ticket", vp)]
 
 
+class UnitArgs(C.Structure):
+    _fields_ = [("channels", i32), ("batch", i32), ("t_len", i32), ("dilation", i32),
+                ("pad_left", i32), ("act", i32), ("leaky_slope", f32), ("_pad0", i32),
+                ("x", vp), ("x_sb", i64), ("x_sc", i64),
+                ("y", vp), ("y_sb", i64), ("y_sc", i64),
+                ("weight", vp), ("bias1", vp), ("bias2", vp), ("alpha0", vp), ("alpha2", vp)]
+
+
 PAYLOAD = 240
 
 
@@ -121,7 +130,7 @@ class Reloc(C.Structure):
 
 
 STRUCTS = [ConvArgs, AnalysisArgs, SynthesisArgs, FillArgs, RvqArgs, ShiftArgs, PlanOp, Reloc,
-           CopyArgs, NoiseArgs, AdainArgs]
+           CopyArgs, NoiseArgs, AdainArgs, UnitArgs]
 
 # every exported symbol of include/rave_amd.h
 EXPORTS = [
@@ -130,6 +139,7 @@ EXPORTS = [
     "rave_conv1d_workspace",
     "rave_pqmf_analysis", "rave_pqmf_synthesis", "rave_fill_channels", "rave_copy",
     "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
+    "rave_unit_packed_size", "rave_unit_pack_weight", "rave_residual_unit",
     "rave_plan_create", "rave_plan_run", "rave_plan_destroy", "rave_plan_size",
     "rave_plan_profile", "rave_plan_op_times",
 ]
@@ -153,12 +163,16 @@ def _load():
     lib.rave_conv1d_packed_size.restype = i64
     lib.rave_conv1d_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
     lib.rave_conv1d_workspace.argtypes = [C.POINTER(ConvArgs)]
+    lib.rave_unit_packed_size.argtypes = [C.c_int]
+    lib.rave_unit_packed_size.restype = i64
+    lib.rave_unit_pack_weight.argtypes = [vp, vp, C.c_int, vp]
     lib.rave_conv1d_workspace.restype = i64
     for name, st in [("rave_conv1d", ConvArgs), ("rave_pqmf_analysis", AnalysisArgs),
                      ("rave_pqmf_synthesis", SynthesisArgs), ("rave_fill_channels", FillArgs),
                      ("rave_rvq_encode", RvqArgs), ("rave_rvq_decode", RvqArgs),
                      ("rave_shift_history", ShiftArgs), ("rave_copy", CopyArgs),
-                     ("rave_noise_synth", NoiseArgs), ("rave_adain", AdainArgs)]:
+                     ("rave_noise_synth", NoiseArgs), ("rave_adain", AdainArgs),
+                     ("rave_residual_unit", UnitArgs)]:
         getattr(lib, name).argtypes = [C.POINTER(st), vp]
     lib.rave_plan_create.argtypes = [C.POINTER(PlanOp), C.c_int, C.POINTER(Reloc), C.c_int,
                                      C.POINTER(vp)]
@@ -213,6 +227,26 @@ def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed, out_s
     out = np.empty(n, np.float32)
     check(lib.rave_conv1d_pack_weight(w.ctypes.data, c_in, c_out, kernel, stride, dilation,
                                       int(transposed), int(out_shift), out.ctypes.data), "pack_weight")
+    return out
+
+
+def unit_supported(channels: int) -> bool:
+    return int(lib.rave_unit_packed_size(int(channels))) > 0
+
+
+def pack_unit_weight(w1, w2, channels):
+    """Fused residual unit weights: W1 (C, C, 3) and W2 (C, C, 1) -> packed float32."""
+    import numpy as np
+    n = int(lib.rave_unit_packed_size(int(channels)))
+    if n <= 0:
+        raise NotImplementedError(f"fused residual unit does not support C={channels}")
+    w1 = np.ascontiguousarray(w1, dtype=np.float32)
+    w2 = np.ascontiguousarray(w2, dtype=np.float32)
+    if w1.shape != (channels, channels, 3) or w2.reshape(channels, channels).shape != (channels, channels):
+        raise ValueError("unit weights must be (C, C, 3) and (C, C, 1)")
+    out = np.empty(n, np.float32)
+    check(lib.rave_unit_pack_weight(w1.ctypes.data, w2.ctypes.data, int(channels), out.ctypes.data),
+          "unit_pack_weight")
     return out
 
 

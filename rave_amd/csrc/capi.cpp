@@ -35,7 +35,7 @@ extern "C" int rave_struct_sizes(int64_t* out, int n) {
         (int64_t)sizeof(rave_rvq_args),          (int64_t)sizeof(rave_shift_args),
         (int64_t)sizeof(rave_plan_op),           (int64_t)sizeof(rave_reloc),
         (int64_t)sizeof(rave_copy_args),         (int64_t)sizeof(rave_noise_args),
-        (int64_t)sizeof(rave_adain_args),
+        (int64_t)sizeof(rave_adain_args),        (int64_t)sizeof(rave_unit_args),
     };
     const int cnt = (int)(sizeof(sizes) / sizeof(sizes[0]));
     if (!out) return cnt;
@@ -152,6 +152,7 @@ extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, v
             case RAVE_OP_COPY: rc = rave_copy(&op.u.copy, stream); break;
             case RAVE_OP_NOISE: rc = rave_noise_synth(&op.u.noise, stream); break;
             case RAVE_OP_ADAIN: rc = rave_adain(&op.u.adain, stream); break;
+            case RAVE_OP_UNIT: rc = rave_residual_unit(&op.u.unit, stream); break;
             default:
                 rave::set_error("plan_run: unknown op kind " + std::to_string(op.kind));
                 return RAVE_ERR_STATE;

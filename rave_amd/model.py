@@ -229,7 +229,7 @@ class RAVE:
 
     def __init__(self, cfg: RaveConfig, params: Mapping[str, np.ndarray], speaker: np.ndarray,
                  device=None, hk: Optional[np.ndarray] = None,
-                 adain_stats: Optional[Mapping] = None):
+                 adain_stats: Optional[Mapping] = None, fuse_units: bool = True):
         check_params(cfg, params)
         self.cfg = cfg
         self.graph = build_graph(cfg)
@@ -249,6 +249,13 @@ class RAVE:
             bo = ar.add(params[n.name + ".bias"]) if n.bias else None
             ao = ar.add(params[n.alpha]) if n.act == "snake" else None
             self.w_off[n.name] = (wo, bo, ao)
+        # fused Residual(DilatedUnit) weights: (k=3 node name) -> arena offset
+        self.unit_off: Dict[str, int] = {}
+        if fuse_units:
+            for k3, k1 in self._unit_pairs(self.graph.convs()):
+                if N.unit_supported(k3.c_in):
+                    self.unit_off[k3.name] = ar.add(N.pack_unit_weight(
+                        conv_weight(k3, params), conv_weight(k1, params), k3.c_in))
         self.noise_target = int(np.prod(cfg.noise.ratios)) if cfg.noise is not None else 0
         self.hk = P.design_bank(cfg.pqmf_attenuation, cfg.n_band) if hk is None else np.asarray(hk, np.float32)
         hkf, hki = P.kernels(self.hk)
@@ -278,6 +285,35 @@ class RAVE:
                 self.adain.load(adain_stats)
         elif adain_stats:
             raise ValueError("adain_stats given for a config without AdaIN")
+
+    @staticmethod
+    def _unit_pairs(nodes: List[ConvNode]) -> List[Tuple[ConvNode, ConvNode]]:
+        """(k=3 dilated conv, 1x1 conv) pairs forming Residual(DilatedUnit)
+        (rave/blocks.py:32-46, 84-113): the 1x1 reads the k=3 output and adds
+        the k=3 input back."""
+        out = []
+        for a, b in zip(nodes, nodes[1:]):
+            if (a.kernel == 3 and a.stride == 1 and not a.transposed and b.kernel == 1
+                    and b.src == a.dst and b.residual == a.src and a.c_in == a.c_out == b.c_out
+                    and a.act == b.act and a.bias == b.bias):
+                out.append((a, b))
+        return out
+
+    def _unit(self, plan: Plan, k3: ConvNode, k1: ConvNode, B: int, T: int, src: View,
+              dst: View) -> None:
+        wo = self.unit_off[k3.name]
+        _, b1, a0 = self.w_off[k3.name]
+        _, b2, a2 = self.w_off[k1.name]
+        arena = lambda o: View("arena", o, 0, 0) if o is not None else None  # noqa: E731
+        C = k3.c_in
+        plan.add(N.OP_UNIT, N.UnitArgs,
+                 dict(channels=C, batch=B, t_len=T, dilation=k3.dilation, pad_left=k3.pad[0],
+                      act=N.ACT[k3.act], leaky_slope=self.cfg.leaky_slope,
+                      x_sb=src.sb, x_sc=src.sc, y_sb=dst.sb, y_sc=dst.sc),
+                 dict(x=src, y=dst, weight=arena(wo), bias1=arena(b1), bias2=arena(b2),
+                      alpha0=arena(a0), alpha2=arena(a2)),
+                 label=k3.name.rsplit(".net.", 1)[0] + ".unit",
+                 flops=2.0 * B * T * C * C * 4)
 
     def _adain_key(self) -> tuple:
         return self.adain.key() + (self.adain_row0,) if self.adain is not None else ()
@@ -331,10 +367,31 @@ class RAVE:
             if n.residual:
                 last_use[n.residual] = i
         tensors: Dict[str, Tuple[View, int, int]] = {k: (v, t, -1) for k, (v, t) in inputs.items()}
+        fused = {a.name: b for a, b in self._unit_pairs(nodes) if a.name in self.unit_off}
+        skip = set()
         for i, n in enumerate(nodes):
+            if n.name in skip:
+                continue
             src, t_in, _ = tensors[n.src]
             if n.adain and self.adain is not None and self.adain.active:
                 self._adain_op(plan, n.adain, B, n.c_in, t_in, src)
+            if n.name in fused:
+                # Residual(DilatedUnit) in one kernel; the k=3 output never exists in HBM
+                k1 = fused[n.name]
+                skip.add(k1.name)
+                if k1.dst in outputs:
+                    dst, size = outputs[k1.dst], -1
+                else:
+                    size = B * k1.c_out * t_in
+                    dst = View("ws", plan.ws.alloc(size), k1.c_out * t_in, t_in)
+                self._unit(plan, n, k1, B, t_in, src, dst)
+                tensors[k1.dst] = (dst, t_in, size)
+                for name in {n.src}:
+                    if last_use.get(name) == i + 1 and name in tensors:
+                        v, _, sz = tensors[name]
+                        if sz > 0 and v.slot == "ws" and name not in outputs:
+                            plan.ws.release(v.off, sz)
+                continue
             t_out = n.out_len(t_in)
             if n.dst in outputs:
                 dst = outputs[n.dst]

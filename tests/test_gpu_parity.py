@@ -5,6 +5,7 @@ Tolerances: the north star is <= 1e-4 max-abs vs the reference fp32 CPU path
 on model outputs; single layers are checked at 2e-5 relative to max|ref|
 (fp32 accumulation over K <= 3072 against a float64 oracle)."""
 import ctypes as C
+import ctypes as C_
 import os
 
 import numpy as np
@@ -472,3 +473,70 @@ def test_no_amplitude_modulation_epilogue(dev):
     torch.cuda.synchronize()
     o = Oracle(cfg, params, spk, hk=m.hk)
     assert maxabs(y.cpu().numpy(), o.forward(x)) < TOL
+
+
+# ------------------------------------------------------------------ fused Residual(DilatedUnit)
+UNIT_CASES = [
+    # C, d, act, causal, B, T
+    (64, 1, "leaky", False, 2, 4096),
+    (64, 9, "leaky", False, 2, 1000),
+    (64, 3, "snake", True, 1, 300),
+    (128, 3, "leaky", False, 3, 1024),
+    (128, 9, "snake", False, 2, 200),
+    (256, 1, "leaky", False, 2, 256),
+    (256, 9, "snake", True, 2, 77),
+    (512, 3, "leaky", False, 2, 128),
+    (512, 1, "snake", False, 1, 40),
+]
+
+
+@pytest.mark.parametrize("case", UNIT_CASES, ids=[str(c) for c in UNIT_CASES])
+def test_residual_unit_kernel(N, dev, case):
+    """rave_residual_unit == x + conv1x1(act(conv3_d(act(x)) + b1)) + b2 (oracle, float64)."""
+    from oracle.rave_oracle import conv1d, leaky_relu, snake
+    C, d, act, causal, B, T = case
+    rng = np.random.default_rng(C + d)
+    x = rng.standard_normal((B, C, T)).astype(np.float32)
+    w1 = (rng.standard_normal((C, C, 3)) / np.sqrt(3 * C)).astype(np.float32)
+    w2 = (rng.standard_normal((C, C, 1)) / np.sqrt(C)).astype(np.float32)
+    b1 = rng.standard_normal(C).astype(np.float32) * 0.1
+    b2 = rng.standard_normal(C).astype(np.float32) * 0.1
+    a0 = (1 + 0.3 * rng.standard_normal(C)).astype(np.float32)
+    a2 = (1 + 0.3 * rng.standard_normal(C)).astype(np.float32)
+    pad = (2 * d, 0) if causal else (d, d)
+    f = (lambda v, al: snake(v, al.reshape(-1, 1))) if act == "snake" else (lambda v, al: leaky_relu(v, 0.2))
+    h = f(conv1d(f(x.astype(np.float64), a0), w1, b1, 1, d, pad), a2)
+    ref = x + conv1d(h, w2, b2, 1, 1, (0, 0))
+    packed = torch.from_numpy(N.pack_unit_weight(w1, w2, C)).to(dev)
+    xd = torch.from_numpy(x).to(dev)
+    y = torch.full_like(xd, float("nan"))
+    dd = {k: torch.from_numpy(v).to(dev) for k, v in dict(b1=b1, b2=b2, a0=a0, a2=a2).items()}
+    a = N.UnitArgs(channels=C, batch=B, t_len=T, dilation=d, pad_left=pad[0], act=N.ACT[act],
+                   leaky_slope=0.2, x=xd.data_ptr(), x_sb=C * T, x_sc=T, y=y.data_ptr(), y_sb=C * T,
+                   y_sc=T, weight=packed.data_ptr(), bias1=dd["b1"].data_ptr(), bias2=dd["b2"].data_ptr(),
+                   alpha0=dd["a0"].data_ptr() if act == "snake" else None,
+                   alpha2=dd["a2"].data_ptr() if act == "snake" else None)
+    N.check(N.lib.rave_residual_unit(C_.byref(a), C_.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    got = y.cpu().numpy()
+    assert np.isfinite(got).all()
+    assert maxabs(got, ref) <= 2e-5 * max(1.0, float(np.abs(ref).max()))
+
+
+def test_fused_units_match_unfused_model(dev):
+    """The v2 plan with fused residual units equals the conv-by-conv plan."""
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.v2()
+    params, spk = init_params(cfg, 0), init_speaker(cfg, 0)
+    mf = RAVE(cfg, params, spk, device=dev)
+    mu = RAVE(cfg, params, spk, device=dev, fuse_units=False)
+    assert len(mf.unit_off) == 22 and not mu.unit_off
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = (0.1 * torch.randn(4, 1, 65536, generator=g)).to(dev)
+    zf, zu = mf.encode(x), mu.encode(x)
+    yf, yu = mf.decode(zf), mu.decode(zf)
+    torch.cuda.synchronize()
+    assert float((zf - zu).abs().max()) < 1e-4
+    assert float((yf - yu).abs().max()) < 1e-4
