@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
     ap.add_argument("--samples", type=int, default=65536, help="samples per clip")
     ap.add_argument("--config", default="v2")
+    ap.add_argument("--precision", default="f32", choices=["f32", "split16", "auto"],
+                    help="conv/unit GEMM arithmetic (include/rave_amd.h RAVE_PREC_*)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
@@ -117,7 +119,7 @@ def main():
     cfg = rcfg.get_config(a.config)
     params = init_params(cfg, seed=0)
     spk = init_speaker(cfg, seed=0)
-    model = RAVE(cfg, params, spk, device=dev)
+    model = RAVE(cfg, params, spk, device=dev, precision=a.precision)
     B, T = a.batch, a.samples
     Fz = T // cfg.hop
     x = torch.from_numpy(synth_batch(B, T, 1000 * rank)).to(dev)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 3
+#define RAVE_ABI_VERSION 4
 
 /* ---------------------------------------------------------------- status */
 enum {
@@ -53,6 +53,20 @@ enum {
 
 /* activation applied to a conv INPUT (fused prologue) */
 enum { RAVE_ACT_NONE = 0, RAVE_ACT_LEAKY = 1, RAVE_ACT_SNAKE = 2 };
+
+/* arithmetic of the conv / unit GEMMs (the `precision` field of their args):
+ *   RAVE_PREC_F32      v_mfma_f32_32x32x2_f32: exact fp32 (k-ordered fmaf chain).
+ *   RAVE_PREC_SPLIT16  every fp32 operand split exactly-ish into an f16 pair
+ *                      (hi = f16(v), lo = f16((v - hi) * 2^11); weights pre-scaled
+ *                      per output row by a power of two), three
+ *                      v_mfma_f32_32x32x16_f16 products hi*hi*2^11 + hi*lo + lo*hi
+ *                      into one fp32 accumulator, exact power-of-two unscale in the
+ *                      epilogue.  Operand representation error <= ~2^-23 relative,
+ *                      products exact in fp32; measured layer error within 1.5x of
+ *                      the fp32 path.  Requires |act(x)| < 65504 (f16 range);
+ *                      5.3x the fp32 MFMA rate.  Weights must be packed with the
+ *                      *_split_* packers. */
+enum { RAVE_PREC_F32 = 0, RAVE_PREC_SPLIT16 = 1 };
 
 const char* rave_last_error(void);
 int rave_abi_version(void);
@@ -86,7 +100,7 @@ typedef struct rave_conv1d_args {
     int32_t batch;
     int32_t t_in;           /* input length (columns of x)                       */
     int32_t t_out;          /* output length (columns of y)                      */
-    int32_t _pad0;
+    int32_t precision;      /* RAVE_PREC_*                                       */
     const float* x;       int64_t x_sb, x_sc;
     float* y;             int64_t y_sb, y_sc;
     const float* residual; int64_t r_sb, r_sc;   /* NULL = none                  */
@@ -113,6 +127,13 @@ int rave_conv1d_pack_weight(const float* w, int c_in, int c_out, int kernel, int
                             int dilation, int transposed, int out_shift, float* packed);
 /* floats of split-K workspace the launcher would use for these args (0 = none) */
 int64_t rave_conv1d_workspace(const rave_conv1d_args* a);
+/* RAVE_PREC_SPLIT16 weight image: per K-chunk, per 32-row block, per K-step of
+ * 16, the (hi, lo) f16 MFMA A-fragments in lane order, then one float row scale
+ * per padded GEMM row.  Sizes in floats (4-byte units). */
+int64_t rave_conv1d_split_packed_size(int c_in, int c_out, int kernel, int stride, int dilation,
+                                      int transposed);
+int rave_conv1d_split_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
+                                  int dilation, int transposed, int out_shift, float* packed);
 int rave_conv1d(const rave_conv1d_args* a, void* stream);
 
 /* ---------------------------------------------------------------- PQMF
@@ -252,7 +273,7 @@ int rave_adain(const rave_adain_args* a, void* stream);
 typedef struct rave_unit_args {
     int32_t channels, batch, t_len, dilation;
     int32_t pad_left, act;
-    float leaky_slope; int32_t _pad0;
+    float leaky_slope; int32_t precision;   /* RAVE_PREC_* */
     const float* x; int64_t x_sb, x_sc;
     float* y;       int64_t y_sb, y_sc;
     const float* weight;
@@ -261,6 +282,12 @@ typedef struct rave_unit_args {
 } rave_unit_args;
 int64_t rave_unit_packed_size(int channels);
 int rave_unit_pack_weight(const float* w1, const float* w2, int channels, float* packed);
+/* RAVE_PREC_SPLIT16 unit weights (C in {64, 128}): (hi, lo) f16 A-fragments of
+ * W1 then W2 per 32-row block and 16-deep K-step, then the two row-scale
+ * vectors.  Other widths return -1 / RAVE_ERR_UNSUPPORTED (run the unit as two
+ * split16 rave_conv1d calls). */
+int64_t rave_unit_split_packed_size(int channels);
+int rave_unit_split_pack_weight(const float* w1, const float* w2, int channels, float* packed);
 int rave_residual_unit(const rave_unit_args* a, void* stream);
 
 /* ---------------------------------------------------------------- plans

@@ -35,7 +35,12 @@ OP_COPY = 8
 OP_NOISE = 9
 OP_ADAIN = 10
 OP_UNIT = 11
-ABI_VERSION = 3
+ABI_VERSION = 4
+
+# GEMM arithmetic of conv / unit ops (include/rave_amd.h RAVE_PREC_*)
+PREC_F32 = 0
+PREC_SPLIT16 = 1
+PRECISION = {"f32": PREC_F32, "split16": PREC_SPLIT16}
 
 i32, i64, f32, vp = C.c_int32, C.c_int64, C.c_float, C.c_void_p
 
@@ -44,7 +49,7 @@ class ConvArgs(C.Structure):
     _fields_ = [("c_in", i32), ("c_out", i32), ("kernel", i32), ("stride", i32), ("dilation", i32),
                 ("pad_left", i32), ("pad_right", i32), ("transposed", i32), ("out_shift", i32),
                 ("act", i32), ("leaky_slope", f32), ("batch", i32), ("t_in", i32), ("t_out", i32),
-                ("_pad0", i32),
+                ("precision", i32),
                 ("x", vp), ("x_sb", i64), ("x_sc", i64),
                 ("y", vp), ("y_sb", i64), ("y_sc", i64),
                 ("residual", vp), ("r_sb", i64), ("r_sc", i64),
@@ -111,7 +116,7 @@ class AdainArgs(C.Structure):
 
 class UnitArgs(C.Structure):
     _fields_ = [("channels", i32), ("batch", i32), ("t_len", i32), ("dilation", i32),
-                ("pad_left", i32), ("act", i32), ("leaky_slope", f32), ("_pad0", i32),
+                ("pad_left", i32), ("act", i32), ("leaky_slope", f32), ("precision", i32),
                 ("x", vp), ("x_sb", i64), ("x_sc", i64),
                 ("y", vp), ("y_sb", i64), ("y_sc", i64),
                 ("weight", vp), ("bias1", vp), ("bias2", vp), ("alpha0", vp), ("alpha2", vp)]
@@ -136,10 +141,11 @@ STRUCTS = [ConvArgs, AnalysisArgs, SynthesisArgs, FillArgs, RvqArgs, ShiftArgs, 
 EXPORTS = [
     "rave_last_error", "rave_abi_version", "rave_struct_sizes",
     "rave_conv1d_chunk", "rave_conv1d_packed_size", "rave_conv1d_pack_weight", "rave_conv1d",
-    "rave_conv1d_workspace",
+    "rave_conv1d_workspace", "rave_conv1d_split_packed_size", "rave_conv1d_split_pack_weight",
     "rave_pqmf_analysis", "rave_pqmf_synthesis", "rave_fill_channels", "rave_copy",
     "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
     "rave_unit_packed_size", "rave_unit_pack_weight", "rave_residual_unit",
+    "rave_unit_split_packed_size", "rave_unit_split_pack_weight",
     "rave_plan_create", "rave_plan_run", "rave_plan_destroy", "rave_plan_size",
     "rave_plan_profile", "rave_plan_op_times",
 ]
@@ -163,9 +169,15 @@ def _load():
     lib.rave_conv1d_packed_size.restype = i64
     lib.rave_conv1d_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
     lib.rave_conv1d_workspace.argtypes = [C.POINTER(ConvArgs)]
+    lib.rave_conv1d_split_packed_size.argtypes = [C.c_int] * 6
+    lib.rave_conv1d_split_packed_size.restype = i64
+    lib.rave_conv1d_split_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
     lib.rave_unit_packed_size.argtypes = [C.c_int]
     lib.rave_unit_packed_size.restype = i64
     lib.rave_unit_pack_weight.argtypes = [vp, vp, C.c_int, vp]
+    lib.rave_unit_split_packed_size.argtypes = [C.c_int]
+    lib.rave_unit_split_packed_size.restype = i64
+    lib.rave_unit_split_pack_weight.argtypes = [vp, vp, C.c_int, vp]
     lib.rave_conv1d_workspace.restype = i64
     for name, st in [("rave_conv1d", ConvArgs), ("rave_pqmf_analysis", AnalysisArgs),
                      ("rave_pqmf_synthesis", SynthesisArgs), ("rave_fill_channels", FillArgs),
@@ -213,40 +225,48 @@ def conv_chunk(c_in, kernel, stride, dilation, transposed) -> int:
     return int(lib.rave_conv1d_chunk(c_in, kernel, stride, dilation, int(transposed)))
 
 
-def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift=None):
-    """Host repack (numpy float32, torch layout) -> packed numpy float32.
+def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift=None,
+                     precision=PREC_F32):
+    """Host repack (numpy float32, torch layout) -> packed numpy float32 (for
+    PREC_SPLIT16 a byte image of f16 fragments + row scales, in 4-byte units).
     ``out_shift`` (ConvTranspose only): stride//2 for torch padding r//2 (default),
     0 for the cached streaming form."""
     if out_shift is None:
         out_shift = stride // 2 if transposed else 0
     import numpy as np
     w = np.ascontiguousarray(w, dtype=np.float32)
-    n = int(lib.rave_conv1d_packed_size(c_in, c_out, kernel, stride, dilation, int(transposed)))
+    size_fn, pack_fn = ((lib.rave_conv1d_packed_size, lib.rave_conv1d_pack_weight)
+                        if precision == PREC_F32 else
+                        (lib.rave_conv1d_split_packed_size, lib.rave_conv1d_split_pack_weight))
+    n = int(size_fn(c_in, c_out, kernel, stride, dilation, int(transposed)))
     if n <= 0:
         raise NotImplementedError(f"unsupported conv shape c_in={c_in} k={kernel} s={stride} d={dilation}")
-    out = np.empty(n, np.float32)
-    check(lib.rave_conv1d_pack_weight(w.ctypes.data, c_in, c_out, kernel, stride, dilation,
-                                      int(transposed), int(out_shift), out.ctypes.data), "pack_weight")
+    out = np.zeros(n, np.float32)
+    check(pack_fn(w.ctypes.data, c_in, c_out, kernel, stride, dilation,
+                  int(transposed), int(out_shift), out.ctypes.data), "pack_weight")
     return out
 
 
-def unit_supported(channels: int) -> bool:
-    return int(lib.rave_unit_packed_size(int(channels))) > 0
+def unit_supported(channels: int, precision: int = PREC_F32) -> bool:
+    size_fn = lib.rave_unit_packed_size if precision == PREC_F32 else lib.rave_unit_split_packed_size
+    return int(size_fn(int(channels))) > 0
 
 
-def pack_unit_weight(w1, w2, channels):
-    """Fused residual unit weights: W1 (C, C, 3) and W2 (C, C, 1) -> packed float32."""
+def pack_unit_weight(w1, w2, channels, precision=PREC_F32):
+    """Fused residual unit weights: W1 (C, C, 3) and W2 (C, C, 1) -> packed float32
+    (PREC_SPLIT16: f16 fragment image + row scales, in 4-byte units)."""
     import numpy as np
-    n = int(lib.rave_unit_packed_size(int(channels)))
+    size_fn, pack_fn = ((lib.rave_unit_packed_size, lib.rave_unit_pack_weight) if precision == PREC_F32
+                        else (lib.rave_unit_split_packed_size, lib.rave_unit_split_pack_weight))
+    n = int(size_fn(int(channels)))
     if n <= 0:
         raise NotImplementedError(f"fused residual unit does not support C={channels}")
     w1 = np.ascontiguousarray(w1, dtype=np.float32)
     w2 = np.ascontiguousarray(w2, dtype=np.float32)
     if w1.shape != (channels, channels, 3) or w2.reshape(channels, channels).shape != (channels, channels):
         raise ValueError("unit weights must be (C, C, 3) and (C, C, 1)")
-    out = np.empty(n, np.float32)
-    check(lib.rave_unit_pack_weight(w1.ctypes.data, w2.ctypes.data, int(channels), out.ctypes.data),
-          "unit_pack_weight")
+    out = np.zeros(n, np.float32)
+    check(pack_fn(w1.ctypes.data, w2.ctypes.data, int(channels), out.ctypes.data), "unit_pack_weight")
     return out
 
 

@@ -1,0 +1,775 @@
+// Split-f16 implicit-GEMM Conv1d / ConvTranspose1d on gfx950
+// (RAVE_PREC_SPLIT16, include/rave_amd.h): the same operator as conv1d.hip --
+// cached_conv's Conv1d / ConvTranspose1d forward at every call site of
+// rave/blocks.py (DilatedUnit :96-106, EncoderV2 :533-584, GeneratorV2
+// :631-677, NoiseGeneratorV2 :257-266) fused with the preceding activation and
+// the Residual add (rave/blocks.py:44-46) -- computed on the f16 matrix cores.
+//
+// Arithmetic.  Every fp32 operand v becomes an f16 pair hi = f16(v),
+// lo = f16((v - hi) * 2^11); weights are first scaled per GEMM row by 2^e_m
+// (max |w'| in [8, 16)).  One fp32 accumulator takes
+//     (hi_w * 2^11) * hi_x  +  hi_w * lo_x  +  lo_w * hi_x
+// (three v_mfma_f32_32x32x16_f16, 32 cycles each per 16-deep K-step, against
+// eight 64-cycle v_mfma_f32_32x32x2_f32 for the same K in fp32: 5.3x the
+// rate).  f16 x f16 products are exact in fp32; the dropped lo*lo term and the
+// two roundings are ~2^-22 relative; the epilogue multiplies by 2^-(e_m+11)
+// exactly.  Result error is on par with the fp32 MFMA path (tests).
+//
+// GEMM view: Y[m, n] = sum_kk W[m, kk] X[kk, n], kk = (tap q, virtual channel).
+// Strided convs (k = 2s, stride s) run polyphase: virtual channel (ci, p) at
+// window row u is x[ci][u*s + p - pad], tap q reads row n + q, so every family
+// is a stride-1 conv over rows of the staged window:
+//     k1: 1 tap       k3: 3 taps at row shift d      k7: 7 taps
+//     k4 s2 / k8 s4: 2 taps over (ci, phase)         ConvT: 2 taps (u-1|u, u|u+1)
+// Per K-chunk (VC virtual channels x all taps) a workgroup stages in LDS:
+//   * the weight image of its BM rows: (hi, lo) A-fragments in lane order,
+//     host-packed, copied by LDS-DMA (global_load_lds_dwordx4), no VGPRs;
+//   * the activation window [rows][VC] channels-last as two f16 planes (hi, lo),
+//     activation applied and split once per element on the way in, so each
+//     B-fragment (8 channels of one column) is one ds_read_b128.
+// Double-buffered (one barrier per chunk): chunk c+2's loads are in flight
+// while chunk c+1 is multiplied.  Each wave owns a 64x64 output tile (2x2
+// blocks of 32x32).  Split-K over grid.z for short-N layers (fp32 slabs,
+// fixed-order reduce: deterministic).
+#include "conv_shared.h"
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+namespace rave {
+
+typedef _Float16 s_h8 __attribute__((ext_vector_type(8)));
+typedef float s_f32x8 __attribute__((ext_vector_type(8)));
+typedef float s_f32x4 __attribute__((ext_vector_type(4)));
+
+// (taps after polyphase Q, phases S, virtual channels per chunk VC, max row shift)
+template <int KT> struct SFam;
+template <> struct SFam<1> { static constexpr int Q = 1, S = 1, VC = 32, DMAX = 0; };
+template <> struct SFam<2> { static constexpr int Q = 2, S = 1, VC = 16, DMAX = 1; };   // ConvT
+template <> struct SFam<3> { static constexpr int Q = 3, S = 1, VC = 16, DMAX = kMaxDil; };
+template <> struct SFam<4> { static constexpr int Q = 2, S = 2, VC = 16, DMAX = 1; };
+template <> struct SFam<7> { static constexpr int Q = 7, S = 1, VC = 16, DMAX = 1; };
+template <> struct SFam<8> { static constexpr int Q = 2, S = 4, VC = 16, DMAX = 1; };
+
+template <int KT> struct SInfo {
+    static constexpr int Q = SFam<KT>::Q, S = SFam<KT>::S, VC = SFam<KT>::VC;
+    static constexpr int KSC = Q * VC / 16;        // 16-deep K-steps per chunk
+    static constexpr int CPC = VC / S;             // real input channels per chunk
+};
+
+static inline int split_cpc(int taps) {
+    switch (taps) {
+        case 1: return SInfo<1>::CPC;
+        case 2: return SInfo<2>::CPC;
+        case 3: return SInfo<3>::CPC;
+        case 4: return SInfo<4>::CPC;
+        case 7: return SInfo<7>::CPC;
+        case 8: return SInfo<8>::CPC;
+        default: return 0;
+    }
+}
+static inline int split_ksc(int taps) {
+    switch (taps) {
+        case 1: return SInfo<1>::KSC;
+        case 2: return SInfo<2>::KSC;
+        case 3: return SInfo<3>::KSC;
+        case 4: return SInfo<4>::KSC;
+        case 7: return SInfo<7>::KSC;
+        case 8: return SInfo<8>::KSC;
+        default: return 0;
+    }
+}
+
+// LDS-DMA issue (inline asm: invisible to hipcc's vmcnt bookkeeping, so no
+// compiler drain of the ring; completion is counted by hand).  M0 = the
+// wave-uniform LDS destination, written and restored inside the statement.
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+// 4 bytes per lane through a buffer descriptor: out-of-range offsets land zeros
+__device__ __forceinline__ void dma4(u32x4_t rsrc, unsigned voff, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_dst) : "memory");
+}
+// 16 bytes per lane through a buffer descriptor (aligned window rows)
+__device__ __forceinline__ void dma16b(u32x4_t rsrc, unsigned voff, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_dst) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
+}
+__device__ __forceinline__ u32x4_t raw_rsrc(const void* p, int bytes) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    u32x4_t r;
+    r[0] = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) & 0xFFFFu;
+    r[2] = __builtin_amdgcn_readfirstlane((uint32_t)bytes);
+    r[3] = 0x00020000u;
+    return r;
+}
+
+// Workgroup tile: BN time columns x BM GEMM rows.  A wave owns WM rows x WN
+// columns (WM = 32: 128 columns; WM = 64: 64 columns), four 32x32 blocks.
+template <int KT, int BM, int BN, int WM, bool XV = true> struct SGeo {
+    using F = SFam<KT>;
+    static constexpr int Q = F::Q, S = F::S, VC = F::VC;
+    static constexpr int KSC = Q * VC / 16, CPC = VC / S;
+    static constexpr int WN = 4096 / WM, NJ = WM / 32, NI = WN / 32;
+    static constexpr int WGM = BM / WM, WGN = BN / WN, NW = WGM * WGN, NT = 64 * NW;
+    // window rows: columns + tap reach (+1: ConvT phase group 1 reads one row later)
+    static constexpr int XW_MAX = BN + (Q - 1) * F::DMAX + (KT == 2 ? 1 : 0);
+    static constexpr int PH = VC + 8;                        // halves per plane row (conflict-free b128)
+    static constexpr int XPLANE = XW_MAX * PH * 2;           // bytes per f16 plane
+    static constexpr int WCHUNK = (BM / 32) * KSC * 2 * 1024;   // weight image of one chunk
+    static constexpr int WI = WCHUNK / 1024 / NW;            // 1 KB weight DMA pieces per wave
+    // raw window rows: XV = 16-byte pieces from a 4-sample-aligned start (row
+    // stride rounded up to 4 samples), else 4-byte pieces
+    static constexpr int RS_MAX = XV ? ((XW_MAX * S + 3 + 3) / 4) * 4 : XW_MAX * S;
+    static constexpr int RAW_F = CPC * RS_MAX;               // raw window floats of one chunk
+    static constexpr int PF = XV ? 4 : 1;                    // floats per lane per DMA
+    static constexpr int XI = (RAW_F + 64 * PF * NW - 1) / (64 * PF * NW);   // window DMA pieces per wave
+    static constexpr int RAW = XI * NW * 256 * PF;           // raw window bytes (with slack)
+    static constexpr int STAGE = WCHUNK + RAW;
+    static constexpr int NS = 3;                             // DMA ring depth
+    static constexpr int LDS = NS * STAGE + 2 * XPLANE;      // ring + one (hi, lo) plane pair
+    static constexpr int DPC = WI + XI;                      // DMA instructions per wave per chunk
+    static constexpr int G8 = VC / 8;                        // 8-channel groups per row
+    static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;   // convert tasks per thread
+    static_assert(WCHUNK % (1024 * NW) == 0, "weight image must split over the waves");
+    static_assert(XPLANE % 16 == 0 && STAGE % 16 == 0, "16-byte LDS alignment");
+    static_assert(NI * NJ == 4 && NW >= 1 && NW <= 8, "tile");
+    static_assert(DPC <= 60, "vmcnt range");
+};
+
+template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_split_kernel(ConvKArgs a) {
+    using G = SGeo<KT, BM, BN, WM, XV>;
+    constexpr int S = G::S, VC = G::VC, KSC = G::KSC, CPC = G::CPC, PH = G::PH;
+    constexpr int NT = G::NT, NW = G::NW, WGM = G::WGM, G8 = G::G8, XT = G::XT;
+    constexpr int NI = G::NI, NJ = G::NJ, WN = G::WN;
+    constexpr int HPS = VC / 16;                 // K-steps per tap
+    constexpr unsigned kOOB = 0xFFFFFFF0u;
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x;
+#ifdef RAVE_STAMPS
+    const int wg_lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    auto stamp = [&](int k) {
+        if (tid == 0 && a.stamps) {
+            a.stamps[wg_lin * 8 + k] = __builtin_amdgcn_s_memtime();
+            if (k == 0) a.stamps[wg_lin * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+        }
+    };
+#else
+    auto stamp = [](int) {};
+#endif
+    stamp(0);
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WGM, wn = wave / WGM;
+    const int h = lane >> 5, l32 = lane & 31;
+
+    const int n0 = blockIdx.x * BN;
+    const int m0 = blockIdx.y * BM;
+    const int mw = m0 + wm * WM;                 // this wave's first GEMM row
+    const int b = __builtin_amdgcn_readfirstlane(blockIdx.z / a.S);
+    const int split = __builtin_amdgcn_readfirstlane(blockIdx.z - b * a.S);
+    const int c_begin = split * a.cps;
+    const int c_end = min(a.nchunks, c_begin + a.cps);
+    // input time of window row 0 (ConvT: group 0's window; group 1 reads one row later)
+    const int tb = n0 * S - a.pad_l;
+    const int gshift = (mw >= a.split_row) ? (a.pad_l - a.pad_g1) : 0;
+    const int XW = a.XW;
+    const int RL = XW * S;                        // raw row length (input samples)
+    const int ta = XV ? (tb & ~3) : tb;           // DMA start (XV: 4-sample aligned)
+    const int off0 = tb - ta;
+    const int RS = XV ? ((RL + off0 + 3) & ~3) : RL;  // raw row stride (floats)
+    const int P4 = XV ? RS / 4 : RS;              // DMA pieces per raw row
+    const unsigned rl_magic = XV ? (unsigned)((0x100000000ull + P4 - 1) / P4) : a.rl_magic;
+    const int ntask = XW * G8;
+    const int ci_lim = min(a.c_in, c_end * CPC);  // window DMA past c_end lands zeros
+    const u32x4_t xrs = raw_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);
+    const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
+    const char* wsrc = reinterpret_cast<const char*>(a.w) + (size_t)(m0 / 32) * KSC * 2 * 1024;
+    const size_t wchunk_stride = (size_t)a.MB * KSC * 2 * 1024;
+    const uint32_t lds0 = lds_addr(smem);
+    char* planes = smem + G::NS * G::STAGE;
+
+    floatx16 acc[NI][NJ];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // epilogue per-row constants, fetched now so their latency hides under the K loop
+    float e_rs[NJ], e_bias[NJ];
+    int e_co[NJ], e_q[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int m = mw + j * 32 + l32;
+        e_rs[j] = a.rscale[m];                   // m < Mpad
+        int co = m, q = 0;
+        if (a.transposed) convt_row(a, m, co, q);
+        e_co[j] = co;
+        e_q[j] = q;
+        const bool rowok = a.transposed ? co < a.bias_rows : m < a.M;
+        e_bias[j] = (a.bias && rowok && a.S == 1) ? a.bias[co] : 0.f;
+    }
+
+    // chunk c -> ring stage (weights: clamped to the last real chunk; window:
+    // per-lane offsets, out-of-range -> zeros)
+    auto issue = [&](int c, int stage) __attribute__((always_inline)) {
+        const uint32_t sbase = lds0 + stage * G::STAGE;
+        const char* src = wsrc + (size_t)min(c, a.nchunks - 1) * wchunk_stride;
+#pragma unroll
+        for (int i = 0; i < G::WI; ++i) {
+            const int piece = i * NW + wave;
+            dma16(src + piece * 1024 + lane * 16, sbase + piece * 1024);
+        }
+        const int ci0 = c * CPC;
+#pragma unroll
+        for (int i = 0; i < G::XI; ++i) {
+            const int piece = i * NW + wave;
+            const unsigned f = (unsigned)(piece * 64 + lane);
+            const int cl = (int)__umulhi(f, rl_magic);
+            const int tt = (int)f - cl * P4;
+            const int ci = ci0 + cl;
+            const int t = ta + tt * G::PF;
+            const bool ok = (cl < CPC) && (ci < ci_lim) && (t >= 0) && (t < a.t_in);
+            const unsigned voff = ok ? (unsigned)(ci * a.x_sc + t) * 4u : kOOB;
+            if constexpr (XV) dma16b(xrs, voff, sbase + G::WCHUNK + piece * 1024);
+            else dma4(xrs, voff, sbase + G::WCHUNK + piece * 256);
+        }
+    };
+    // raw window of a stage -> activation -> (hi, lo) f16 planes
+    auto convert = [&](int c, int stage) __attribute__((always_inline)) {
+        const float* raw = reinterpret_cast<const float*>(smem + stage * G::STAGE + G::WCHUNK);
+        _Float16* xh = reinterpret_cast<_Float16*>(planes);
+        _Float16* xl = reinterpret_cast<_Float16*>(planes + G::XPLANE);
+        const int ci0 = c * CPC;
+#pragma unroll
+        for (int i = 0; i < XT; ++i) {
+            const int e = tid + i * NT;
+            const int g = (int)(((unsigned)e * a.xw_magic) >> 24);
+            const int w = e - g * XW;
+            if (e < ntask) {
+                s_f32x8 v8;
+#pragma unroll
+                for (int v = 0; v < 8; ++v) {
+                    const int vc = g * 8 + v;
+                    float val = raw[(vc / S) * RS + off0 + w * S + (vc % S)];
+                    if constexpr (SNAKE) {
+                        const float al = a.alpha[min(ci0 + vc / S, a.c_in - 1)];
+                        val = val + (1.0f / (al + 1e-9f)) * sin_squared(al * val);
+                    } else {
+                        val = val > 0.f ? val : val * slope;
+                    }
+                    v8[v] = val;
+                }
+                const s_h8 hi = __builtin_convertvector(v8, s_h8);
+                const s_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, s_f32x8)) * 2048.0f, s_h8);
+                *reinterpret_cast<s_h8*>(xh + w * PH + g * 8) = hi;
+                *reinterpret_cast<s_h8*>(xl + w * PH + g * 8) = lo;
+            }
+        }
+    };
+
+    // per-lane A-fragment offsets (halves): window row wn*WN + l32 + q*d (+ group shift)
+    int xoff[G::Q];
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q) xoff[q] = (wn * WN + l32 + q * a.d + gshift) * PH + 8 * h;
+
+    struct Frag {
+        s_h8 ah[NI], al[NI], bh[NJ], bl[NJ];
+    };
+    auto read_frag = [&](int stage, int st, Frag& f) __attribute__((always_inline)) {
+        const int q = st / HPS, hv = st - q * HPS;
+        const _Float16* xh = reinterpret_cast<const _Float16*>(planes);
+        const _Float16* xl = reinterpret_cast<const _Float16*>(planes + G::XPLANE);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            f.ah[i] = *reinterpret_cast<const s_h8*>(xh + xoff[q] + i * 32 * PH + hv * 16);
+            f.al[i] = *reinterpret_cast<const s_h8*>(xl + xoff[q] + i * 32 * PH + hv * 16);
+        }
+        const char* wimg = smem + stage * G::STAGE;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const char* p = wimg + (((wm * NJ + j) * KSC + st) * 2) * 1024 + lane * 16;
+            f.bh[j] = *reinterpret_cast<const s_h8*>(p);
+            f.bl[j] = *reinterpret_cast<const s_h8*>(p + 1024);
+        }
+    };
+
+    // ------------------------------------------------------------ prologue
+    issue(c_begin, 0);
+    issue(c_begin + 1, 1);
+    wait_vm<G::DPC>();
+    __syncthreads();
+    convert(c_begin, 0);
+    __syncthreads();
+    stamp(1);
+
+    // per chunk: DMA two chunks ahead | MFMAs | wait + barrier | split the next
+    // chunk's window into the (single) plane pair | barrier
+    int stage = 0;
+    for (int c = c_begin; c < c_end; ++c) {
+        issue(c + 2, stage == 0 ? 2 : stage - 1);       // = (stage + 2) % 3
+        Frag f[2];
+        read_frag(stage, 0, f[0]);
+#pragma unroll
+        for (int st = 0; st < KSC; ++st) {
+            if (st + 1 < KSC) read_frag(stage, st + 1, f[(st + 1) & 1]);   // next reads in flight
+            __builtin_amdgcn_sched_barrier(0);
+            const Frag& g = f[st & 1];
+            s_h8 b2[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) b2[j] = g.bh[j] * (_Float16)2048.0f;
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.ah[i], b2[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.al[i], g.bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.ah[i], g.bl[j], acc[i][j], 0, 0, 0);
+        }
+        const int nstage = stage == 2 ? 0 : stage + 1;
+        wait_vm<G::DPC>();                  // chunk c+1 landed (c+2 may still fly)
+        __syncthreads();                    // ... for every wave; the planes / chunk c's weights free
+        if (c + 1 < c_end) {
+            convert(c + 1, nstage);
+            __syncthreads();
+        }
+        stage = nstage;
+        if (c == c_begin) stamp(2);
+    }
+    stamp(3);
+    wait_vm<0>();                           // drain the ring before the epilogue's own loads
+
+    // ---------------------------------------------------------------- epilogue
+    // lane = one GEMM row per m-block; registers 4g..4g+3 of a block = 4 consecutive columns
+    const bool partial = a.S > 1;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] *= e_rs[j];
+    }
+    if (partial) {
+        const __amdgpu_buffer_rsrc_t prs = make_rsrc(
+            a.partial + ((int64_t)split * a.B + b) * (int64_t)a.M * a.U, a.M * a.U * 4);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int m = mw + j * 32 + l32;
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int n = n0 + wn * WN + i * 32 + 8 * g + 4 * h;
+                    if (a.vec_p && m < a.M && n + 3 < a.U) {
+                        const s_f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                                           acc[i][j][4 * g + 3]};
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), prs,
+                                                               (unsigned)(m * a.U + n) * 4u, 0, 0);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const unsigned off = (m < a.M && n + e < a.U) ? (unsigned)(m * a.U + n + e) * 4u : kOOB;
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][j][4 * g + e]),
+                                                                  prs, off, 0, 0);
+                        }
+                    }
+                }
+        }
+        stamp(4);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t yrs = make_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
+    if (a.transposed) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int co = e_co[j], q = e_q[j];
+            const bool rowok = co < a.bias_rows;
+            const float bv = e_bias[j];
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int n = n0 + wn * WN + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int t = n * a.R + q;
+                    const unsigned off = (rowok && n < a.U && t < a.t_y) ? (unsigned)(co * a.y_sc + t) * 4u : kOOB;
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][j][r] + bv), yrs, off, 0, 0);
+                }
+        }
+        stamp(4);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t rrs = make_rsrc(a.res ? a.res + (int64_t)b * a.r_sb : a.y, a.res ? a.r_bytes : 0);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int m = mw + j * 32 + l32;
+        const float bv = e_bias[j];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = n0 + wn * WN + i * 32 + 8 * g + 4 * h;
+                if (a.vec_y && m < a.M && n + 3 < a.U) {
+                    s_f32x4 rv = {0.f, 0.f, 0.f, 0.f};
+                    if (a.res)
+                        rv = __builtin_bit_cast(s_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                            rrs, (unsigned)(m * a.r_sc + n) * 4u, 0, 0));
+                    const s_f32x4 v = {acc[i][j][4 * g] + bv + rv[0], acc[i][j][4 * g + 1] + bv + rv[1],
+                                       acc[i][j][4 * g + 2] + bv + rv[2], acc[i][j][4 * g + 3] + bv + rv[3]};
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), yrs,
+                                                           (unsigned)(m * a.y_sc + n) * 4u, 0, 0);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const bool ok = m < a.M && n + e < a.U;
+                        const float rv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                            rrs, ok ? (unsigned)(m * a.r_sc + n + e) * 4u : kOOB, 0, 0));
+                        __builtin_amdgcn_raw_buffer_store_b32(
+                            __builtin_bit_cast(unsigned, acc[i][j][4 * g + e] + bv + rv), yrs,
+                            ok ? (unsigned)(m * a.y_sc + n + e) * 4u : kOOB, 0, 0);
+                    }
+                }
+            }
+    }
+    stamp(4);
+}
+
+// Sum the split-K slabs in split order (fixed order: deterministic), then
+// bias / residual / ConvT interleave.  One thread = 4 consecutive columns of
+// one (b, m) row; grid.y = B * M rows.
+__global__ __launch_bounds__(256) void split_reduce_kernel(ConvKArgs a) {
+    const int row = blockIdx.y;                     // b * M + m
+    const int b = row / a.M, m = row - b * a.M;
+    const int n = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (n >= a.U) return;
+    const int64_t total = (int64_t)a.B * a.M * a.U;
+    const float* p = a.partial + (int64_t)row * a.U + n;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    const int cnt = min(4, a.U - n);
+    if (a.vec_p && cnt == 4) {
+        for (int s = 0; s < a.S; ++s) {
+            const s_f32x4 t = *reinterpret_cast<const s_f32x4*>(p + s * total);
+            v[0] += t[0]; v[1] += t[1]; v[2] += t[2]; v[3] += t[3];
+        }
+    } else {
+        for (int s = 0; s < a.S; ++s)
+            for (int e = 0; e < cnt; ++e) v[e] += p[s * total + e];
+    }
+    for (int e = 0; e < cnt; ++e) store_out(a, b, m, n + e, v[e]);
+}
+
+// --------------------------------------------------------------------- host side
+struct SplitCfg {
+    int bm, bn, wm, S;
+};
+
+// Tile + split-K choice.  Tiles (BM rows x BN columns, wave WM x 4096/WM):
+// least padding with the most waves per workgroup that still fills the chip;
+// K split over workgroups (fp32 slabs + a fixed-order reduce) when the output
+// alone cannot give every SIMD a wave.
+constexpr int kSplitTiles[6][3] = {{128, 128, 32}, {64, 256, 32}, {64, 128, 32},
+                                   {256, 64, 64}, {128, 64, 64}, {64, 64, 64}};
+template <int KT>
+static bool split_tile_fits(int idx) {   // the 4-byte-DMA variant is the larger one
+    switch (idx) {
+        case 0: return SGeo<KT, 128, 128, 32, true>::LDS <= 160 * 1024 && SGeo<KT, 128, 128, 32, false>::LDS <= 160 * 1024;
+        case 1: return SGeo<KT, 64, 256, 32, true>::LDS <= 160 * 1024 && SGeo<KT, 64, 256, 32, false>::LDS <= 160 * 1024;
+        case 2: return SGeo<KT, 64, 128, 32, true>::LDS <= 160 * 1024 && SGeo<KT, 64, 128, 32, false>::LDS <= 160 * 1024;
+        case 3: return SGeo<KT, 256, 64, 64, true>::LDS <= 160 * 1024 && SGeo<KT, 256, 64, 64, false>::LDS <= 160 * 1024;
+        case 4: return SGeo<KT, 128, 64, 64, true>::LDS <= 160 * 1024 && SGeo<KT, 128, 64, 64, false>::LDS <= 160 * 1024;
+        default: return SGeo<KT, 64, 64, 64, true>::LDS <= 160 * 1024 && SGeo<KT, 64, 64, 64, false>::LDS <= 160 * 1024;
+    }
+}
+static bool split_fits(int taps, int idx) {
+    switch (taps) {
+        case 1: return split_tile_fits<1>(idx);
+        case 2: return split_tile_fits<2>(idx);
+        case 3: return split_tile_fits<3>(idx);
+        case 4: return split_tile_fits<4>(idx);
+        case 7: return split_tile_fits<7>(idx);
+        default: return split_tile_fits<8>(idx);
+    }
+}
+
+static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int split_row) {
+    const auto& all = kSplitTiles;
+    auto waste = [&](int bm, int bn) {
+        return double(ceil_div(M, bm) * bm) * double(ceil_div(U, bn) * bn) / (double(M) * double(U));
+    };
+    SplitCfg best{64, 64, 64, 1};
+    double bscore = 1e30;
+    for (int ti = 0; ti < 6; ++ti) {
+        const int* c = all[ti];
+        if (!split_fits(taps, ti)) continue;
+        if (split_row < M && split_row % c[2] != 0) continue;      // a wave never straddles ConvT groups
+        const int nw = (c[0] / c[2]) * (c[1] / (4096 / c[2]));
+        const int64_t wgs = (int64_t)ceil_div(M, c[0]) * ceil_div(U, c[1]) * B;
+        const int64_t waves = wgs * nw;
+        double score = waste(c[0], c[1]);
+        if (waves < 1024) score *= 1.0 + 0.5 * (1024.0 / waves - 1.0) / std::max(1, nchunks / 8);
+        score *= 1.0 + 0.03 * (4 - nw);                                 // prefer fat workgroups
+        if (score < bscore) { bscore = score; best = {c[0], c[1], c[2], 1}; }
+    }
+    const int nw = (best.bm / best.wm) * (best.bn / (4096 / best.wm));
+    const int64_t waves = (int64_t)ceil_div(M, best.bm) * ceil_div(U, best.bn) * B * nw;
+    if (waves < 1024 && nchunks >= 8) {
+        int S = (int)std::min<int64_t>(16, ceil_div64(2048, waves));
+        S = std::min(S, nchunks / 4);
+        best.S = std::max(1, S);
+    }
+    return best;
+}
+
+template <int KT, int BM, int BN, int WM, bool XV>
+static int split_launch_xv(ConvKArgs k, hipStream_t st) {
+    using G = SGeo<KT, BM, BN, WM, XV>;
+    if constexpr (G::LDS > 160 * 1024) {
+        set_error("conv1d(split16): tile exceeds LDS");
+        return RAVE_ERR_UNSUPPORTED;
+    } else {
+    if (k.XW > G::XW_MAX) {
+        set_error("conv1d(split16): dilation too large for the staged window");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    constexpr size_t lds = (size_t)G::LDS;
+    static_assert(lds <= 160 * 1024, "LDS budget");
+    dim3 grid(ceil_div(k.U, BN), ceil_div(k.M, BM), k.B * k.S);
+    const bool snake = k.act == RAVE_ACT_SNAKE;
+    auto kern = snake ? conv1d_split_kernel<KT, BM, BN, WM, true, XV> : conv1d_split_kernel<KT, BM, BN, WM, false, XV>;
+    if (lds > 64 * 1024) {
+        static bool done[2] = {false, false};
+        if (!done[snake]) {
+            RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            done[snake] = true;
+        }
+    }
+    launch(kern, grid, dim3(G::NT), (uint32_t)lds, st, k);
+    return launch_status("conv1d_split_kernel");
+    }
+}
+
+template <int KT, int BM, int BN, int WM>
+static int split_launch_k(ConvKArgs k, hipStream_t st) {
+    return k.x_vec ? split_launch_xv<KT, BM, BN, WM, true>(k, st) : split_launch_xv<KT, BM, BN, WM, false>(k, st);
+}
+
+template <int KT>
+static int split_launch_family(ConvKArgs k, const SplitCfg& c, hipStream_t st) {
+    k.XW = c.bn + (SFam<KT>::Q - 1) * k.d + (k.transposed ? 1 : 0);
+    k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
+    const unsigned rl = (unsigned)(k.XW * SFam<KT>::S);
+    k.rl_magic = (unsigned)((0x100000000ull + rl - 1) / rl);
+    if (c.bm == 128 && c.bn == 128) return split_launch_k<KT, 128, 128, 32>(k, st);
+    if (c.bm == 64 && c.bn == 256) return split_launch_k<KT, 64, 256, 32>(k, st);
+    if (c.bm == 64 && c.bn == 128) return split_launch_k<KT, 64, 128, 32>(k, st);
+    if (c.bm == 256 && c.bn == 64) return split_launch_k<KT, 256, 64, 64>(k, st);
+    if (c.bm == 128 && c.bn == 64) return split_launch_k<KT, 128, 64, 64>(k, st);
+    return split_launch_k<KT, 64, 64, 64>(k, st);
+}
+
+static int split_prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
+    int rc = prepare_common(a, k, taps);
+    if (rc != RAVE_OK) return rc;
+    k.nchunks = ceil_div(a.c_in, split_cpc(taps));
+    k.Mpad = ceil_div(k.M, 128) * 128;
+    k.MB = k.Mpad / 32;
+    const int64_t frag_floats = (int64_t)k.nchunks * k.MB * split_ksc(taps) * 2 * 256;
+    RAVE_CHECK_ARG(frag_floats * 4 < (1ll << 31), "conv1d(split16): packed weight beyond 2 GiB");
+    k.w_bytes = (int)(frag_floats * 4);
+    k.rscale = a.weight + frag_floats;                 // after the fragments
+    auto aligned = [](const void* p, int64_t sb, int64_t sc) {
+        return (reinterpret_cast<uintptr_t>(p) % 16 == 0) && sb % 4 == 0 && sc % 4 == 0;
+    };
+    k.vec_y = aligned(a.y, a.y_sb, a.y_sc) && (!a.residual || aligned(a.residual, a.r_sb, a.r_sc));
+    k.vec_p = (k.U % 4 == 0) && (!a.partial || reinterpret_cast<uintptr_t>(a.partial) % 16 == 0);
+    // 16-byte window DMA: rows 16-byte aligned and whole 4-sample pieces inside [0, t_in)
+    k.x_vec = aligned(a.x, a.x_sb, a.x_sc) && a.t_in % 4 == 0;
+    return RAVE_OK;
+}
+
+int64_t conv1d_split_workspace(const rave_conv1d_args& a) {
+    ConvKArgs k;
+    int taps;
+    if (split_prepare(a, k, taps) != RAVE_OK) return -1;
+    SplitCfg c = split_choose(taps, k.M, k.U, k.B, k.nchunks, k.split_row);
+    if (c.S <= 1) return 0;
+    return (int64_t)c.S * k.B * (int64_t)k.M * k.U;
+}
+
+int conv1d_split(const rave_conv1d_args& a, void* stream) {
+    ConvKArgs k;
+    int taps;
+    int rc = split_prepare(a, k, taps);
+    if (rc != RAVE_OK) return rc;
+    SplitCfg c = split_choose(taps, k.M, k.U, k.B, k.nchunks, k.split_row);
+    if (c.S > 1 && a.partial == nullptr) c.S = 1;
+    k.cps = ceil_div(k.nchunks, c.S);
+    k.S = ceil_div(k.nchunks, k.cps);
+    k.partial = a.partial;
+#ifdef RAVE_STAMPS
+    k.stamps = a.stamps;
+#endif
+    hipStream_t st = as_stream(stream);
+    switch (taps) {
+        case 1: rc = split_launch_family<1>(k, c, st); break;
+        case 2: rc = split_launch_family<2>(k, c, st); break;
+        case 3: rc = split_launch_family<3>(k, c, st); break;
+        case 4: rc = split_launch_family<4>(k, c, st); break;
+        case 7: rc = split_launch_family<7>(k, c, st); break;
+        case 8: rc = split_launch_family<8>(k, c, st); break;
+        default: set_error("conv1d: unsupported kernel size"); return RAVE_ERR_UNSUPPORTED;
+    }
+    if (rc != RAVE_OK || k.S <= 1) return rc;
+    RAVE_CHECK_ARG((int64_t)k.B * k.M <= 65535, "conv1d(split16): too many rows for the split-K reduce");
+    launch(split_reduce_kernel, dim3(ceil_div(k.U, 1024), k.B * k.M), dim3(256), 0, st, k);
+    return launch_status("split_reduce_kernel");
+}
+
+// ------------------------------------------------------------ weight packing
+// Power-of-two row exponent: max |w * 2^e| in [8, 16) (e = 0 for an all-zero row).
+static int row_exponent(double amax) {
+    if (!(amax > 0.0)) return 0;
+    int e = (int)std::floor(std::log2(16.0 / amax));
+    while (std::ldexp(amax, e) >= 16.0) --e;
+    while (std::ldexp(amax, e) < 8.0) ++e;
+    return e;
+}
+
+}  // namespace rave
+
+using namespace rave;
+
+// GEMM-row geometry of a layer (shared by the size query and the packer)
+static int split_geometry(int c_in, int c_out, int kernel, int stride, int dilation, int transposed,
+                          int out_shift, int& taps, int& M, int& Mpad, int& nchunks, int& split_row,
+                          int& q0) {
+    (void)dilation;
+    if (transposed) {
+        if (kernel != 2 * stride || stride % 2) return -1;
+        taps = 2;
+        q0 = stride - out_shift;
+        split_row = convt_group1_row(c_out, stride, q0);
+        M = split_row + c_out * (stride - q0);
+    } else {
+        if (!family_supported(kernel) || family_stride(kernel) != stride) return -1;
+        taps = kernel;
+        q0 = 1;
+        split_row = 1 << 30;
+        M = c_out;
+    }
+    Mpad = ceil_div(M, 128) * 128;
+    nchunks = ceil_div(c_in, split_cpc(taps));
+    return 0;
+}
+
+extern "C" int64_t rave_conv1d_split_packed_size(int c_in, int c_out, int kernel, int stride, int dilation,
+                                                 int transposed) {
+    if (c_in <= 0 || c_out <= 0) return -1;
+    int taps, M, Mpad, nchunks, split_row, q0;
+    // transposed: the larger of the two row layouts (out_shift 0 / stride/2)
+    int64_t best = -1;
+    for (int os = 0; os <= (transposed ? 1 : 0); ++os) {
+        if (split_geometry(c_in, c_out, kernel, stride, dilation, transposed, os ? stride / 2 : 0, taps, M,
+                           Mpad, nchunks, split_row, q0) != 0)
+            return -1;
+        const int64_t n = (int64_t)nchunks * (Mpad / 32) * split_ksc(taps) * 2 * 256 + Mpad;
+        best = std::max(best, n);
+    }
+    return best;
+}
+
+extern "C" int rave_conv1d_split_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
+                                             int dilation, int transposed, int out_shift, float* packed) {
+    RAVE_CHECK_ARG(w && packed, "split_pack_weight: null pointer");
+    RAVE_CHECK_ARG(c_in > 0 && c_out > 0 && kernel > 0 && stride > 0 && dilation > 0,
+                   "split_pack_weight: bad shape");
+    RAVE_CHECK_ARG(!transposed || out_shift == 0 || out_shift == stride / 2,
+                   "split_pack_weight: transposed out_shift must be 0 or stride/2");
+    int taps, M, Mpad, nchunks, split_row, q0;
+    if (split_geometry(c_in, c_out, kernel, stride, dilation, transposed, out_shift, taps, M, Mpad, nchunks,
+                       split_row, q0) != 0) {
+        set_error("split_pack_weight: unsupported layer shape");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    const int R = transposed ? stride : 1;
+    const int S = transposed ? 1 : family_stride(taps);
+    const int VC = split_cpc(taps) * S;
+    const int KSC = split_ksc(taps), HPS = VC / 16, CPC = VC / S;
+    const int MB = Mpad / 32;
+    // GEMM weight of (row m, input channel ci, original tap j); 0 outside
+    auto wval = [&](int m, int ci, int j) -> float {
+        if (m >= M || ci >= c_in) return 0.f;
+        if (!transposed) return w[((int64_t)m * c_in + ci) * kernel + j];
+        int co, q;
+        if (m < split_row) { co = m / q0; q = m % q0; }
+        else { const int p = R - q0; co = (m - split_row) / p; q = q0 + (m - split_row) % p; }
+        if (co >= c_out) return 0.f;                    // group-0 padding rows
+        int kidx;
+        if (q < q0) kidx = (j == 0) ? q + out_shift + R : q + out_shift;
+        else kidx = (j == 0) ? q + out_shift : q + out_shift - R;
+        return w[((int64_t)ci * c_out + co) * kernel + kidx];
+    };
+    // (tap q after polyphase, virtual channel vc of chunk c) -> (ci, original tap)
+    auto kmap = [&](int c, int q, int vc, int& ci, int& j) {
+        ci = c * CPC + vc / S;
+        j = (S > 1) ? q * S + vc % S : q;
+    };
+    const int KT_orig = transposed ? 2 : kernel;
+    std::vector<int> ex(Mpad, 0);
+    for (int m = 0; m < Mpad; ++m) {
+        double amax = 0.0;
+        for (int ci = 0; ci < c_in; ++ci)
+            for (int j = 0; j < KT_orig; ++j) amax = std::max(amax, (double)std::fabs(wval(m, ci, j)));
+        ex[m] = row_exponent(amax);
+    }
+    _Float16* out = reinterpret_cast<_Float16*>(packed);
+    for (int c = 0; c < nchunks; ++c)
+        for (int mb = 0; mb < MB; ++mb)
+            for (int st = 0; st < KSC; ++st) {
+                const int q = st / HPS, hv = st % HPS;
+                _Float16* hi = out + (((int64_t)(c * MB + mb) * KSC + st) * 2) * 512;
+                _Float16* lo = hi + 512;
+                for (int l = 0; l < 64; ++l)
+                    for (int e = 0; e < 8; ++e) {
+                        const int m = mb * 32 + (l & 31);
+                        const int vc = hv * 16 + 8 * (l >> 5) + e;
+                        int ci, j;
+                        kmap(c, q, vc, ci, j);
+                        const float v = std::ldexp(wval(m, ci, j), ex[m]);
+                        const _Float16 vh = (_Float16)v;
+                        const _Float16 vl = (_Float16)((v - (float)vh) * 2048.0f);
+                        hi[l * 8 + e] = vh;
+                        lo[l * 8 + e] = vl;
+                    }
+            }
+    float* rs = packed + (int64_t)nchunks * MB * KSC * 2 * 256;
+    for (int m = 0; m < Mpad; ++m) rs[m] = (float)std::ldexp(1.0, -(ex[m] + 11));
+    return RAVE_OK;
+}

@@ -229,33 +229,50 @@ class RAVE:
 
     def __init__(self, cfg: RaveConfig, params: Mapping[str, np.ndarray], speaker: np.ndarray,
                  device=None, hk: Optional[np.ndarray] = None,
-                 adain_stats: Optional[Mapping] = None, fuse_units: bool = True):
+                 adain_stats: Optional[Mapping] = None, fuse_units: bool = True,
+                 precision: str = "f32"):
         check_params(cfg, params)
+        if precision not in list(N.PRECISION) + ["auto"]:
+            raise ValueError(f"precision must be one of {sorted(N.PRECISION) + ['auto']}")
+        self.precision = precision
+        # "auto": every conv / fused-unit op is timed in both arithmetic paths at
+        # plan-build time on scratch tensors of its own shape; the faster is kept
+        self.precs = [N.PREC_F32, N.PREC_SPLIT16] if precision == "auto" else [N.PRECISION[precision]]
+        self.prec = self.precs[-1]
+        self._tuned: Dict[tuple, int] = {}
         self.cfg = cfg
         self.graph = build_graph(cfg)
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise ValueError("rave_amd.RAVE runs on the GPU only (device must be cuda)")
         ar = Arena()
-        self.w_off: Dict[str, Tuple[int, Optional[int], Optional[int]]] = {}
-        self.w_off_stream: Dict[str, int] = {}
+        # packed conv weights per precision: (name, prec) -> arena offset
+        self.w_off: Dict[str, Tuple[int, Optional[int], Optional[int]]] = {}   # f32 / first precision
+        self.w_pack: Dict[Tuple[str, int], int] = {}
+        self.w_pack_stream: Dict[Tuple[str, int], int] = {}
         for n in self.graph.convs():
             w = conv_weight(n, params)
-            packed = N.pack_conv_weight(w, n.c_in, n.c_out, n.kernel, n.stride, n.dilation, n.transposed)
-            wo = ar.add(packed)
-            if n.transposed:   # cached (streaming) form: overlap-add cache, no r//2 crop
-                self.w_off_stream[n.name] = ar.add(N.pack_conv_weight(
-                    w, n.c_in, n.c_out, n.kernel, n.stride, n.dilation, True, out_shift=0))
+            for pr in self.precs:
+                self.w_pack[(n.name, pr)] = ar.add(N.pack_conv_weight(
+                    w, n.c_in, n.c_out, n.kernel, n.stride, n.dilation, n.transposed, precision=pr))
+                if n.transposed:   # cached (streaming) form: overlap-add cache, no r//2 crop
+                    self.w_pack_stream[(n.name, pr)] = ar.add(N.pack_conv_weight(
+                        w, n.c_in, n.c_out, n.kernel, n.stride, n.dilation, True, out_shift=0, precision=pr))
             bo = ar.add(params[n.name + ".bias"]) if n.bias else None
             ao = ar.add(params[n.alpha]) if n.act == "snake" else None
-            self.w_off[n.name] = (wo, bo, ao)
-        # fused Residual(DilatedUnit) weights: (k=3 node name) -> arena offset
+            self.w_off[n.name] = (self.w_pack[(n.name, self.precs[0])], bo, ao)
+        # fused Residual(DilatedUnit) weights: (k=3 node name, prec) -> arena offset
+        self.unit_pack: Dict[Tuple[str, int], int] = {}
         self.unit_off: Dict[str, int] = {}
         if fuse_units:
             for k3, k1 in self._unit_pairs(self.graph.convs()):
-                if N.unit_supported(k3.c_in):
-                    self.unit_off[k3.name] = ar.add(N.pack_unit_weight(
-                        conv_weight(k3, params), conv_weight(k1, params), k3.c_in))
+                for pr in self.precs:
+                    if N.unit_supported(k3.c_in, pr):
+                        self.unit_pack[(k3.name, pr)] = ar.add(N.pack_unit_weight(
+                            conv_weight(k3, params), conv_weight(k1, params), k3.c_in, precision=pr))
+                cands = [pr for pr in self.precs if (k3.name, pr) in self.unit_pack]
+                if cands:
+                    self.unit_off[k3.name] = self.unit_pack[(k3.name, cands[0])]
         self.noise_target = int(np.prod(cfg.noise.ratios)) if cfg.noise is not None else 0
         self.hk = P.design_bank(cfg.pqmf_attenuation, cfg.n_band) if hk is None else np.asarray(hk, np.float32)
         hkf, hki = P.kernels(self.hk)
@@ -299,21 +316,74 @@ class RAVE:
                 out.append((a, b))
         return out
 
+    # ------------------------------------------------------------ per-op precision choice
+    def _time_native(self, fn, args, reps: int = 5) -> float:
+        st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for _ in range(2):
+            N.check(fn(C.byref(args), st), "autotune")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn(C.byref(args), st)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    def _bind_scratch(self, args, ptrs: Dict[str, Optional[View]], shapes: Dict[str, tuple],
+                      keep: list) -> None:
+        """Point an op's pointer fields at scratch tensors (tensor fields) or the
+        arena (constants) for a timing run."""
+        for field, view in ptrs.items():
+            if view is None:
+                setattr(args, field, None)
+            elif view.slot == "arena":
+                setattr(args, field, self.arena.ptr(view.off))
+            elif view.slot == "abs":
+                setattr(args, field, view.off)
+            else:
+                t = torch.randn(shapes[field], device=self.device) * 0.5
+                keep.append(t)
+                setattr(args, field, t.data_ptr())
+
+    def _pick(self, key: tuple, cands: List[int], run) -> int:
+        """The faster precision of ``cands`` for the op ``key`` (cached); ``run(prec)``
+        returns milliseconds."""
+        if len(cands) == 1:
+            return cands[0]
+        if key not in self._tuned:
+            times = {pr: run(pr) for pr in cands}
+            self._tuned[key] = min(times, key=times.get)
+        return self._tuned[key]
+
     def _unit(self, plan: Plan, k3: ConvNode, k1: ConvNode, B: int, T: int, src: View,
               dst: View) -> None:
-        wo = self.unit_off[k3.name]
         _, b1, a0 = self.w_off[k3.name]
         _, b2, a2 = self.w_off[k1.name]
         arena = lambda o: View("arena", o, 0, 0) if o is not None else None  # noqa: E731
-        C = k3.c_in
-        plan.add(N.OP_UNIT, N.UnitArgs,
-                 dict(channels=C, batch=B, t_len=T, dilation=k3.dilation, pad_left=k3.pad[0],
-                      act=N.ACT[k3.act], leaky_slope=self.cfg.leaky_slope,
-                      x_sb=src.sb, x_sc=src.sc, y_sb=dst.sb, y_sc=dst.sc),
-                 dict(x=src, y=dst, weight=arena(wo), bias1=arena(b1), bias2=arena(b2),
-                      alpha0=arena(a0), alpha2=arena(a2)),
+        C_ = k3.c_in
+        cands = [pr for pr in self.precs if (k3.name, pr) in self.unit_pack]
+
+        def desc(pr, x_sb, x_sc, y_sb, y_sc):
+            s = dict(channels=C_, batch=B, t_len=T, dilation=k3.dilation, pad_left=k3.pad[0],
+                     act=N.ACT[k3.act], leaky_slope=self.cfg.leaky_slope, precision=pr,
+                     x_sb=x_sb, x_sc=x_sc, y_sb=y_sb, y_sc=y_sc)
+            p = dict(weight=arena(self.unit_pack[(k3.name, pr)]), bias1=arena(b1), bias2=arena(b2),
+                     alpha0=arena(a0), alpha2=arena(a2))
+            return s, p
+
+        def run(pr):
+            s, p = desc(pr, C_ * T, T, C_ * T, T)
+            args = N.UnitArgs(**s)
+            keep: list = []
+            self._bind_scratch(args, dict(p, x=View("t", 0, 0, 0), y=View("t", 0, 0, 0)),
+                               {"x": (B, C_, T), "y": (B, C_, T)}, keep)
+            return self._time_native(N.lib.rave_residual_unit, args)
+
+        pr = self._pick(("unit", k3.name, B, T), cands, run)
+        s, p = desc(pr, src.sb, src.sc, dst.sb, dst.sc)
+        plan.add(N.OP_UNIT, N.UnitArgs, s, dict(p, x=src, y=dst),
                  label=k3.name.rsplit(".net.", 1)[0] + ".unit",
-                 flops=2.0 * B * T * C * C * 4)
+                 flops=2.0 * B * T * C_ * C_ * 4)
 
     def _adain_key(self) -> tuple:
         return self.adain.key() + (self.adain_row0,) if self.adain is not None else ()
@@ -334,9 +404,39 @@ class RAVE:
                  label="adain:" + name)
 
     # ------------------------------------------------------------ plan pieces
+    def conv_precision(self, n: ConvNode, scalars: dict, ptrs: Dict[str, Optional[View]],
+                       stream_form: bool = False) -> int:
+        """Precision for one conv op (autotuned when several are available);
+        ``scalars`` / ``ptrs`` describe the op without its precision / weight."""
+        pack = self.w_pack_stream if stream_form else self.w_pack
+
+        def run(pr):
+            s = dict(scalars, precision=pr)
+            args = N.ConvArgs(**s)
+            keep: list = []
+            B, t_in, t_out = s["batch"], s["t_in"], s["t_out"]
+            shapes = {"x": (B, n.c_in, t_in), "y": (B, n.c_out, t_out), "residual": (B, n.c_out, t_out)}
+            p = dict(ptrs, weight=View("arena", pack[(n.name, pr)], 0, 0), partial=None)
+            for f in ("x", "y", "residual"):
+                if p.get(f) is not None:
+                    p[f] = View("t", 0, 0, 0)
+            args.x_sb, args.x_sc = n.c_in * t_in, t_in
+            args.y_sb = args.r_sb = n.c_out * t_out
+            args.y_sc = args.r_sc = t_out
+            self._bind_scratch(args, p, shapes, keep)
+            nws = int(N.lib.rave_conv1d_workspace(C.byref(args)))
+            if nws > 0:
+                ws = torch.empty(nws, device=self.device)
+                keep.append(ws)
+                args.partial = ws.data_ptr()
+            return self._time_native(N.lib.rave_conv1d, args)
+
+        key = ("conv", n.name, stream_form, scalars["batch"], scalars["t_in"])
+        return self._pick(key, self.precs, run)
+
     def _conv(self, plan: Plan, n: ConvNode, B: int, t_in: int, src: View, dst: View,
               res: Optional[View]) -> int:
-        wo, bo, ao = self.w_off[n.name]
+        _, bo, ao = self.w_off[n.name]
         t_out = n.out_len(t_in)
         s = dict(c_in=n.c_in, c_out=n.c_out, kernel=n.kernel, stride=n.stride, dilation=n.dilation,
                  act=N.ACT[n.act], leaky_slope=self.cfg.leaky_slope, batch=B, t_in=t_in, t_out=t_out,
@@ -346,9 +446,12 @@ class RAVE:
             s.update(pad_left=0, pad_right=0, transposed=1, out_shift=n.stride // 2)
         else:
             s.update(pad_left=n.pad[0], pad_right=n.pad[1], transposed=0, out_shift=0)
-        ptrs = dict(x=src, y=dst, residual=res, weight=View("arena", wo, 0, 0),
+        ptrs = dict(x=src, y=dst, residual=res,
                     bias=View("arena", bo, 0, 0) if bo is not None else None,
                     alpha=View("arena", ao, 0, 0) if ao is not None else None)
+        pr = self.conv_precision(n, s, ptrs)
+        s["precision"] = pr
+        ptrs["weight"] = View("arena", self.w_pack[(n.name, pr)], 0, 0)
         ptrs["partial"] = plan.splitk_view(splitk_floats(s, res is not None))
         if n.transposed:
             flops = 2.0 * B * n.c_out * t_out * n.c_in * 2          # 2 taps per output sample

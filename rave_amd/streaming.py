@@ -93,9 +93,7 @@ class StreamingRAVE:
         if n.residual:
             r, h_r, _ = bufs[n.residual]
             res = View("ws", r.off + h_r, r.sb, r.sc)
-        wo, bo, ao = m.w_off[n.name]
-        if n.transposed:
-            wo = m.w_off_stream[n.name]      # packed for the cached form (out_shift 0)
+        _, bo, ao = m.w_off[n.name]
         t_in = need + t_src
         s = dict(c_in=n.c_in, c_out=n.c_out, kernel=n.kernel, stride=n.stride, dilation=n.dilation,
                  pad_left=1 if n.transposed else 0, pad_right=0, transposed=int(n.transposed),
@@ -103,9 +101,14 @@ class StreamingRAVE:
                  act=N.ACT[n.act], leaky_slope=self.cfg.leaky_slope, batch=self.B, t_in=t_in,
                  t_out=t_dst, x_sb=x.sb, x_sc=x.sc, y_sb=y.sb, y_sc=y.sc,
                  r_sb=res.sb if res else 0, r_sc=res.sc if res else 0)
-        ptrs = dict(x=x, y=y, residual=res, weight=View("arena", wo, 0, 0),
+        ptrs = dict(x=x, y=y, residual=res,
                     bias=View("arena", bo, 0, 0) if bo is not None else None,
                     alpha=View("arena", ao, 0, 0) if ao is not None else None)
+        pr = m.conv_precision(n, s, ptrs, stream_form=n.transposed)
+        s["precision"] = pr
+        # ConvTranspose: packed for the cached form (out_shift 0)
+        pack = m.w_pack_stream if n.transposed else m.w_pack
+        ptrs["weight"] = View("arena", pack[(n.name, pr)], 0, 0)
         ptrs["partial"] = plan.splitk_view(splitk_floats(s, res is not None))
         plan.add(N.OP_CONV, N.ConvArgs, s, ptrs, label=n.name)
 

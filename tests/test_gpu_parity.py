@@ -71,9 +71,11 @@ CONV_CASES = [
 ]
 
 
-def run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act, split=True):
+def run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act, split=True,
+             precision=0):
     B, _, T = x.shape
-    packed = torch.from_numpy(N.pack_conv_weight(w, c_in, c_out, k, s, d, transposed)).to(dev)
+    packed = torch.from_numpy(N.pack_conv_weight(w, c_in, c_out, k, s, d, transposed,
+                                                 precision=precision)).to(dev)
     xd = torch.from_numpy(x).to(dev)
     if transposed:
         t_out = T * s
@@ -86,7 +88,7 @@ def run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed,
     a = N.ConvArgs(c_in=c_in, c_out=c_out, kernel=k, stride=s, dilation=d,
                    pad_left=0 if transposed else pad[0], pad_right=0 if transposed else pad[1],
                    transposed=transposed, out_shift=s // 2 if transposed else 0, act=N.ACT[act],
-                   leaky_slope=0.2, batch=B, t_in=T, t_out=t_out,
+                   leaky_slope=0.2, batch=B, t_in=T, t_out=t_out, precision=precision,
                    x=xd.data_ptr(), x_sb=c_in * T, x_sc=T, y=y.data_ptr(), y_sb=c_out * t_out, y_sc=t_out,
                    residual=rd.data_ptr() if rd is not None else None, r_sb=c_out * t_out, r_sc=t_out,
                    weight=packed.data_ptr(), bias=bd.data_ptr() if bd is not None else None,
@@ -103,9 +105,10 @@ def run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed,
     return y.cpu().numpy()
 
 
+@pytest.mark.parametrize("precision", ["f32", "split16"])
 @pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("case", CONV_CASES, ids=[str(c[:8]) for c in CONV_CASES])
-def test_conv_layer(N, dev, case, split):
+def test_conv_layer(N, dev, case, split, precision):
     from oracle.rave_oracle import conv1d, conv_transpose1d, leaky_relu, snake
     c_in, c_out, k, s, d, transposed, act, has_res, B, T = case
     rng = np.random.default_rng(hash(case) & 0xFFFF)
@@ -133,7 +136,7 @@ def test_conv_layer(N, dev, case, split):
     if has_res:
         ref = ref + res
     got = run_conv(N, dev, x, w, b, alpha.reshape(-1) if alpha is not None else None, res,
-                   c_in, c_out, k, s, d, pad, transposed, act, split)
+                   c_in, c_out, k, s, d, pad, transposed, act, split, N.PRECISION[precision])
     assert np.isfinite(got).all()
     assert maxabs(got, ref) <= 2e-5 * max(1.0, np.abs(ref).max())
 
@@ -169,28 +172,35 @@ def test_pqmf_golden(N, dev, golden, causal):
 
 
 # ------------------------------------------------------------------ full model vs golden
-def _model(cfg, g, dev, golden):
+def _model(cfg, g, dev, golden, precision="f32"):
     from rave_amd.model import RAVE
     from rave_amd.weights import init_params
     return RAVE(cfg, init_params(cfg, seed=int(g["seed"])), g["speaker"], device=dev,
-                hk=_golden_hk(golden))
+                hk=_golden_hk(golden), precision=precision)
 
 
+PRECISIONS = ["f32", "split16", "auto"]
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name", ["v2", "causal", "discrete"])
-def test_model_golden(dev, golden, name):
+def test_model_golden(dev, golden, name, precision):
     from rave_amd import config as rcfg
     cfg = rcfg.get_config(name)
     g = golden(name)
-    m = _model(cfg, g, dev, golden)
+    m = _model(cfg, g, dev, golden, precision)
     x = torch.from_numpy(g["x"]).to(dev)
     z = m.encode(x)
     ref_z = g["z_enc"] if name == "discrete" else g["z"]
     zz = z.cpu().numpy()
-    assert maxabs(zz[:, :cfg.latent_size], ref_z[:, :cfg.latent_size]) < TOL
+    ez = maxabs(zz[:, :cfg.latent_size], ref_z[:, :cfg.latent_size])
+    assert ez < TOL
     assert maxabs(zz[:, cfg.latent_size:], g["speaker"][None, :, None]) == 0.0
     y = m.decode(torch.from_numpy(g["z"]).to(dev))
     torch.cuda.synchronize()
-    assert maxabs(y.cpu().numpy(), g["y"]) < TOL
+    ey = maxabs(y.cpu().numpy(), g["y"])
+    print(f"\n[parity] {name} {precision}: z max-abs {ez:.3e}, y max-abs {ey:.3e}")
+    assert ey < TOL
 
 
 def test_discrete_codes_golden(dev, golden):
@@ -241,7 +251,8 @@ def test_rvq_kernels_golden(dev, golden, N):
 
 
 # ------------------------------------------------------------------ larger sizes vs oracle
-def test_v2_full_clip_vs_oracle(dev):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_v2_full_clip_vs_oracle(dev, precision):
     """One 65536-sample clip (BASELINE config 1 size) against the oracle."""
     from oracle.rave_oracle import Oracle
     from rave_amd import config as rcfg
@@ -253,15 +264,18 @@ def test_v2_full_clip_vs_oracle(dev):
     n = np.arange(T)
     x = (0.3 * np.sin(2 * np.pi * 440 * n / 48000)
          + 0.1 * np.random.default_rng(0).standard_normal(T)).astype(np.float32)[None, None]
-    m = RAVE(cfg, params, spk, device=dev)
+    m = RAVE(cfg, params, spk, device=dev, precision=precision)
     z = m.encode(torch.from_numpy(x).to(dev))
     y = m.decode(z)
     torch.cuda.synchronize()
     o = Oracle(cfg, params, spk, hk=m.hk)
     zr = o.encode(x)
-    assert maxabs(z.cpu().numpy(), zr) < TOL
+    ez = maxabs(z.cpu().numpy(), zr)
     yr = o.decode(zr)
-    assert maxabs(y.cpu().numpy(), yr) < TOL
+    ey = maxabs(y.cpu().numpy(), yr)
+    print(f"\n[parity] v2 1x65536 {precision} vs float64 oracle: z {ez:.3e}, y {ey:.3e}")
+    assert ez < TOL
+    assert ey < TOL
 
 
 def test_batch_independence_and_determinism(dev):
@@ -490,8 +504,9 @@ UNIT_CASES = [
 ]
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("case", UNIT_CASES, ids=[str(c) for c in UNIT_CASES])
-def test_residual_unit_kernel(N, dev, case):
+def test_residual_unit_kernel(N, dev, case, precision):
     """rave_residual_unit == x + conv1x1(act(conv3_d(act(x)) + b1)) + b2 (oracle, float64)."""
     from oracle.rave_oracle import conv1d, leaky_relu, snake
     C, d, act, causal, B, T = case
@@ -507,12 +522,17 @@ def test_residual_unit_kernel(N, dev, case):
     f = (lambda v, al: snake(v, al.reshape(-1, 1))) if act == "snake" else (lambda v, al: leaky_relu(v, 0.2))
     h = f(conv1d(f(x.astype(np.float64), a0), w1, b1, 1, d, pad), a2)
     ref = x + conv1d(h, w2, b2, 1, 1, (0, 0))
-    packed = torch.from_numpy(N.pack_unit_weight(w1, w2, C)).to(dev)
+    if precision == "auto":
+        pytest.skip("auto is a per-op choice between the two kernels tested here")
+    prec = N.PRECISION[precision]
+    if not N.unit_supported(C, prec):
+        pytest.skip(f"no fused {precision} unit for C={C} (the model runs it as two convs)")
+    packed = torch.from_numpy(N.pack_unit_weight(w1, w2, C, precision=prec)).to(dev)
     xd = torch.from_numpy(x).to(dev)
     y = torch.full_like(xd, float("nan"))
     dd = {k: torch.from_numpy(v).to(dev) for k, v in dict(b1=b1, b2=b2, a0=a0, a2=a2).items()}
     a = N.UnitArgs(channels=C, batch=B, t_len=T, dilation=d, pad_left=pad[0], act=N.ACT[act],
-                   leaky_slope=0.2, x=xd.data_ptr(), x_sb=C * T, x_sc=T, y=y.data_ptr(), y_sb=C * T,
+                   leaky_slope=0.2, precision=prec, x=xd.data_ptr(), x_sb=C * T, x_sc=T, y=y.data_ptr(), y_sb=C * T,
                    y_sc=T, weight=packed.data_ptr(), bias1=dd["b1"].data_ptr(), bias2=dd["b2"].data_ptr(),
                    alpha0=dd["a0"].data_ptr() if act == "snake" else None,
                    alpha2=dd["a2"].data_ptr() if act == "snake" else None)
@@ -523,16 +543,17 @@ def test_residual_unit_kernel(N, dev, case):
     assert maxabs(got, ref) <= 2e-5 * max(1.0, float(np.abs(ref).max()))
 
 
-def test_fused_units_match_unfused_model(dev):
+@pytest.mark.parametrize("precision,n_fused", [("f32", 22), ("split16", 12), ("auto", 22)])
+def test_fused_units_match_unfused_model(dev, precision, n_fused):
     """The v2 plan with fused residual units equals the conv-by-conv plan."""
     from rave_amd import config as rcfg
     from rave_amd.model import RAVE
     from rave_amd.weights import init_params, init_speaker
     cfg = rcfg.v2()
     params, spk = init_params(cfg, 0), init_speaker(cfg, 0)
-    mf = RAVE(cfg, params, spk, device=dev)
-    mu = RAVE(cfg, params, spk, device=dev, fuse_units=False)
-    assert len(mf.unit_off) == 22 and not mu.unit_off
+    mf = RAVE(cfg, params, spk, device=dev, precision=precision)
+    mu = RAVE(cfg, params, spk, device=dev, fuse_units=False, precision=precision)
+    assert len(mf.unit_off) == n_fused and not mu.unit_off
     g = torch.Generator(device="cpu").manual_seed(1)
     x = (0.1 * torch.randn(4, 1, 65536, generator=g)).to(dev)
     zf, zu = mf.encode(x), mu.encode(x)

@@ -6,6 +6,7 @@ kernel tuning and per-layer PMC profiling:
 """
 import argparse
 import ctypes as C
+import ctypes as C_
 import os
 import sys
 
@@ -33,16 +34,73 @@ LAYERS = {
     "dec_in": (320, 1024, 3, 1, 1, 0, "none", False, 64),
     "wave": (64, 32, 7, 1, 1, 0, "leaky", False, 4096),
 }
+# fused Residual(DilatedUnit): name: (C, d, t per clip)
+UNITS = {"unit_64": (64, 9, 4096), "unit_128": (128, 3, 1024), "unit_256": (256, 3, 256),
+         "unit_512": (512, 3, 128)}
+PREC = 0
 
 
 STAMPS = os.environ.get("RAVE_AMD_DIAG_LIB") == "1"
 
 
+def stamp_report(s_):
+    s_ = s_[s_[:, 7] != 0].astype(np.float64)
+    if not len(s_):
+        return
+    rt = (s_[:, 7] - s_[:, 7].min()) * 10.0 / 1e3   # us (100 MHz)
+    q = lambda v: f"{np.median(v):7.0f} [{np.percentile(v, 10):6.0f},{np.percentile(v, 90):6.0f}]"
+    last = max(k for k in range(7) if (s_[:, k] != 0).all())
+    segs = "  ".join(f"s{k}-{k + 1} {q(s_[:, k + 1] - s_[:, k])}" for k in range(last))
+    print(f"   WGs={len(s_)}  cycles median [p10,p90]: {segs}  total {q(s_[:, last] - s_[:, 0])}; "
+          f"WG start spread {rt.max():.1f} us", flush=True)
+
+
+def run_unit(name, B, iters, dev):
+    C, d, T = UNITS[name]
+    rng = np.random.default_rng(0)
+    w1 = (rng.standard_normal((C, C, 3)) / np.sqrt(3 * C)).astype(np.float32)
+    w2 = (rng.standard_normal((C, C, 1)) / np.sqrt(C)).astype(np.float32)
+    packed = torch.from_numpy(N.pack_unit_weight(w1, w2, C, precision=PREC)).to(dev)
+    x = torch.randn(B, C, T, device=dev)
+    y = torch.empty_like(x)
+    b1, b2 = torch.randn(C, device=dev), torch.randn(C, device=dev)
+    a = N.UnitArgs(channels=C, batch=B, t_len=T, dilation=d, pad_left=d, act=N.ACT["leaky"],
+                   leaky_slope=0.2, precision=PREC, x=x.data_ptr(), x_sb=C * T, x_sc=T, y=y.data_ptr(),
+                   y_sb=C * T, y_sc=T, weight=packed.data_ptr(), bias1=b1.data_ptr(), bias2=b2.data_ptr())
+    st = C_.c_void_p(torch.cuda.current_stream().cuda_stream)
+    stamps = None
+    if STAMPS and PREC == N.PREC_SPLIT16:
+        stamps = torch.zeros(8 * 200000, dtype=torch.int64, device=dev)
+        N.check(N.lib.rave_diag_unit_stamps(C_.c_void_p(stamps.data_ptr())))
+    for _ in range(3):
+        N.check(N.lib.rave_residual_unit(C_.byref(a), st))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        N.check(N.lib.rave_residual_unit(C_.byref(a), st))
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    fl = 2.0 * B * T * C * C * 4
+    mb = 3 * B * C * T * 4 / 1e6
+    print(f"{name:12s} B={B}  {ms * 1e3:8.2f} us  {fl / ms / 1e9:7.2f} TFLOP/s  "
+          f"{mb / ms / 1e3:6.2f} TB/s (x, y, residual)", flush=True)
+    if stamps is not None:
+        stamps.zero_()
+        N.check(N.lib.rave_residual_unit(C_.byref(a), st))
+        torch.cuda.synchronize()
+        stamp_report(stamps.view(-1, 8).cpu().numpy())
+        N.check(N.lib.rave_diag_unit_stamps(C_.c_void_p(0)))
+    return ms
+
+
 def run(name, B, iters, dev):
+    if name in UNITS:
+        return run_unit(name, B, iters, dev)
     ci, co, k, s, d, tr, act, has_res, T = LAYERS[name]
     rng = np.random.default_rng(0)
     w = rng.uniform(-0.05, 0.05, (ci, co, k) if tr else (co, ci, k)).astype(np.float32)
-    packed = torch.from_numpy(N.pack_conv_weight(w, ci, co, k, s, d, tr)).to(dev)
+    packed = torch.from_numpy(N.pack_conv_weight(w, ci, co, k, s, d, tr, precision=PREC)).to(dev)
     x = torch.randn(B, ci, T, device=dev)
     if tr:
         t_out, pl, pr = T * s, 0, 0
@@ -55,7 +113,7 @@ def run(name, B, iters, dev):
     bias = torch.randn(co, device=dev)
     a = N.ConvArgs(c_in=ci, c_out=co, kernel=k, stride=s, dilation=d, pad_left=pl, pad_right=pr,
                    transposed=tr, out_shift=s // 2 if tr else 0, act=N.ACT[act], leaky_slope=0.2,
-                   batch=B, t_in=T, t_out=t_out, x=x.data_ptr(), x_sb=ci * T, x_sc=T,
+                   batch=B, t_in=T, t_out=t_out, precision=PREC, x=x.data_ptr(), x_sb=ci * T, x_sc=T,
                    y=y.data_ptr(), y_sb=co * t_out, y_sc=t_out,
                    residual=res.data_ptr() if res is not None else None, r_sb=co * t_out, r_sc=t_out,
                    weight=packed.data_ptr(), bias=bias.data_ptr())
@@ -84,22 +142,19 @@ def run(name, B, iters, dev):
         stamps.zero_()
         N.check(N.lib.rave_conv1d(C.byref(a), st))
         torch.cuda.synchronize()
-        s_ = stamps.view(-1, 8).cpu().numpy()
-        s_ = s_[s_[:, 7] != 0].astype(np.float64)
-        pro, main, epi, tot = (s_[:, 1] - s_[:, 0], s_[:, 2] - s_[:, 1], s_[:, 3] - s_[:, 2], s_[:, 3] - s_[:, 0])
-        rt = (s_[:, 7] - s_[:, 7].min()) * 10.0 / 1e3   # us (100 MHz)
-        q = lambda v: f"{np.median(v):8.0f} [{np.percentile(v, 10):7.0f},{np.percentile(v, 90):7.0f}]"
-        print(f"   WGs={len(s_)}  cycles median [p10,p90]: prologue {q(pro)} main {q(main)} "
-              f"epilogue {q(epi)} total {q(tot)}; WG start spread {rt.max():.1f} us", flush=True)
+        stamp_report(stamps.view(-1, 8).cpu().numpy())
     return ms
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--layers", default=",".join(LAYERS))
+    ap.add_argument("--layers", default=",".join(list(LAYERS) + list(UNITS)))
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--precision", default="split16", choices=["f32", "split16"])
     a = ap.parse_args()
+    global PREC
+    PREC = N.PRECISION[a.precision]
     dev = torch.device("cuda")
     for name in a.layers.split(","):
         run(name, a.batch, a.iters, dev)
