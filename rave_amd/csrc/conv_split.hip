@@ -101,6 +101,18 @@ __device__ __forceinline__ void dma16b(u32x4_t rsrc, unsigned voff, uint32_t lds
     asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_dst) : "memory");
 }
+// 16-byte register load through a buffer descriptor, hidden from hipcc's vmcnt
+// bookkeeping (form (ii) of the guide: the consumer waits with the registers
+// named "+v"); out-of-range offsets read zeros
+__device__ __forceinline__ u32x4_t bload16(u32x4_t rsrc, unsigned voff) {
+    u32x4_t r;
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(r) : "v"(voff), "s"(rsrc) : "memory");
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_regs(u32x4_t& a0, u32x4_t& a1) {
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a0), "+v"(a1) : "n"(N) : "memory");
+}
 template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -130,8 +142,7 @@ template <int KT, int BM, int BN, int WM, bool XV = true> struct SGeo {
     static constexpr int XW_MAX = BN + (Q - 1) * F::DMAX + (KT == 2 ? 1 : 0);
     static constexpr int PH = VC + 8;                        // halves per plane row (conflict-free b128)
     static constexpr int XPLANE = XW_MAX * PH * 2;           // bytes per f16 plane
-    static constexpr int WCHUNK = (BM / 32) * KSC * 2 * 1024;   // weight image of one chunk
-    static constexpr int WI = WCHUNK / 1024 / NW;            // 1 KB weight DMA pieces per wave
+    static constexpr int WR = KSC * NJ * 2;                  // weight fragment loads per wave per chunk
     // raw window rows: XV = 16-byte pieces from a 4-sample-aligned start (row
     // stride rounded up to 4 samples), else 4-byte pieces
     static constexpr int RS_MAX = XV ? ((XW_MAX * S + 3 + 3) / 4) * 4 : XW_MAX * S;
@@ -139,16 +150,18 @@ template <int KT, int BM, int BN, int WM, bool XV = true> struct SGeo {
     static constexpr int PF = XV ? 4 : 1;                    // floats per lane per DMA
     static constexpr int XI = (RAW_F + 64 * PF * NW - 1) / (64 * PF * NW);   // window DMA pieces per wave
     static constexpr int RAW = XI * NW * 256 * PF;           // raw window bytes (with slack)
-    static constexpr int STAGE = WCHUNK + RAW;
-    static constexpr int NS = 3;                             // DMA ring depth
-    static constexpr int LDS = NS * STAGE + 2 * XPLANE;      // ring + one (hi, lo) plane pair
-    static constexpr int DPC = WI + XI;                      // DMA instructions per wave per chunk
+    static constexpr int STAGE = RAW;
+    static constexpr int NS = 3;                             // window DMA ring depth
+    static constexpr int ALPHA = 4096;                       // Snake alphas (<= 1024 channels)
+    static constexpr int EROW = WN + 4;                      // epilogue transpose row stride (floats)
+    static constexpr int EPI = NW * WM * EROW * 4;           // epilogue transpose area (reuses the ring)
+    static constexpr int MAIN = NS * STAGE + 2 * 2 * XPLANE + ALPHA;  // ring + two (hi, lo) plane pairs
+    static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
     static constexpr int G8 = VC / 8;                        // 8-channel groups per row
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;   // convert tasks per thread
-    static_assert(WCHUNK % (1024 * NW) == 0, "weight image must split over the waves");
     static_assert(XPLANE % 16 == 0 && STAGE % 16 == 0, "16-byte LDS alignment");
     static_assert(NI * NJ == 4 && NW >= 1 && NW <= 8, "tile");
-    static_assert(DPC <= 60, "vmcnt range");
+    static_assert(WR + XI <= 63, "vmcnt range");
 };
 
 template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV>
@@ -201,10 +214,15 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
     const int ci_lim = min(a.c_in, c_end * CPC);  // window DMA past c_end lands zeros
     const u32x4_t xrs = raw_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);
     const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
-    const char* wsrc = reinterpret_cast<const char*>(a.w) + (size_t)(m0 / 32) * KSC * 2 * 1024;
-    const size_t wchunk_stride = (size_t)a.MB * KSC * 2 * 1024;
+    const u32x4_t wrs = raw_rsrc(a.w, a.w_bytes);
+    const unsigned wcstride = (unsigned)(a.MB * KSC * 2) * 1024u;
+    const unsigned wbase = (unsigned)((mw / 32) * KSC * 2) * 1024u + (unsigned)lane * 16u;
     const uint32_t lds0 = lds_addr(smem);
     char* planes = smem + G::NS * G::STAGE;
+    float* alpha_s = reinterpret_cast<float*>(smem + G::NS * G::STAGE + 4 * G::XPLANE);
+    if constexpr (SNAKE) {
+        for (int i = tid; i < a.c_in; i += NT) alpha_s[i] = a.alpha[i];
+    }
 
     floatx16 acc[NI][NJ];
 #pragma unroll
@@ -229,16 +247,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
         e_bias[j] = (a.bias && rowok && a.S == 1) ? a.bias[co] : 0.f;
     }
 
-    // chunk c -> ring stage (weights: clamped to the last real chunk; window:
-    // per-lane offsets, out-of-range -> zeros)
+    // window of chunk c -> ring slot (per-lane offsets, out-of-range -> zeros)
     auto issue = [&](int c, int stage) __attribute__((always_inline)) {
         const uint32_t sbase = lds0 + stage * G::STAGE;
-        const char* src = wsrc + (size_t)min(c, a.nchunks - 1) * wchunk_stride;
-#pragma unroll
-        for (int i = 0; i < G::WI; ++i) {
-            const int piece = i * NW + wave;
-            dma16(src + piece * 1024 + lane * 16, sbase + piece * 1024);
-        }
         const int ci0 = c * CPC;
 #pragma unroll
         for (int i = 0; i < G::XI; ++i) {
@@ -250,18 +261,28 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
             const int t = ta + tt * G::PF;
             const bool ok = (cl < CPC) && (ci < ci_lim) && (t >= 0) && (t < a.t_in);
             const unsigned voff = ok ? (unsigned)(ci * a.x_sc + t) * 4u : kOOB;
-            if constexpr (XV) dma16b(xrs, voff, sbase + G::WCHUNK + piece * 1024);
-            else dma4(xrs, voff, sbase + G::WCHUNK + piece * 256);
+            if constexpr (XV) dma16b(xrs, voff, sbase + piece * 1024);
+            else dma4(xrs, voff, sbase + piece * 256);
         }
     };
-    // raw window of a stage -> activation -> (hi, lo) f16 planes
-    auto convert = [&](int c, int stage) __attribute__((always_inline)) {
-        const float* raw = reinterpret_cast<const float*>(smem + stage * G::STAGE + G::WCHUNK);
-        _Float16* xh = reinterpret_cast<_Float16*>(planes);
-        _Float16* xl = reinterpret_cast<_Float16*>(planes + G::XPLANE);
-        const int ci0 = c * CPC;
+    // this wave's weight fragments: register ring, one chunk ahead (chunks past
+    // the packed image read zeros)
+    u32x4_t wr[KSC][NJ][2];
+    auto load_w = [&](int c, int st) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < XT; ++i) {
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl)
+                wr[st][j][pl] = bload16(wrs, wbase + (unsigned)c * wcstride +
+                                                 (unsigned)(((j * KSC + st) * 2 + pl) * 1024));
+    };
+    // raw window of a stage -> activation -> (hi, lo) f16 planes
+    auto convert_task = [&](int c, int stage, int pb, int i) __attribute__((always_inline)) {
+        const float* raw = reinterpret_cast<const float*>(smem + stage * G::STAGE);
+        _Float16* xh = reinterpret_cast<_Float16*>(planes + pb * 2 * G::XPLANE);
+        _Float16* xl = reinterpret_cast<_Float16*>(planes + pb * 2 * G::XPLANE + G::XPLANE);
+        const int ci0 = c * CPC;
+        {
             const int e = tid + i * NT;
             const int g = (int)(((unsigned)e * a.xw_magic) >> 24);
             const int w = e - g * XW;
@@ -272,7 +293,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
                     const int vc = g * 8 + v;
                     float val = raw[(vc / S) * RS + off0 + w * S + (vc % S)];
                     if constexpr (SNAKE) {
-                        const float al = a.alpha[min(ci0 + vc / S, a.c_in - 1)];
+                        const float al = alpha_s[min(ci0 + vc / S, a.c_in - 1)];
                         val = val + (1.0f / (al + 1e-9f)) * sin_squared(al * val);
                     } else {
                         val = val > 0.f ? val : val * slope;
@@ -286,81 +307,97 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
             }
         }
     };
+    auto convert = [&](int c, int stage, int pb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < XT; ++i) convert_task(c, stage, pb, i);
+    };
 
     // per-lane A-fragment offsets (halves): window row wn*WN + l32 + q*d (+ group shift)
     int xoff[G::Q];
 #pragma unroll
     for (int q = 0; q < G::Q; ++q) xoff[q] = (wn * WN + l32 + q * a.d + gshift) * PH + 8 * h;
 
-    struct Frag {
-        s_h8 ah[NI], al[NI], bh[NJ], bl[NJ];
+    struct AFrag {
+        s_h8 h[NI], l[NI];
     };
-    auto read_frag = [&](int stage, int st, Frag& f) __attribute__((always_inline)) {
+    auto read_a = [&](int pb, int st, AFrag& f) __attribute__((always_inline)) {
         const int q = st / HPS, hv = st - q * HPS;
-        const _Float16* xh = reinterpret_cast<const _Float16*>(planes);
-        const _Float16* xl = reinterpret_cast<const _Float16*>(planes + G::XPLANE);
+        const _Float16* xh = reinterpret_cast<const _Float16*>(planes + pb * 2 * G::XPLANE);
+        const _Float16* xl = reinterpret_cast<const _Float16*>(planes + pb * 2 * G::XPLANE + G::XPLANE);
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            f.ah[i] = *reinterpret_cast<const s_h8*>(xh + xoff[q] + i * 32 * PH + hv * 16);
-            f.al[i] = *reinterpret_cast<const s_h8*>(xl + xoff[q] + i * 32 * PH + hv * 16);
-        }
-        const char* wimg = smem + stage * G::STAGE;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const char* p = wimg + (((wm * NJ + j) * KSC + st) * 2) * 1024 + lane * 16;
-            f.bh[j] = *reinterpret_cast<const s_h8*>(p);
-            f.bl[j] = *reinterpret_cast<const s_h8*>(p + 1024);
+            f.h[i] = *reinterpret_cast<const s_h8*>(xh + xoff[q] + i * 32 * PH + hv * 16);
+            f.l[i] = *reinterpret_cast<const s_h8*>(xl + xoff[q] + i * 32 * PH + hv * 16);
         }
     };
 
     // ------------------------------------------------------------ prologue
+    // vmcnt bookkeeping (every load below is hand-counted asm): per chunk a
+    // wave issues XI window DMAs, then per K-step 2*NJ weight loads.
+    constexpr int WR = G::WR, XI = G::XI;
     issue(c_begin, 0);
     issue(c_begin + 1, 1);
-    wait_vm<G::DPC>();
+#pragma unroll
+    for (int st = 0; st < KSC; ++st) load_w(c_begin, st);
+    wait_vm<XI + WR>();                     // window c_begin landed
     __syncthreads();
-    convert(c_begin, 0);
+    convert(c_begin, 0, 0);
+    wait_vm<WR>();                          // window c_begin+1 landed
     __syncthreads();
     stamp(1);
 
-    // per chunk: DMA two chunks ahead | MFMAs | wait + barrier | split the next
-    // chunk's window into the (single) plane pair | barrier
+    // per chunk c: DMA window c+2 | K-steps (weights of c from the ring, refill
+    // with c+1) | split window c+1 into the other plane pair | wait + barrier
     int stage = 0;
     for (int c = c_begin; c < c_end; ++c) {
-        issue(c + 2, stage == 0 ? 2 : stage - 1);       // = (stage + 2) % 3
-        Frag f[2];
-        read_frag(stage, 0, f[0]);
+        const int pb = (c - c_begin) & 1;
+        const int s1 = stage == 2 ? 0 : stage + 1;
+        const int s2 = s1 == 2 ? 0 : s1 + 1;
+        issue(c + 2, s2);
+        AFrag f[2];
+        read_a(pb, 0, f[0]);
 #pragma unroll
         for (int st = 0; st < KSC; ++st) {
-            if (st + 1 < KSC) read_frag(stage, st + 1, f[(st + 1) & 1]);   // next reads in flight
+            if (st + 1 < KSC) read_a(pb, st + 1, f[(st + 1) & 1]);   // next reads in flight
+            // weights of (c, st): issued one chunk ago; younger: the rest of that
+            // chunk's weights, this chunk's window DMA and this chunk's earlier refills
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) wait_vm_regs<2 * (WR / 2 - NJ) + XI>(wr[st][j][0], wr[st][j][1]);
             __builtin_amdgcn_sched_barrier(0);
-            const Frag& g = f[st & 1];
-            s_h8 b2[NJ];
+            const AFrag& g = f[st & 1];
+            s_h8 bh[NJ], bl[NJ], b2[NJ];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) b2[j] = g.bh[j] * (_Float16)2048.0f;
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.ah[i], b2[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.al[i], g.bh[j], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < NJ; ++j) {
+                bh[j] = __builtin_bit_cast(s_h8, wr[st][j][0]);
+                bl[j] = __builtin_bit_cast(s_h8, wr[st][j][1]);
+                b2[j] = bh[j] * (_Float16)2048.0f;
+            }
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.ah[i], g.bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.h[i], b2[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.l[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.h[i], bl[j], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            load_w(c + 1, st);              // refill the slot one chunk ahead
+            // split part of window c+1 into the other plane pair (VALU beside the MFMAs)
+            if (c + 1 < c_end) {
+#pragma unroll
+                for (int i = st; i < XT; i += KSC) convert_task(c + 1, s1, pb ^ 1, i);
+            }
         }
-        const int nstage = stage == 2 ? 0 : stage + 1;
-        wait_vm<G::DPC>();                  // chunk c+1 landed (c+2 may still fly)
-        __syncthreads();                    // ... for every wave; the planes / chunk c's weights free
-        if (c + 1 < c_end) {
-            convert(c + 1, nstage);
-            __syncthreads();
-        }
-        stage = nstage;
+        wait_vm<WR>();                      // window c+2 landed (weights of c+1 may fly)
+        __syncthreads();
+        stage = s1;
         if (c == c_begin) stamp(2);
     }
     stamp(3);
@@ -374,44 +411,111 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] *= e_rs[j];
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * e_rs[j] + e_bias[j];
     }
-    if (partial) {
-        const __amdgpu_buffer_rsrc_t prs = make_rsrc(
-            a.partial + ((int64_t)split * a.B + b) * (int64_t)a.M * a.U, a.M * a.U * 4);
+    if (!a.transposed || partial) {     // (split-K slabs are GEMM rows even for ConvT)
+        // Row-contiguous stores: each wave parks its WM x WN tile in LDS (the
+        // ring is dead) and re-reads it so that a store instruction writes whole
+        // rows (the accumulator layout gives 16-byte pieces of 32 rows).
+        __syncthreads();
+        float* et = reinterpret_cast<float*>(smem) + wave * WM * G::EROW;
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int m = mw + j * 32 + l32;
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const int n = n0 + wn * WN + i * 32 + 8 * g + 4 * h;
-                    if (a.vec_p && m < a.M && n + 3 < a.U) {
-                        const s_f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
-                                           acc[i][j][4 * g + 3]};
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), prs,
-                                                               (unsigned)(m * a.U + n) * 4u, 0, 0);
-                    } else {
+                    const s_f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                                       acc[i][j][4 * g + 3]};
+                    *reinterpret_cast<s_f32x4*>(et + (j * 32 + l32) * G::EROW + i * 32 + 8 * g + 4 * h) = v;
+                }
+        __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0): own writes landed (wave-private area)
+        constexpr int LPR = WN / 4;                  // lanes per row
+        constexpr int RPI = 64 / LPR;                // rows per instruction
+        const int rr = lane / LPR, cc = (lane % LPR) * 4;
+        const int n = n0 + wn * WN + cc;
+        if (partial) {
+            const __amdgpu_buffer_rsrc_t prs = make_rsrc(
+                a.partial + ((int64_t)split * a.B + b) * (int64_t)a.M * a.U, a.M * a.U * 4);
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const unsigned off = (m < a.M && n + e < a.U) ? (unsigned)(m * a.U + n + e) * 4u : kOOB;
-                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][j][4 * g + e]),
-                                                                  prs, off, 0, 0);
-                        }
+            for (int it = 0; it < WM / RPI; ++it) {
+                const int r = it * RPI + rr;
+                const int m = mw + r;
+                const float* vp = et + r * G::EROW + cc;
+                if (a.vec_p && m < a.M && n + 3 < a.U) {
+                    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4_t*>(vp), prs,
+                                                           (unsigned)(m * a.U + n) * 4u, 0, 0);
+                } else {
+                    // element-wise tail (no ext-vector lane indexing here: hipcc
+                    // miscompiled v[e] of an LDS-loaded vector in this branch)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const unsigned off = (m < a.M && n + e < a.U) ? (unsigned)(m * a.U + n + e) * 4u : kOOB;
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, vp[e]), prs, off, 0, 0);
                     }
                 }
+            }
+            stamp(4);
+            return;
+        }
+        const __amdgpu_buffer_rsrc_t yrs = make_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
+        const __amdgpu_buffer_rsrc_t rrs = make_rsrc(a.res ? a.res + (int64_t)b * a.r_sb : a.y, a.res ? a.r_bytes : 0);
+        if (a.vec_y) {
+            s_f32x4 rv[WM / RPI];
+#pragma unroll
+            for (int it = 0; it < WM / RPI; ++it) {  // every residual load before the first store
+                const int m = mw + it * RPI + rr;
+                const bool ok = a.res && m < a.M && n + 3 < a.U;
+                rv[it] = __builtin_bit_cast(s_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                    rrs, ok ? (unsigned)(m * a.r_sc + n) * 4u : kOOB, 0, 0));
+            }
+#pragma unroll
+            for (int it = 0; it < WM / RPI; ++it) {
+                const int r = it * RPI + rr;
+                const int m = mw + r;
+                const s_f32x4 v = *reinterpret_cast<const s_f32x4*>(et + r * G::EROW + cc) + rv[it];
+                if (m < a.M && n + 3 < a.U) {
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), yrs,
+                                                           (unsigned)(m * a.y_sc + n) * 4u, 0, 0);
+                } else {
+                    float vv[4];
+                    *reinterpret_cast<s_f32x4*>(vv) = *reinterpret_cast<const s_f32x4*>(et + r * G::EROW + cc);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const bool ok = m < a.M && n + e < a.U;
+                        const float rs = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                            rrs, ok ? (unsigned)(m * a.r_sc + n + e) * 4u : kOOB, 0, 0));
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, vv[e] + rs), yrs,
+                                                              ok ? (unsigned)(m * a.y_sc + n + e) * 4u : kOOB, 0, 0);
+                    }
+                }
+            }
+        } else {                                    // unaligned rows: element-wise
+#pragma unroll
+            for (int it = 0; it < WM / RPI; ++it) {
+                const int r = it * RPI + rr;
+                const int m = mw + r;
+                const float* vp = et + r * G::EROW + cc;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const bool ok = m < a.M && n + e < a.U;
+                    const float rs = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        rrs, ok ? (unsigned)(m * a.r_sc + n + e) * 4u : kOOB, 0, 0));
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, vp[e] + rs), yrs,
+                                                          ok ? (unsigned)(m * a.y_sc + n + e) * 4u : kOOB, 0, 0);
+                }
+            }
         }
         stamp(4);
         return;
     }
     const __amdgpu_buffer_rsrc_t yrs = make_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
-    if (a.transposed) {
+    {   // ConvTranspose: phase-interleaved columns t = n*R + q, one store per element
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int co = e_co[j], q = e_q[j];
             const bool rowok = co < a.bias_rows;
-            const float bv = e_bias[j];
+            const float bv = 0.f;   // added above
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -423,41 +527,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
                 }
         }
         stamp(4);
-        return;
     }
-    const __amdgpu_buffer_rsrc_t rrs = make_rsrc(a.res ? a.res + (int64_t)b * a.r_sb : a.y, a.res ? a.r_bytes : 0);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const int m = mw + j * 32 + l32;
-        const float bv = e_bias[j];
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int n = n0 + wn * WN + i * 32 + 8 * g + 4 * h;
-                if (a.vec_y && m < a.M && n + 3 < a.U) {
-                    s_f32x4 rv = {0.f, 0.f, 0.f, 0.f};
-                    if (a.res)
-                        rv = __builtin_bit_cast(s_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                            rrs, (unsigned)(m * a.r_sc + n) * 4u, 0, 0));
-                    const s_f32x4 v = {acc[i][j][4 * g] + bv + rv[0], acc[i][j][4 * g + 1] + bv + rv[1],
-                                       acc[i][j][4 * g + 2] + bv + rv[2], acc[i][j][4 * g + 3] + bv + rv[3]};
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), yrs,
-                                                           (unsigned)(m * a.y_sc + n) * 4u, 0, 0);
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const bool ok = m < a.M && n + e < a.U;
-                        const float rv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                            rrs, ok ? (unsigned)(m * a.r_sc + n + e) * 4u : kOOB, 0, 0));
-                        __builtin_amdgcn_raw_buffer_store_b32(
-                            __builtin_bit_cast(unsigned, acc[i][j][4 * g + e] + bv + rv), yrs,
-                            ok ? (unsigned)(m * a.y_sc + n + e) * 4u : kOOB, 0, 0);
-                    }
-                }
-            }
-    }
-    stamp(4);
 }
 
 // Sum the split-K slabs in split order (fixed order: deterministic), then
@@ -628,6 +698,7 @@ int conv1d_split(const rave_conv1d_args& a, void* stream) {
     int taps;
     int rc = split_prepare(a, k, taps);
     if (rc != RAVE_OK) return rc;
+    RAVE_CHECK_ARG(a.act != RAVE_ACT_SNAKE || a.c_in <= 1024, "conv1d(split16): Snake on more than 1024 channels");
     SplitCfg c = split_choose(taps, k.M, k.U, k.B, k.nchunks, k.split_row);
     if (c.S > 1 && a.partial == nullptr) c.S = 1;
     k.cps = ceil_div(k.nchunks, c.S);
