@@ -239,7 +239,7 @@ class RAVE:
         # plan-build time on scratch tensors of its own shape; the faster is kept
         self.precs = [N.PREC_F32, N.PREC_SPLIT16] if precision == "auto" else [N.PRECISION[precision]]
         self.prec = self.precs[-1]
-        self._tuned: Dict[tuple, int] = {}
+        self._tuned: Dict[tuple, Tuple[int, float]] = {}   # op key -> (choice, ms)
         self.cfg = cfg
         self.graph = build_graph(cfg)
         self.device = torch.device(device if device is not None else "cuda")
@@ -345,18 +345,39 @@ class RAVE:
                 keep.append(t)
                 setattr(args, field, t.data_ptr())
 
-    def _pick(self, key: tuple, cands: List[int], run) -> int:
-        """The faster precision of ``cands`` for the op ``key`` (cached); ``run(prec)``
-        returns milliseconds."""
-        if len(cands) == 1:
+    def _pick(self, key: tuple, cands: List[int], run, timed: bool = False) -> int:
+        """The faster precision of ``cands`` for the op ``key`` (cached with its
+        time); ``run(prec)`` returns milliseconds.  A single candidate is only
+        timed when ``timed`` (its time is wanted by a fusion decision)."""
+        if len(cands) == 1 and not timed:
             return cands[0]
         if key not in self._tuned:
             times = {pr: run(pr) for pr in cands}
-            self._tuned[key] = min(times, key=times.get)
-        return self._tuned[key]
+            best = min(times, key=times.get)
+            self._tuned[key] = (best, times[best])
+        return self._tuned[key][0]
 
-    def _unit(self, plan: Plan, k3: ConvNode, k1: ConvNode, B: int, T: int, src: View,
-              dst: View) -> None:
+    def _fuse_unit(self, k3: ConvNode, k1: ConvNode, B: int, T: int, src: View) -> bool:
+        """Run Residual(DilatedUnit) as the fused kernel (True) or as its two
+        convs (False): with several precisions the faster by measurement
+        (e.g. exact-fp32 fused against two split-f16 convs at C=512)."""
+        if len(self.precs) == 1:
+            return True
+        key = ("fuse", k3.name, B, T)
+        if key not in self._tuned:
+            fused_ms = self._unit_time(k3, k1, B, T)
+            tmp = View("t", 0, k3.c_out * T, T)
+            s3, p3 = self._conv_desc(k3, B, T, src, tmp, None)
+            self.conv_precision(k3, s3, p3, timed=True)
+            s1, p1 = self._conv_desc(k1, B, T, tmp, tmp, src)
+            self.conv_precision(k1, s1, p1, timed=True)
+            split_ms = (self._tuned[self._conv_key(k3, False, s3)][1]
+                        + self._tuned[self._conv_key(k1, False, s1)][1])
+            self._tuned[key] = (fused_ms <= split_ms, min(fused_ms, split_ms))
+        return bool(self._tuned[key][0])
+
+    def _unit_parts(self, k3: ConvNode, k1: ConvNode, B: int, T: int):
+        """(descriptor builder, fused-kernel precisions, timing run) of one unit."""
         _, b1, a0 = self.w_off[k3.name]
         _, b2, a2 = self.w_off[k1.name]
         arena = lambda o: View("arena", o, 0, 0) if o is not None else None  # noqa: E731
@@ -379,6 +400,18 @@ class RAVE:
                                {"x": (B, C_, T), "y": (B, C_, T)}, keep)
             return self._time_native(N.lib.rave_residual_unit, args)
 
+        return desc, cands, run
+
+    def _unit_time(self, k3: ConvNode, k1: ConvNode, B: int, T: int) -> float:
+        _, cands, run = self._unit_parts(k3, k1, B, T)
+        key = ("unit", k3.name, B, T)
+        self._pick(key, cands, run, timed=True)
+        return self._tuned[key][1]
+
+    def _unit(self, plan: Plan, k3: ConvNode, k1: ConvNode, B: int, T: int, src: View,
+              dst: View) -> None:
+        desc, cands, run = self._unit_parts(k3, k1, B, T)
+        C_ = k3.c_in
         pr = self._pick(("unit", k3.name, B, T), cands, run)
         s, p = desc(pr, src.sb, src.sc, dst.sb, dst.sc)
         plan.add(N.OP_UNIT, N.UnitArgs, s, dict(p, x=src, y=dst),
@@ -404,8 +437,12 @@ class RAVE:
                  label="adain:" + name)
 
     # ------------------------------------------------------------ plan pieces
+    @staticmethod
+    def _conv_key(n: ConvNode, stream_form: bool, scalars: dict) -> tuple:
+        return ("conv", n.name, stream_form, scalars["batch"], scalars["t_in"])
+
     def conv_precision(self, n: ConvNode, scalars: dict, ptrs: Dict[str, Optional[View]],
-                       stream_form: bool = False) -> int:
+                       stream_form: bool = False, timed: bool = False) -> int:
         """Precision for one conv op (autotuned when several are available);
         ``scalars`` / ``ptrs`` describe the op without its precision / weight."""
         pack = self.w_pack_stream if stream_form else self.w_pack
@@ -431,11 +468,11 @@ class RAVE:
                 args.partial = ws.data_ptr()
             return self._time_native(N.lib.rave_conv1d, args)
 
-        key = ("conv", n.name, stream_form, scalars["batch"], scalars["t_in"])
-        return self._pick(key, self.precs, run)
+        return self._pick(self._conv_key(n, stream_form, scalars), self.precs, run, timed)
 
-    def _conv(self, plan: Plan, n: ConvNode, B: int, t_in: int, src: View, dst: View,
-              res: Optional[View]) -> int:
+    def _conv_desc(self, n: ConvNode, B: int, t_in: int, src: View, dst: View,
+                   res: Optional[View]) -> Tuple[dict, Dict[str, Optional[View]]]:
+        """Scalars and pointer views of one conv op, without precision / weight."""
         _, bo, ao = self.w_off[n.name]
         t_out = n.out_len(t_in)
         s = dict(c_in=n.c_in, c_out=n.c_out, kernel=n.kernel, stride=n.stride, dilation=n.dilation,
@@ -449,6 +486,12 @@ class RAVE:
         ptrs = dict(x=src, y=dst, residual=res,
                     bias=View("arena", bo, 0, 0) if bo is not None else None,
                     alpha=View("arena", ao, 0, 0) if ao is not None else None)
+        return s, ptrs
+
+    def _conv(self, plan: Plan, n: ConvNode, B: int, t_in: int, src: View, dst: View,
+              res: Optional[View]) -> int:
+        t_out = n.out_len(t_in)
+        s, ptrs = self._conv_desc(n, B, t_in, src, dst, res)
         pr = self.conv_precision(n, s, ptrs)
         s["precision"] = pr
         ptrs["weight"] = View("arena", self.w_pack[(n.name, pr)], 0, 0)
@@ -478,7 +521,7 @@ class RAVE:
             src, t_in, _ = tensors[n.src]
             if n.adain and self.adain is not None and self.adain.active:
                 self._adain_op(plan, n.adain, B, n.c_in, t_in, src)
-            if n.name in fused:
+            if n.name in fused and self._fuse_unit(n, fused[n.name], B, t_in, src):
                 # Residual(DilatedUnit) in one kernel; the k=3 output never exists in HBM
                 k1 = fused[n.name]
                 skip.add(k1.name)
