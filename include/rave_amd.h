@@ -40,7 +40,9 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 4
+#define RAVE_ABI_VERSION 5
+/* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
+#define RAVE_SPLITK_TICKETS 4096
 
 /* ---------------------------------------------------------------- status */
 enum {
@@ -107,10 +109,17 @@ typedef struct rave_conv1d_args {
     const float* weight;  /* packed by rave_conv1d_pack_weight                   */
     const float* bias;    /* c_out floats or NULL                                */
     const float* alpha;   /* c_in Snake alphas (act == RAVE_ACT_SNAKE)           */
-    float* partial;       /* split-K slab of rave_conv1d_workspace() floats, or
-                             NULL (then the layer runs unsplit)                 */
+    float* partial;       /* split-K workspace of rave_conv1d_workspace() floats, or
+                             NULL (then the layer runs unsplit).  Its first
+                             RAVE_SPLITK_TICKETS 4-byte words are arrival
+                             counters: zero them once before the first call;
+                             every call leaves them zero again.  The slabs
+                             after them need no initialisation.              */
     unsigned long long* stamps;   /* diagnostic builds only (-DRAVE_STAMPS): 8 clock
                                      stamps per workgroup; ignored otherwise      */
+    int32_t config;       /* launch configuration: 0 = the launcher's own choice,
+                             else one of rave_conv1d_configs() for these args  */
+    int32_t _pad1;
 } rave_conv1d_args;
 
 /* Supported layer families (every RAVE conv): kernel 1/3/7 stride 1, kernel 4
@@ -125,7 +134,13 @@ int64_t rave_conv1d_packed_size(int c_in, int c_out, int kernel, int stride, int
  * ConvTranspose1d: (c_in, c_out, k)) into the kernel's K-chunked layout. */
 int rave_conv1d_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
                             int dilation, int transposed, int out_shift, float* packed);
-/* floats of split-K workspace the launcher would use for these args (0 = none) */
+/* Launch configurations (tile shape, K-splits, split-K combine) valid for
+ * these args and precision, for plan-time autotuning (cf. cuDNN's Find API):
+ * writes up to max_cfgs values for rave_conv1d_args.config into cfgs and
+ * returns how many exist (0 is always valid and is not listed), or an error. */
+int rave_conv1d_configs(const rave_conv1d_args* a, int32_t* cfgs, int max_cfgs);
+/* floats of split-K workspace the launcher would use for these args (0 = none);
+ * RAVE_SPLITK_TICKETS counter words + the fp32 slabs */
 int64_t rave_conv1d_workspace(const rave_conv1d_args* a);
 /* RAVE_PREC_SPLIT16 weight image: per K-chunk, per 32-row block, per K-step of
  * 16, the (hi, lo) f16 MFMA A-fragments in lane order, then one float row scale

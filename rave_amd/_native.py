@@ -35,7 +35,8 @@ OP_COPY = 8
 OP_NOISE = 9
 OP_ADAIN = 10
 OP_UNIT = 11
-ABI_VERSION = 4
+ABI_VERSION = 5
+SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 
 # GEMM arithmetic of conv / unit ops (include/rave_amd.h RAVE_PREC_*)
 PREC_F32 = 0
@@ -53,7 +54,8 @@ class ConvArgs(C.Structure):
                 ("x", vp), ("x_sb", i64), ("x_sc", i64),
                 ("y", vp), ("y_sb", i64), ("y_sc", i64),
                 ("residual", vp), ("r_sb", i64), ("r_sc", i64),
-                ("weight", vp), ("bias", vp), ("alpha", vp), ("partial", vp), ("stamps", vp)]
+                ("weight", vp), ("bias", vp), ("alpha", vp), ("partial", vp), ("stamps", vp),
+                ("config", i32), ("_pad1", i32)]
 
 
 class AnalysisArgs(C.Structure):
@@ -141,7 +143,7 @@ STRUCTS = [ConvArgs, AnalysisArgs, SynthesisArgs, FillArgs, RvqArgs, ShiftArgs, 
 EXPORTS = [
     "rave_last_error", "rave_abi_version", "rave_struct_sizes",
     "rave_conv1d_chunk", "rave_conv1d_packed_size", "rave_conv1d_pack_weight", "rave_conv1d",
-    "rave_conv1d_workspace", "rave_conv1d_split_packed_size", "rave_conv1d_split_pack_weight",
+    "rave_conv1d_workspace", "rave_conv1d_configs", "rave_conv1d_split_packed_size", "rave_conv1d_split_pack_weight",
     "rave_pqmf_analysis", "rave_pqmf_synthesis", "rave_fill_channels", "rave_copy",
     "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
     "rave_unit_packed_size", "rave_unit_pack_weight", "rave_residual_unit",
@@ -169,6 +171,7 @@ def _load():
     lib.rave_conv1d_packed_size.restype = i64
     lib.rave_conv1d_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
     lib.rave_conv1d_workspace.argtypes = [C.POINTER(ConvArgs)]
+    lib.rave_conv1d_configs.argtypes = [C.POINTER(ConvArgs), C.POINTER(i32), C.c_int]
     lib.rave_conv1d_split_packed_size.argtypes = [C.c_int] * 6
     lib.rave_conv1d_split_packed_size.restype = i64
     lib.rave_conv1d_split_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
@@ -219,6 +222,15 @@ def check(rc: int, what: str = "") -> None:
     if rc == RAVE_ERR_UNSUPPORTED:
         raise NotImplementedError(text)
     raise NativeError(f"{text} (status {rc})")
+
+
+def conv_configs(args: "ConvArgs") -> list:
+    """Launch configurations valid for ``args`` (rave_conv1d_configs), without 0."""
+    buf = (i32 * 256)()
+    n = int(lib.rave_conv1d_configs(C.byref(args), buf, 256))
+    if n < 0:
+        check(n, "conv1d_configs")
+    return [int(buf[i]) for i in range(min(n, 256))]
 
 
 def conv_chunk(c_in, kernel, stride, dilation, transposed) -> int:

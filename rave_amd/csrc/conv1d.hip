@@ -338,8 +338,10 @@ static int family_cit(int taps) {
 // Tile + split-K choice.  Prefer the largest tile (fewest K-groups) that gives
 // >= 2 workgroups per CU with little padding; otherwise the least-padding tile
 // with K split across workgroups until ~2 workgroups per CU.
+constexpr int kF32Tiles[5][2] = {{128, 128}, {64, 256}, {128, 64}, {64, 128}, {64, 64}};
+
 static LaunchCfg choose(int M, int U, int B, int nchunks, int split_row = 1 << 30) {
-    const int all[5][2] = {{128, 128}, {64, 256}, {128, 64}, {64, 128}, {64, 64}};
+    const auto& all = kF32Tiles;
     int cand[5][2], nc = 0;
     for (auto& c : all)   // a tile may not straddle the ConvT phase-group boundary
         if (split_row >= M || split_row % c[0] == 0) { cand[nc][0] = c[0]; cand[nc][1] = c[1]; ++nc; }
@@ -496,6 +498,46 @@ extern "C" int rave_conv1d_pack_weight(const float* w, int c_in, int c_out, int 
     return RAVE_OK;
 }
 
+static bool f32_tile_ok(int ti, int M, int split_row) {
+    return ti >= 0 && ti < 5 && (split_row >= M || split_row % kF32Tiles[ti][0] == 0);
+}
+
+// The launch configuration: args.config when set (validated), else the heuristic.
+static int resolve(const rave_conv1d_args& a, const ConvKArgs& k, LaunchCfg& c) {
+    if (a.config == 0) {
+        c = choose(k.M, k.U, k.B, k.nchunks, k.split_row);
+        return RAVE_OK;
+    }
+    ConfigCode cc;
+    RAVE_CHECK_ARG(decode_config(a.config, cc) && cc.sep == 0 && f32_tile_ok(cc.tile, k.M, k.split_row) &&
+                       split_count_distinct(cc.S, k.nchunks),
+                   "conv1d: config not valid for these args (see rave_conv1d_configs)");
+    c = {kF32Tiles[cc.tile][0], kF32Tiles[cc.tile][1], cc.S};
+    return RAVE_OK;
+}
+
+extern "C" int rave_conv1d_configs(const rave_conv1d_args* p, int32_t* cfgs, int max_cfgs) {
+    RAVE_CHECK_ARG(p && max_cfgs >= 0, "conv1d_configs: null args");
+    if (p->precision == RAVE_PREC_SPLIT16) return conv1d_split_configs(*p, cfgs, max_cfgs);
+    RAVE_CHECK_ARG(p->precision == RAVE_PREC_F32, "conv1d_configs: unknown precision");
+    ConvKArgs k;
+    int taps;
+    int rc = prepare(*p, k, taps);
+    if (rc != RAVE_OK) return rc;
+    int n = 0;
+    for (int ti = 0; ti < 5; ++ti) {
+        if (!f32_tile_ok(ti, k.M, k.split_row)) continue;
+        const int64_t wg = (int64_t)ceil_div(k.M, kF32Tiles[ti][0]) * ceil_div(k.U, kF32Tiles[ti][1]) * k.B;
+        for (int S : kSplitCands) {
+            if (!split_count_distinct(S, k.nchunks)) continue;
+            if (S > 1 && (wg * S > 8192 || wg >= 1024)) continue;      // enough workgroups unsplit
+            if (n < max_cfgs && cfgs) cfgs[n] = encode_config(ti, S, 0);
+            ++n;
+        }
+    }
+    return n;
+}
+
 extern "C" int64_t rave_conv1d_workspace(const rave_conv1d_args* p) {
     if (!p) return -1;
     if (p->precision == RAVE_PREC_SPLIT16) return conv1d_split_workspace(*p);
@@ -503,9 +545,10 @@ extern "C" int64_t rave_conv1d_workspace(const rave_conv1d_args* p) {
     ConvKArgs k;
     int taps;
     if (prepare(*p, k, taps) != RAVE_OK) return -1;
-    LaunchCfg c = choose(k.M, k.U, k.B, k.nchunks, k.split_row);
+    LaunchCfg c;
+    if (resolve(*p, k, c) != RAVE_OK) return -1;
     if (c.S <= 1) return 0;
-    return (int64_t)c.S * k.B * (int64_t)k.M * k.U;
+    return kSplitTickets + (int64_t)c.S * k.B * (int64_t)k.M * k.U;   // same layout as the split path
 }
 
 extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
@@ -516,11 +559,13 @@ extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
     int taps;
     int rc = prepare(*p, k, taps);
     if (rc != RAVE_OK) return rc;
-    LaunchCfg c = choose(k.M, k.U, k.B, k.nchunks, k.split_row);
+    LaunchCfg c;
+    rc = resolve(*p, k, c);
+    if (rc != RAVE_OK) return rc;
     if (c.S > 1 && p->partial == nullptr) c.S = 1;   // no workspace given: single pass
     k.cps = ceil_div(k.nchunks, c.S);
     k.S = ceil_div(k.nchunks, k.cps);                 // no empty splits
-    k.partial = p->partial;
+    k.partial = p->partial ? p->partial + kSplitTickets : nullptr;   // slabs after the counters
 #ifdef RAVE_STAMPS
     k.stamps = p->stamps;
 #endif

@@ -13,6 +13,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));   // native vector (HIP
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
+constexpr int kSplitTickets = RAVE_SPLITK_TICKETS;   // int32 words ahead of the split-K slabs
 constexpr int kMaxDil = 16;       // largest dilation of a 3-tap conv the kernels stage
 
 struct ConvKArgs {
@@ -37,6 +38,9 @@ struct ConvKArgs {
     int vec_y, vec_p;             // split path: 16-byte epilogue stores allowed (y/res, slabs)
     unsigned rl_magic;            // split path: ceil(2^32 / raw window row length)
     int x_vec;                    // split path: 16-byte window DMA allowed
+    int* tickets;                 // split path: per-tile arrival counters (zero between calls)
+    int gx, gy;                   // split path: column / row tiles per batch item (1-D grid)
+    int inlaunch;                 // split path: the last-arriving K-split sums the slabs
 };
 
 // Buffer descriptor from wave-uniform inputs (guide T8/T20).
@@ -108,6 +112,27 @@ static inline int convt_group1_row(int c_out, int R, int q0) {
 struct LaunchCfg {
     int bm, bn, S;
 };
+
+// rave_conv1d_args.config: 0 = heuristic, else 1 + tile + 8 (S - 1) + 256 sep
+// (tile: index into the precision's tile table; S: K-splits; sep: split-K
+// combine in a separate reduce launch instead of in-launch)
+struct ConfigCode {
+    int tile, S, sep;
+};
+static inline bool decode_config(int cfg, ConfigCode& c) {
+    if (cfg <= 0) return false;
+    const int v = cfg - 1;
+    c.tile = v & 7;
+    c.S = ((v >> 3) & 31) + 1;
+    c.sep = (v >> 8) & 1;
+    return (v >> 9) == 0;
+}
+static inline int encode_config(int tile, int S, int sep) { return 1 + tile + 8 * (S - 1) + 256 * sep; }
+// K-split counts the autotuner tries (an S whose chunks per split equal a smaller S's is skipped)
+constexpr int kSplitCands[] = {1, 2, 3, 4, 6, 8, 12, 16};
+static inline bool split_count_distinct(int S, int nchunks) {
+    return S <= nchunks && ceil_div(nchunks, ceil_div(nchunks, S)) == S;
+}
 
 static inline double pad_waste(int M, int U, int bm, int bn) {
     return double(ceil_div(M, bm) * bm) * double(ceil_div(U, bn) * bn) / (double(M) * double(U));
@@ -192,5 +217,6 @@ static inline int prepare_common(const rave_conv1d_args& a, ConvKArgs& k, int& t
 // RAVE_PREC_SPLIT16 path (conv_split.hip)
 int conv1d_split(const rave_conv1d_args& a, void* stream);
 int64_t conv1d_split_workspace(const rave_conv1d_args& a);
+int conv1d_split_configs(const rave_conv1d_args& a, int32_t* cfgs, int max_cfgs);
 
 }  // namespace rave

@@ -157,6 +157,7 @@ template <int KT, int BM, int BN, int WM, bool XV = true> struct SGeo {
     static constexpr int EPI = NW * WM * EROW * 4;           // epilogue transpose area (reuses the ring)
     static constexpr int MAIN = NS * STAGE + 2 * 2 * XPLANE + ALPHA;  // ring + two (hi, lo) plane pairs
     static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
+    static constexpr int LDS_ALL = LDS + 16;                 // + the split-K "last arriver" word
     static constexpr int G8 = VC / 8;                        // 8-channel groups per row
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;   // convert tasks per thread
     static_assert(XPLANE % 16 == 0 && STAGE % 16 == 0, "16-byte LDS alignment");
@@ -177,7 +178,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
 
     const int tid = threadIdx.x;
 #ifdef RAVE_STAMPS
-    const int wg_lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int wg_lin = blockIdx.x;
     auto stamp = [&](int k) {
         if (tid == 0 && a.stamps) {
             a.stamps[wg_lin * 8 + k] = __builtin_amdgcn_s_memtime();
@@ -193,11 +194,20 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
     const int wm = wave % WGM, wn = wave / WGM;
     const int h = lane >> 5, l32 = lane & 31;
 
-    const int n0 = blockIdx.x * BN;
-    const int m0 = blockIdx.y * BM;
+    // 1-D grid, logical id remapped so that consecutive ids -- a tile's K-splits,
+    // then neighbouring tiles -- land on one XCD (blocks are dealt round-robin
+    // over the 8 XCDs): split-K slabs are summed out of the XCD's own L2.
+    int lg = blockIdx.x;
+    if ((gridDim.x & 7) == 0) lg = (lg & 7) * (gridDim.x >> 3) + (lg >> 3);
+    lg = __builtin_amdgcn_readfirstlane(lg);
+    const int tix = __builtin_amdgcn_readfirstlane(lg / a.S);          // tile (ticket) index
+    const int split = __builtin_amdgcn_readfirstlane(lg - tix * a.S);
+    const int bxy = __builtin_amdgcn_readfirstlane(tix % (a.gx * a.gy));
+    const int b = __builtin_amdgcn_readfirstlane(tix / (a.gx * a.gy));
+    const int by = __builtin_amdgcn_readfirstlane(bxy / a.gx);
+    const int n0 = (bxy - by * a.gx) * BN;
+    const int m0 = by * BM;
     const int mw = m0 + wm * WM;                 // this wave's first GEMM row
-    const int b = __builtin_amdgcn_readfirstlane(blockIdx.z / a.S);
-    const int split = __builtin_amdgcn_readfirstlane(blockIdx.z - b * a.S);
     const int c_begin = split * a.cps;
     const int c_end = min(a.nchunks, c_begin + a.cps);
     // input time of window row 0 (ConvT: group 0's window; group 1 reads one row later)
@@ -455,6 +465,87 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
                     }
                 }
             }
+            if (!a.inlaunch) {
+                stamp(4);
+                return;
+            }
+            // In-launch combine (guide §5 "In-launch split-K reduction"): publish the
+            // slab with an agent-scope release, draw a ticket; the split that draws
+            // S-1 acquires and sums every slab of the tile in split order.
+            wait_vm<0>();
+            __syncthreads();
+            volatile int* last_s = reinterpret_cast<volatile int*>(smem + G::LDS);
+            if (tid == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                wait_vm<0>();
+                const int prev = __hip_atomic_fetch_add(a.tickets + tix, 1, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+                const int last = prev == a.S - 1;
+                if (last) {
+                    __hip_atomic_store(a.tickets + tix, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    wait_vm<0>();
+                }
+                *last_s = last;
+            }
+            __syncthreads();
+            if (!*last_s) {
+                stamp(4);
+                return;
+            }
+            constexpr int IT = WM / RPI;
+            s_f32x4 sum[IT];
+#pragma unroll
+            for (int it = 0; it < IT; ++it) sum[it] = s_f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int s = 0; s < a.S; ++s) {        // slabs outer: IT independent loads per round trip
+                const __amdgpu_buffer_rsrc_t srs = make_rsrc(
+                    a.partial + ((int64_t)s * a.B + b) * (int64_t)a.M * a.U, a.M * a.U * 4);
+                s_f32x4 pv[IT];
+#pragma unroll
+                for (int it = 0; it < IT; ++it) {
+                    const int m = mw + it * RPI + rr;
+                    const bool ok = m < a.M && n < a.U;          // U % 4 == 0 here (vec_p)
+                    pv[it] = __builtin_bit_cast(s_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                        srs, ok ? (unsigned)(m * a.U + n) * 4u : kOOB, 0, 0));
+                }
+#pragma unroll
+                for (int it = 0; it < IT; ++it) sum[it] += pv[it];
+            }
+            // then the separate reduce's store_out: + bias, + residual, ConvT interleave
+            if (!a.transposed && a.vec_y) {
+                const __amdgpu_buffer_rsrc_t yrs = make_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
+                const __amdgpu_buffer_rsrc_t rrs =
+                    make_rsrc(a.res ? a.res + (int64_t)b * a.r_sb : a.y, a.res ? a.r_bytes : 0);
+                s_f32x4 rv[IT];
+#pragma unroll
+                for (int it = 0; it < IT; ++it) {
+                    const int m = mw + it * RPI + rr;
+                    const bool ok = a.res && m < a.M && n < a.U;
+                    rv[it] = __builtin_bit_cast(s_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                        rrs, ok ? (unsigned)(m * a.r_sc + n) * 4u : kOOB, 0, 0));
+                }
+#pragma unroll
+                for (int it = 0; it < IT; ++it) {
+                    const int m = mw + it * RPI + rr;
+                    if (m < a.M && n < a.U) {
+                        s_f32x4 v = sum[it];
+                        if (a.bias) v += a.bias[m];
+                        if (a.res) v += rv[it];
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), yrs,
+                                                               (unsigned)(m * a.y_sc + n) * 4u, 0, 0);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int it = 0; it < IT; ++it) {
+                    const int m = mw + it * RPI + rr;
+                    float vv[4];
+                    *reinterpret_cast<s_f32x4*>(vv) = sum[it];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (m < a.M && n + e < a.U) store_out(a, b, m, n + e, vv[e]);
+                }
+            }
             stamp(4);
             return;
         }
@@ -556,7 +647,7 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(ConvKArgs a) {
 
 // --------------------------------------------------------------------- host side
 struct SplitCfg {
-    int bm, bn, wm, S;
+    int bm, bn, wm, S, sep;
 };
 
 // Tile + split-K choice.  Tiles (BM rows x BN columns, wave WM x 4096/WM):
@@ -568,12 +659,12 @@ constexpr int kSplitTiles[6][3] = {{128, 128, 32}, {64, 256, 32}, {64, 128, 32},
 template <int KT>
 static bool split_tile_fits(int idx) {   // the 4-byte-DMA variant is the larger one
     switch (idx) {
-        case 0: return SGeo<KT, 128, 128, 32, true>::LDS <= 160 * 1024 && SGeo<KT, 128, 128, 32, false>::LDS <= 160 * 1024;
-        case 1: return SGeo<KT, 64, 256, 32, true>::LDS <= 160 * 1024 && SGeo<KT, 64, 256, 32, false>::LDS <= 160 * 1024;
-        case 2: return SGeo<KT, 64, 128, 32, true>::LDS <= 160 * 1024 && SGeo<KT, 64, 128, 32, false>::LDS <= 160 * 1024;
-        case 3: return SGeo<KT, 256, 64, 64, true>::LDS <= 160 * 1024 && SGeo<KT, 256, 64, 64, false>::LDS <= 160 * 1024;
-        case 4: return SGeo<KT, 128, 64, 64, true>::LDS <= 160 * 1024 && SGeo<KT, 128, 64, 64, false>::LDS <= 160 * 1024;
-        default: return SGeo<KT, 64, 64, 64, true>::LDS <= 160 * 1024 && SGeo<KT, 64, 64, 64, false>::LDS <= 160 * 1024;
+        case 0: return SGeo<KT, 128, 128, 32, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 128, 128, 32, false>::LDS_ALL <= 160 * 1024;
+        case 1: return SGeo<KT, 64, 256, 32, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 64, 256, 32, false>::LDS_ALL <= 160 * 1024;
+        case 2: return SGeo<KT, 64, 128, 32, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 64, 128, 32, false>::LDS_ALL <= 160 * 1024;
+        case 3: return SGeo<KT, 256, 64, 64, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 256, 64, 64, false>::LDS_ALL <= 160 * 1024;
+        case 4: return SGeo<KT, 128, 64, 64, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 128, 64, 64, false>::LDS_ALL <= 160 * 1024;
+        default: return SGeo<KT, 64, 64, 64, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 64, 64, 64, false>::LDS_ALL <= 160 * 1024;
     }
 }
 static bool split_fits(int taps, int idx) {
@@ -592,7 +683,7 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
     auto waste = [&](int bm, int bn) {
         return double(ceil_div(M, bm) * bm) * double(ceil_div(U, bn) * bn) / (double(M) * double(U));
     };
-    SplitCfg best{64, 64, 64, 1};
+    SplitCfg best{64, 64, 64, 1, 0};
     double bscore = 1e30;
     for (int ti = 0; ti < 6; ++ti) {
         const int* c = all[ti];
@@ -604,7 +695,7 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
         double score = waste(c[0], c[1]);
         if (waves < 1024) score *= 1.0 + 0.5 * (1024.0 / waves - 1.0) / std::max(1, nchunks / 8);
         score *= 1.0 + 0.03 * (4 - nw);                                 // prefer fat workgroups
-        if (score < bscore) { bscore = score; best = {c[0], c[1], c[2], 1}; }
+        if (score < bscore) { bscore = score; best = {c[0], c[1], c[2], 1, 0}; }
     }
     const int nw = (best.bm / best.wm) * (best.bn / (4096 / best.wm));
     const int64_t waves = (int64_t)ceil_div(M, best.bm) * ceil_div(U, best.bn) * B * nw;
@@ -619,7 +710,7 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
 template <int KT, int BM, int BN, int WM, bool XV>
 static int split_launch_xv(ConvKArgs k, hipStream_t st) {
     using G = SGeo<KT, BM, BN, WM, XV>;
-    if constexpr (G::LDS > 160 * 1024) {
+    if constexpr (G::LDS_ALL > 160 * 1024) {
         set_error("conv1d(split16): tile exceeds LDS");
         return RAVE_ERR_UNSUPPORTED;
     } else {
@@ -627,9 +718,9 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
         set_error("conv1d(split16): dilation too large for the staged window");
         return RAVE_ERR_UNSUPPORTED;
     }
-    constexpr size_t lds = (size_t)G::LDS;
+    constexpr size_t lds = (size_t)G::LDS_ALL;
     static_assert(lds <= 160 * 1024, "LDS budget");
-    dim3 grid(ceil_div(k.U, BN), ceil_div(k.M, BM), k.B * k.S);
+    dim3 grid(k.gx * k.gy * k.B * k.S);
     const bool snake = k.act == RAVE_ACT_SNAKE;
     auto kern = snake ? conv1d_split_kernel<KT, BM, BN, WM, true, XV> : conv1d_split_kernel<KT, BM, BN, WM, false, XV>;
     if (lds > 64 * 1024) {
@@ -684,13 +775,59 @@ static int split_prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
     return RAVE_OK;
 }
 
+static bool split_tile_ok(int taps, int ti, int M, int split_row) {
+    return ti >= 0 && ti < 6 && split_fits(taps, ti) &&
+           (split_row >= M || split_row % kSplitTiles[ti][2] == 0);   // a wave never straddles ConvT groups
+}
+
+// The launch configuration: args.config when set (validated), else the heuristic.
+static int split_resolve(const rave_conv1d_args& a, const ConvKArgs& k, int taps, SplitCfg& c) {
+    if (a.config == 0) {
+        c = split_choose(taps, k.M, k.U, k.B, k.nchunks, k.split_row);
+        return RAVE_OK;
+    }
+    ConfigCode cc;
+    RAVE_CHECK_ARG(decode_config(a.config, cc) && split_tile_ok(taps, cc.tile, k.M, k.split_row) &&
+                       split_count_distinct(cc.S, k.nchunks),
+                   "conv1d(split16): config not valid for these args (see rave_conv1d_configs)");
+    c = {kSplitTiles[cc.tile][0], kSplitTiles[cc.tile][1], kSplitTiles[cc.tile][2], cc.S, cc.sep};
+    return RAVE_OK;
+}
+
+int conv1d_split_configs(const rave_conv1d_args& a, int32_t* cfgs, int max_cfgs) {
+    ConvKArgs k;
+    int taps;
+    int rc = split_prepare(a, k, taps);
+    if (rc != RAVE_OK) return rc;
+    int n = 0;
+    auto put = [&](int v) {
+        if (n < max_cfgs && cfgs) cfgs[n] = v;
+        ++n;
+    };
+    for (int ti = 0; ti < 6; ++ti) {
+        if (!split_tile_ok(taps, ti, k.M, k.split_row)) continue;
+        const int* t = kSplitTiles[ti];
+        const int nw = (t[0] / t[2]) * (t[1] / (4096 / t[2]));
+        const int64_t ntiles = (int64_t)ceil_div(k.M, t[0]) * ceil_div(k.U, t[1]) * k.B;
+        for (int S : kSplitCands) {
+            if (!split_count_distinct(S, k.nchunks)) continue;
+            const int64_t waves = ntiles * nw * S;
+            if (S > 1 && (waves > 16384 || ntiles * nw >= 4096)) continue;   // enough waves unsplit
+            if (S == 1 || ntiles <= kSplitTickets) put(encode_config(ti, S, 0));
+            if (S > 1) put(encode_config(ti, S, 1));
+        }
+    }
+    return n;
+}
+
 int64_t conv1d_split_workspace(const rave_conv1d_args& a) {
     ConvKArgs k;
     int taps;
     if (split_prepare(a, k, taps) != RAVE_OK) return -1;
-    SplitCfg c = split_choose(taps, k.M, k.U, k.B, k.nchunks, k.split_row);
+    SplitCfg c;
+    if (split_resolve(a, k, taps, c) != RAVE_OK) return -1;
     if (c.S <= 1) return 0;
-    return (int64_t)c.S * k.B * (int64_t)k.M * k.U;
+    return kSplitTickets + (int64_t)c.S * k.B * (int64_t)k.M * k.U;
 }
 
 int conv1d_split(const rave_conv1d_args& a, void* stream) {
@@ -699,11 +836,21 @@ int conv1d_split(const rave_conv1d_args& a, void* stream) {
     int rc = split_prepare(a, k, taps);
     if (rc != RAVE_OK) return rc;
     RAVE_CHECK_ARG(a.act != RAVE_ACT_SNAKE || a.c_in <= 1024, "conv1d(split16): Snake on more than 1024 channels");
-    SplitCfg c = split_choose(taps, k.M, k.U, k.B, k.nchunks, k.split_row);
+    SplitCfg c;
+    rc = split_resolve(a, k, taps, c);
+    if (rc != RAVE_OK) return rc;
     if (c.S > 1 && a.partial == nullptr) c.S = 1;
     k.cps = ceil_div(k.nchunks, c.S);
     k.S = ceil_div(k.nchunks, k.cps);
-    k.partial = a.partial;
+    k.tickets = reinterpret_cast<int*>(a.partial);
+    k.partial = a.partial ? a.partial + kSplitTickets : nullptr;   // slabs after the counters
+    k.vec_p = (k.U % 4 == 0) && (!k.partial || reinterpret_cast<uintptr_t>(k.partial) % 16 == 0);
+    k.gx = ceil_div(k.U, c.bn);
+    k.gy = ceil_div(k.M, c.bm);
+    const int64_t ntiles = (int64_t)k.gx * k.gy * k.B;
+    RAVE_CHECK_ARG(ntiles * k.S < (1ll << 31), "conv1d(split16): grid too large");
+    // the last-arriving split sums the tile's slabs (16-byte slab rows, counters for every tile)
+    k.inlaunch = k.S > 1 && !c.sep && k.vec_p && ntiles <= kSplitTickets;
 #ifdef RAVE_STAMPS
     k.stamps = a.stamps;
 #endif
@@ -717,7 +864,7 @@ int conv1d_split(const rave_conv1d_args& a, void* stream) {
         case 8: rc = split_launch_family<8>(k, c, st); break;
         default: set_error("conv1d: unsupported kernel size"); return RAVE_ERR_UNSUPPORTED;
     }
-    if (rc != RAVE_OK || k.S <= 1) return rc;
+    if (rc != RAVE_OK || k.S <= 1 || k.inlaunch) return rc;
     RAVE_CHECK_ARG((int64_t)k.B * k.M <= 65535, "conv1d(split16): too many rows for the split-K reduce");
     launch(split_reduce_kernel, dim3(ceil_div(k.U, 1024), k.B * k.M), dim3(256), 0, st, k);
     return launch_status("split_reduce_kernel");

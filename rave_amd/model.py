@@ -131,6 +131,7 @@ class Plan:
         self.sym: List[Tuple[int, type, dict, dict]] = []
         self.labels: List[str] = []
         self.flops: List[float] = []
+        self.nbytes: List[float] = []     # algorithmic HBM bytes (tensors read/written once)
         self.handle = None
         self.ws_tensor: Optional[torch.Tensor] = None
         self._splitk: List[View] = []
@@ -146,7 +147,7 @@ class Plan:
         return v
 
     def add(self, kind: int, st: type, scalars: dict, ptrs: Dict[str, Optional[View]],
-            label: str = "", flops: float = 0.0):
+            label: str = "", flops: float = 0.0, nbytes: float = 0.0):
         self.sym.append((kind, st, scalars, ptrs))
         self.labels.append(label or {N.OP_CONV: "conv", N.OP_PQMF_ANALYSIS: "pqmf_analysis",
                                      N.OP_PQMF_SYNTHESIS: "pqmf_synthesis", N.OP_FILL: "fill",
@@ -154,6 +155,7 @@ class Plan:
                                      N.OP_SHIFT_HISTORY: "shift_history", N.OP_COPY: "copy",
                                      N.OP_NOISE: "noise_synth", N.OP_ADAIN: "adain"}.get(kind, "op"))
         self.flops.append(float(flops))
+        self.nbytes.append(float(nbytes))
 
     def finalize(self, device) -> "Plan":
         # The slab is live at different points of the plan than any tensor, so it
@@ -162,6 +164,8 @@ class Plan:
         splitk_off = self.splitk_off = self.ws.top
         self.ws.top += ((self.splitk_max + Workspace.ALIGN - 1) // Workspace.ALIGN) * Workspace.ALIGN
         self.ws_tensor = torch.empty(max(self.ws.top, 1), dtype=torch.float32, device=device)
+        if self.splitk_max > 0:     # split-K arrival counters start (and stay) zero
+            self.ws_tensor[splitk_off:splitk_off + N.SPLITK_TICKETS].zero_()
         n = len(self.sym)
         ops = (N.PlanOp * max(n, 1))()
         relocs = []
@@ -230,7 +234,8 @@ class RAVE:
     def __init__(self, cfg: RaveConfig, params: Mapping[str, np.ndarray], speaker: np.ndarray,
                  device=None, hk: Optional[np.ndarray] = None,
                  adain_stats: Optional[Mapping] = None, fuse_units: bool = True,
-                 precision: str = "f32"):
+                 precision: str = "f32", tuning: Optional[list] = None,
+                 autotune: Optional[bool] = None):
         check_params(cfg, params)
         if precision not in list(N.PRECISION) + ["auto"]:
             raise ValueError(f"precision must be one of {sorted(N.PRECISION) + ['auto']}")
@@ -239,7 +244,12 @@ class RAVE:
         # plan-build time on scratch tensors of its own shape; the faster is kept
         self.precs = [N.PREC_F32, N.PREC_SPLIT16] if precision == "auto" else [N.PRECISION[precision]]
         self.prec = self.precs[-1]
+        # launch configurations (tile, K-splits) timed per conv op at plan build:
+        # by default with "auto" precision, else the launchers' heuristics
+        self.autotune = precision == "auto" if autotune is None else bool(autotune)
         self._tuned: Dict[tuple, Tuple[int, float]] = {}   # op key -> (choice, ms)
+        if tuning:                  # choices recorded by tuning() of an earlier model
+            self._tuned = {tuple(k): (c, ms) for k, c, ms in tuning}
         self.cfg = cfg
         self.graph = build_graph(cfg)
         self.device = torch.device(device if device is not None else "cuda")
@@ -317,6 +327,11 @@ class RAVE:
         return out
 
     # ------------------------------------------------------------ per-op precision choice
+    def tuning(self) -> list:
+        """The autotuner's choices so far, JSON-serialisable; pass it back as
+        ``RAVE(..., tuning=...)`` to build the same plans without timing runs."""
+        return [[list(k), int(c), float(ms)] for k, (c, ms) in self._tuned.items()]
+
     def _time_native(self, fn, args, reps: int = 5) -> float:
         st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
         for _ in range(2):
@@ -368,9 +383,9 @@ class RAVE:
             fused_ms = self._unit_time(k3, k1, B, T)
             tmp = View("t", 0, k3.c_out * T, T)
             s3, p3 = self._conv_desc(k3, B, T, src, tmp, None)
-            self.conv_precision(k3, s3, p3, timed=True)
+            self.conv_launch(k3, s3, p3, timed=True)
             s1, p1 = self._conv_desc(k1, B, T, tmp, tmp, src)
-            self.conv_precision(k1, s1, p1, timed=True)
+            self.conv_launch(k1, s1, p1, timed=True)
             split_ms = (self._tuned[self._conv_key(k3, False, s3)][1]
                         + self._tuned[self._conv_key(k1, False, s1)][1])
             self._tuned[key] = (fused_ms <= split_ms, min(fused_ms, split_ms))
@@ -416,7 +431,7 @@ class RAVE:
         s, p = desc(pr, src.sb, src.sc, dst.sb, dst.sc)
         plan.add(N.OP_UNIT, N.UnitArgs, s, dict(p, x=src, y=dst),
                  label=k3.name.rsplit(".net.", 1)[0] + ".unit",
-                 flops=2.0 * B * T * C_ * C_ * 4)
+                 flops=2.0 * B * T * C_ * C_ * 4, nbytes=4.0 * (2 * B * C_ * T + 4 * C_ * C_))
 
     def _adain_key(self) -> tuple:
         return self.adain.key() + (self.adain_row0,) if self.adain is not None else ()
@@ -441,34 +456,60 @@ class RAVE:
     def _conv_key(n: ConvNode, stream_form: bool, scalars: dict) -> tuple:
         return ("conv", n.name, stream_form, scalars["batch"], scalars["t_in"])
 
-    def conv_precision(self, n: ConvNode, scalars: dict, ptrs: Dict[str, Optional[View]],
-                       stream_form: bool = False, timed: bool = False) -> int:
-        """Precision for one conv op (autotuned when several are available);
-        ``scalars`` / ``ptrs`` describe the op without its precision / weight."""
+    def conv_launch(self, n: ConvNode, scalars: dict, ptrs: Dict[str, Optional[View]],
+                    stream_form: bool = False, timed: bool = False) -> Tuple[int, int]:
+        """(precision, launch config) of one conv op.  With ``autotune`` every
+        precision and every launch configuration rave_conv1d_configs() lists
+        (tile shape, K-splits, split-K combine) is timed once on scratch tensors
+        of the op's shape and the fastest kept; else config 0 (the launcher's
+        heuristic).  ``scalars`` / ``ptrs`` describe the op without them."""
         pack = self.w_pack_stream if stream_form else self.w_pack
-
-        def run(pr):
-            s = dict(scalars, precision=pr)
-            args = N.ConvArgs(**s)
-            keep: list = []
-            B, t_in, t_out = s["batch"], s["t_in"], s["t_out"]
+        key = self._conv_key(n, stream_form, scalars)
+        if key not in self._tuned and (len(self.precs) > 1 or timed or self.autotune):
+            B, t_in, t_out = scalars["batch"], scalars["t_in"], scalars["t_out"]
             shapes = {"x": (B, n.c_in, t_in), "y": (B, n.c_out, t_out), "residual": (B, n.c_out, t_out)}
-            p = dict(ptrs, weight=View("arena", pack[(n.name, pr)], 0, 0), partial=None)
+            keep: list = []
+            p = dict(ptrs, partial=None)
             for f in ("x", "y", "residual"):
                 if p.get(f) is not None:
                     p[f] = View("t", 0, 0, 0)
-            args.x_sb, args.x_sc = n.c_in * t_in, t_in
-            args.y_sb = args.r_sb = n.c_out * t_out
-            args.y_sc = args.r_sc = t_out
-            self._bind_scratch(args, p, shapes, keep)
-            nws = int(N.lib.rave_conv1d_workspace(C.byref(args)))
-            if nws > 0:
-                ws = torch.empty(nws, device=self.device)
-                keep.append(ws)
-                args.partial = ws.data_ptr()
-            return self._time_native(N.lib.rave_conv1d, args)
+            base = N.ConvArgs(**scalars)
+            base.x_sb, base.x_sc = n.c_in * t_in, t_in
+            base.y_sb = base.r_sb = n.c_out * t_out
+            base.y_sc = base.r_sc = t_out
+            self._bind_scratch(base, p, shapes, keep)
+            cands = []
+            for pr in self.precs:
+                base.precision = pr
+                base.weight = self.arena.ptr(pack[(n.name, pr)])
+                cfgs = N.conv_configs(base) if (self.autotune or len(self.precs) > 1) else []
+                cands += [(pr, c) for c in [0] + cfgs]
+            nws = 0
+            for pr, c in cands:
+                base.precision, base.config = pr, c
+                base.weight = self.arena.ptr(pack[(n.name, pr)])
+                nws = max(nws, int(N.lib.rave_conv1d_workspace(C.byref(base))))
+            ws = torch.zeros(max(nws, 1), device=self.device)   # counters zero, slabs free
+            times = {}
+            for pr, c in cands:
+                args = N.ConvArgs.from_buffer_copy(base)
+                args.precision, args.config = pr, c
+                args.weight = self.arena.ptr(pack[(n.name, pr)])
+                args.partial = ws.data_ptr() if nws > 0 else None
+                try:
+                    times[(pr, c)] = self._time_native(N.lib.rave_conv1d, args)
+                except (NotImplementedError, ValueError):
+                    if c == 0:
+                        raise               # the default configuration must run
 
-        return self._pick(self._conv_key(n, stream_form, scalars), self.precs, run, timed)
+            best = min(times, key=times.get)
+            self._tuned[key] = (best[0] * self.CFG_BASE + best[1], times[best])
+        if key in self._tuned:
+            v = int(self._tuned[key][0])
+            return v // self.CFG_BASE, v % self.CFG_BASE
+        return self.precs[0], 0
+
+    CFG_BASE = 1 << 16          # tuned conv choice = precision * CFG_BASE + config
 
     def _conv_desc(self, n: ConvNode, B: int, t_in: int, src: View, dst: View,
                    res: Optional[View]) -> Tuple[dict, Dict[str, Optional[View]]]:
@@ -492,15 +533,17 @@ class RAVE:
               res: Optional[View]) -> int:
         t_out = n.out_len(t_in)
         s, ptrs = self._conv_desc(n, B, t_in, src, dst, res)
-        pr = self.conv_precision(n, s, ptrs)
-        s["precision"] = pr
+        pr, cfg = self.conv_launch(n, s, ptrs)
+        s["precision"], s["config"] = pr, cfg
         ptrs["weight"] = View("arena", self.w_pack[(n.name, pr)], 0, 0)
         ptrs["partial"] = plan.splitk_view(splitk_floats(s, res is not None))
         if n.transposed:
             flops = 2.0 * B * n.c_out * t_out * n.c_in * 2          # 2 taps per output sample
         else:
             flops = 2.0 * B * n.c_out * t_out * n.c_in * n.kernel
-        plan.add(N.OP_CONV, N.ConvArgs, s, ptrs, label=n.name, flops=flops)
+        nbytes = 4.0 * (B * n.c_in * t_in + B * n.c_out * t_out * (2 if res is not None else 1)
+                        + n.c_in * n.c_out * n.kernel)
+        plan.add(N.OP_CONV, N.ConvArgs, s, ptrs, label=n.name, flops=flops, nbytes=nbytes)
         return t_out
 
     def _run_stack(self, plan: Plan, nodes: List[ConvNode], B: int, inputs: Dict[str, Tuple[View, int]],
@@ -563,7 +606,7 @@ class RAVE:
                  dict(n_band=cfg.n_band, taps=self.taps_a, n_out_bands=n_out, batch=B, t_in=T,
                       pad_left=pad, t_out=F, x_sb=x.sb, y_sb=y.sb, y_sc=y.sc),
                  dict(x=x, y=y, hkf=View("arena", self.hkf_off, 0, 0)),
-                 flops=2.0 * B * n_out * F * self.taps_a)
+                 flops=2.0 * B * n_out * F * self.taps_a, nbytes=4.0 * (B * T + B * n_out * F))
         return F
 
     def _synthesis(self, plan: Plan, B: int, F: int, x: View, y: View, mode: int,
@@ -575,7 +618,8 @@ class RAVE:
                       frame0=frame0, x_sb=x.sb, x_sc=x.sc,
                       n_sb=noise.sb if noise else 0, n_sc=noise.sc if noise else 0, y_sb=y.sb),
                  dict(x=x, y=y, noise=noise, hki=View("arena", self.hki_off, 0, 0)),
-                 flops=2.0 * B * F * cfg.n_band * cfg.n_band * self.taps_s)
+                 flops=2.0 * B * F * cfg.n_band * cfg.n_band * self.taps_s,
+                 nbytes=4.0 * (2 * B * F * cfg.n_band + (B * F * cfg.n_band if noise else 0)))
 
     def _fill_speaker(self, plan: Plan, B: int, Fz: int, z: View) -> None:
         cfg = self.cfg

@@ -104,8 +104,8 @@ class StreamingRAVE:
         ptrs = dict(x=x, y=y, residual=res,
                     bias=View("arena", bo, 0, 0) if bo is not None else None,
                     alpha=View("arena", ao, 0, 0) if ao is not None else None)
-        pr = m.conv_precision(n, s, ptrs, stream_form=n.transposed)
-        s["precision"] = pr
+        pr, cfg = m.conv_launch(n, s, ptrs, stream_form=n.transposed)
+        s["precision"], s["config"] = pr, cfg
         # ConvTranspose: packed for the cached form (out_shift 0)
         pack = m.w_pack_stream if n.transposed else m.w_pack
         ptrs["weight"] = View("arena", pack[(n.name, pr)], 0, 0)

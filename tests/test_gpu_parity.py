@@ -72,7 +72,7 @@ CONV_CASES = [
 
 
 def run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act, split=True,
-             precision=0):
+             precision=0, config=0):
     B, _, T = x.shape
     packed = torch.from_numpy(N.pack_conv_weight(w, c_in, c_out, k, s, d, transposed,
                                                  precision=precision)).to(dev)
@@ -92,23 +92,31 @@ def run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed,
                    x=xd.data_ptr(), x_sb=c_in * T, x_sc=T, y=y.data_ptr(), y_sb=c_out * t_out, y_sc=t_out,
                    residual=rd.data_ptr() if rd is not None else None, r_sb=c_out * t_out, r_sc=t_out,
                    weight=packed.data_ptr(), bias=bd.data_ptr() if bd is not None else None,
-                   alpha=ad.data_ptr() if ad is not None else None)
+                   alpha=ad.data_ptr() if ad is not None else None, config=config)
     ws = None
     if split:
         nws = N.lib.rave_conv1d_workspace(C.byref(a))
         assert nws >= 0
         if nws > 0:
-            ws = torch.full((nws,), float("nan"), device=dev)
+            ws = torch.full((nws,), float("nan"), device=dev)   # slabs need no initialisation,
+            ws[:N.SPLITK_TICKETS] = 0                              # the arrival counters start zero
             a.partial = ws.data_ptr()
-    N.check(N.lib.rave_conv1d(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream)), "conv1d")
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    N.check(N.lib.rave_conv1d(C.byref(a), st), "conv1d")
     torch.cuda.synchronize()
-    return y.cpu().numpy()
+    out = y.cpu().numpy()
+    if ws is not None:
+        # the call left the counters zero, and a second call gives bitwise the same output
+        assert int((ws[:N.SPLITK_TICKETS].view(torch.int32) != 0).sum()) == 0
+        y.fill_(float("nan"))
+        N.check(N.lib.rave_conv1d(C.byref(a), st), "conv1d")
+        torch.cuda.synchronize()
+        assert np.array_equal(y.cpu().numpy(), out)
+    return out
 
 
-@pytest.mark.parametrize("precision", ["f32", "split16"])
-@pytest.mark.parametrize("split", [True, False])
-@pytest.mark.parametrize("case", CONV_CASES, ids=[str(c[:8]) for c in CONV_CASES])
-def test_conv_layer(N, dev, case, split, precision):
+def conv_case(case):
+    """Seeded inputs of a CONV_CASES row and the oracle's output (float64)."""
     from oracle.rave_oracle import conv1d, conv_transpose1d, leaky_relu, snake
     c_in, c_out, k, s, d, transposed, act, has_res, B, T = case
     rng = np.random.default_rng(hash(case) & 0xFFFF)
@@ -135,10 +143,44 @@ def test_conv_layer(N, dev, case, split, precision):
     res = rng.standard_normal(ref.shape).astype(np.float32) if has_res else None
     if has_res:
         ref = ref + res
-    got = run_conv(N, dev, x, w, b, alpha.reshape(-1) if alpha is not None else None, res,
+    return x, w, b, alpha.reshape(-1) if alpha is not None else None, res, pad, ref
+
+
+@pytest.mark.parametrize("precision", ["f32", "split16"])
+@pytest.mark.parametrize("split", [True, False])
+@pytest.mark.parametrize("case", CONV_CASES, ids=[str(c[:8]) for c in CONV_CASES])
+def test_conv_layer(N, dev, case, split, precision):
+    c_in, c_out, k, s, d, transposed, act, has_res, B, T = case
+    x, w, b, alpha, res, pad, ref = conv_case(case)
+    got = run_conv(N, dev, x, w, b, alpha, res,
                    c_in, c_out, k, s, d, pad, transposed, act, split, N.PRECISION[precision])
     assert np.isfinite(got).all()
     assert maxabs(got, ref) <= 2e-5 * max(1.0, np.abs(ref).max())
+
+
+CONFIG_CASES = [CONV_CASES[i] for i in (1, 2, 4, 5, 8, 9, 11, 12, 14)]
+
+
+@pytest.mark.parametrize("precision", ["f32", "split16"])
+@pytest.mark.parametrize("case", CONFIG_CASES, ids=[str(c[:8]) for c in CONFIG_CASES])
+def test_conv_every_config(N, dev, case, precision):
+    """Every launch configuration rave_conv1d_configs() offers the autotuner
+    (tile shape x K-splits x split-K combine) meets the layer tolerance."""
+    c_in, c_out, k, s, d, transposed, act, has_res, B, T = case
+    x, w, b, alpha, res, pad, ref = conv_case(case)
+    t_out = ref.shape[-1]
+    a = N.ConvArgs(c_in=c_in, c_out=c_out, kernel=k, stride=s, dilation=d,
+                   pad_left=0 if transposed else pad[0], pad_right=0 if transposed else pad[1],
+                   transposed=transposed, out_shift=s // 2 if transposed else 0, act=N.ACT[act],
+                   batch=B, t_in=T, t_out=t_out, precision=N.PRECISION[precision], x=16, y=16, weight=16,
+                   alpha=16 if alpha is not None else None, residual=16 if res is not None else None)
+    cfgs = N.conv_configs(a)
+    assert cfgs, "no configurations listed"
+    for cfg in cfgs:
+        got = run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act, True,
+                       N.PRECISION[precision], config=cfg)
+        err = maxabs(got, ref)
+        assert np.isfinite(got).all() and err <= 2e-5 * max(1.0, np.abs(ref).max()), (cfg, err)
 
 
 # ------------------------------------------------------------------ PQMF
@@ -561,3 +603,26 @@ def test_fused_units_match_unfused_model(dev, precision, n_fused):
     torch.cuda.synchronize()
     assert float((zf - zu).abs().max()) < 1e-4
     assert float((yf - yu).abs().max()) < 1e-4
+
+
+def test_auto_tuning_roundtrip(dev):
+    """RAVE.tuning() replayed into a new model builds the same plans (same
+    per-op choices, no timing runs) and gives bitwise the same output."""
+    import json
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.v2()
+    params, spk = init_params(cfg, 0), init_speaker(cfg, 0)
+    m1 = RAVE(cfg, params, spk, device=dev, precision="auto")
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = (0.1 * torch.randn(2, 1, 32768, generator=g)).to(dev)
+    y1 = m1.forward(x)
+    tun = json.loads(json.dumps(m1.tuning()))
+    assert any(k[0] == "fuse" for k, _, _ in tun) and any(k[0] == "conv" for k, _, _ in tun)
+    m2 = RAVE(cfg, params, spk, device=dev, precision="auto", tuning=tun)
+    m2._time_native = None          # a timing run would now raise
+    y2 = m2.forward(x)
+    torch.cuda.synchronize()
+    assert m2.tuning() == m1.tuning()
+    assert torch.equal(y1, y2)

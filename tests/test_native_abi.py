@@ -121,6 +121,23 @@ def test_validation_errors():
     assert N.lib.rave_conv1d_workspace(C.byref(a)) >= 0
 
 
+@pytest.mark.parametrize("precision", [0, 1])
+def test_conv_configs_listing(precision):
+    """rave_conv1d_configs lists configurations the launcher accepts (host-side
+    validation only: the workspace query resolves each), and rejects others."""
+    a = N.ConvArgs(c_in=128, c_out=128, kernel=3, stride=1, dilation=3, pad_left=3, pad_right=3,
+                   batch=16, t_in=1024, t_out=1024, precision=precision, x=16, y=16, weight=16)
+    cfgs = N.conv_configs(a)
+    assert len(cfgs) >= 4 and 0 not in cfgs and len(set(cfgs)) == len(cfgs)
+    for c in cfgs:
+        a.config = c
+        assert N.lib.rave_conv1d_workspace(C.byref(a)) >= 0
+    a.config = 1 + 7          # tile index 7: no such tile
+    assert N.lib.rave_conv1d_workspace(C.byref(a)) == -1
+    a.config = -3
+    assert N.lib.rave_conv1d_workspace(C.byref(a)) == -1
+
+
 def test_plan_create_and_relocation_bounds():
     ops = (N.PlanOp * 1)()
     ops[0].kind = N.OP_FILL

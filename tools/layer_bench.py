@@ -94,7 +94,14 @@ def run_unit(name, B, iters, dev):
     return ms
 
 
-def run(name, B, iters, dev):
+def cfg_str(c):
+    if c == 0:
+        return "heuristic"
+    v = c - 1
+    return f"tile{v & 7} S{((v >> 3) & 31) + 1}{' sep' if (v >> 8) & 1 else ''}"
+
+
+def run(name, B, iters, dev, config=0):
     if name in UNITS:
         return run_unit(name, B, iters, dev)
     ci, co, k, s, d, tr, act, has_res, T = LAYERS[name]
@@ -116,13 +123,22 @@ def run(name, B, iters, dev):
                    batch=B, t_in=T, t_out=t_out, precision=PREC, x=x.data_ptr(), x_sb=ci * T, x_sc=T,
                    y=y.data_ptr(), y_sb=co * t_out, y_sc=t_out,
                    residual=res.data_ptr() if res is not None else None, r_sb=co * t_out, r_sc=t_out,
-                   weight=packed.data_ptr(), bias=bias.data_ptr())
+                   weight=packed.data_ptr(), bias=bias.data_ptr(),
+                   config=config if isinstance(config, int) else 0)
+    if config == "all":
+        a.config = 0
+        res_ = {c: None for c in [0] + N.conv_configs(a)}
+        for c in res_:
+            res_[c] = run(name, B, iters, dev, c)
+        best = min(res_, key=res_.get)
+        print(f"  -> best {cfg_str(best)} {res_[best] * 1e3:.2f} us", flush=True)
+        return res_[best]
     stamps = None
     if STAMPS:
         stamps = torch.zeros(8 * 200000, dtype=torch.int64, device=dev)
         a.stamps = stamps.data_ptr()
     nws = N.lib.rave_conv1d_workspace(C.byref(a))
-    ws = torch.empty(max(nws, 1), device=dev)
+    ws = torch.zeros(max(nws, 1), device=dev)
     if nws > 0:
         a.partial = ws.data_ptr()
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -137,7 +153,8 @@ def run(name, B, iters, dev):
     ms = e0.elapsed_time(e1) / iters
     taps = 2 if tr else k
     fl = 2.0 * B * co * t_out * ci * taps
-    print(f"{name:12s} B={B} ws={nws:>9d}  {ms * 1e3:8.2f} us  {fl / ms / 1e9:7.2f} TFLOP/s", flush=True)
+    print(f"{name:12s} B={B} {cfg_str(config):16s} ws={nws:>9d}  {ms * 1e3:8.2f} us  "
+          f"{fl / ms / 1e9:7.2f} TFLOP/s", flush=True)
     if stamps is not None:
         stamps.zero_()
         N.check(N.lib.rave_conv1d(C.byref(a), st))
@@ -152,12 +169,13 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--precision", default="split16", choices=["f32", "split16"])
+    ap.add_argument("--config", default="0", help="launch config value, or 'all' (every listed one)")
     a = ap.parse_args()
     global PREC
     PREC = N.PRECISION[a.precision]
     dev = torch.device("cuda")
     for name in a.layers.split(","):
-        run(name, a.batch, a.iters, dev)
+        run(name, a.batch, a.iters, dev, a.config if a.config == "all" else int(a.config))
 
 
 if __name__ == "__main__":

@@ -1,29 +1,44 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 CSV output of ``bench.py`` for the conv roofline.
+"""Summarise rocprofv3 CSV output of ``bench.py`` for the roofline line.
 
     python tools/rocprof_summary.py --trace KT.csv [--fetch FETCH.csv] [--write WRITE.csv] \
-        [--bench BENCH.json] [--out SUMMARY.json]
+        [--bench BENCH.json] [--out SUMMARY.json] [--traffic-out TRAFFIC.json]
 
-* ``--trace``: a ``*_kernel_trace.csv`` (rocprofv3 --kernel-trace).  One conv
-  op of a plan is the main ``conv1d_mfma_kernel`` launch plus, when split-K is
-  used, its ``conv1d_splitk_reduce_kernel``; the per-op duration is
-  (sum of both kernels) / (number of main launches) -- the same quantity
-  bench.py's HIP events time per conv op.
+* ``--trace``: a ``*_kernel_trace.csv`` (rocprofv3 --kernel-trace).  Kernels
+  are grouped into the GEMM families bench.py reports (``FAMILIES``): one op
+  of a family is its main kernel launch plus, for the convs, the split-K
+  reduce launched after it when the op splits K; the per-op duration is
+  (sum over the family's kernels) / (number of main launches) -- the same
+  quantity bench.py's HIP events time per op.
 * ``--fetch`` / ``--write``: ``*_counter_collection.csv`` of two separate
   ``--pmc FETCH_SIZE`` / ``--pmc WRITE_SIZE`` passes (the counters do not fit
   one pass on gfx950).  FETCH_SIZE is doubled (gfx950 tallies 128-B
   requests at 64 B, MI355X_MICROARCH.md "HBM"); both are in KB.  Traffic per
-  conv op = (2*FETCH + WRITE) over the conv kernels / main launches.
+  op launch = (2*FETCH + WRITE) over the family's kernels / main launches.
 """
 from __future__ import annotations
 
 import argparse
 import csv
 import json
+import re
 from collections import defaultdict
 
-MAIN = "conv1d_mfma_kernel"
-REDUCE = "conv1d_splitk_reduce_kernel"
+# family -> (main kernel, helper kernels launched by the same op)
+FAMILIES = {
+    "conv_f32": ("conv1d_mfma_kernel", ("conv1d_splitk_reduce_kernel",)),
+    "conv_split16": ("conv1d_split_kernel", ("split_reduce_kernel",)),
+    "unit_f32": ("residual_unit_kernel", ()),
+    "unit_split16": ("unit_split_kernel", ()),
+    "pqmf_analysis": ("pqmf_analysis_kernel", ()),
+    "pqmf_synthesis": ("pqmf_synthesis_kernel", ()),
+}
+_KERNEL_FAMILY = {}
+for _fam, (_main, _helpers) in FAMILIES.items():
+    _KERNEL_FAMILY[_main] = (_fam, True)
+    for _h in _helpers:
+        _KERNEL_FAMILY[_h] = (_fam, False)
+_NAME = re.compile(r"(?:^|[\s:])([A-Za-z_][A-Za-z0-9_]*)\s*[<(]")
 
 
 def _rows(path):
@@ -31,48 +46,54 @@ def _rows(path):
         return list(csv.DictReader(fh))
 
 
-def kernel_family(name: str) -> str:
-    for fam in (MAIN, REDUCE, "pqmf_analysis_kernel", "pqmf_synthesis_kernel", "fill_channels_kernel",
-                "rvq_encode_kernel", "rvq_decode_kernel", "noise_synth_kernel", "adain_kernel",
-                "copy_kernel", "shift_history_kernel"):
-        if fam in name:
-            return fam
-    return name.split("(")[0][:60]
+def kernel_name(demangled: str) -> str:
+    """Bare function name of a demangled kernel symbol
+    ('void rave::conv1d_split_kernel<3, 64>(rave::ConvKArgs)' -> 'conv1d_split_kernel')."""
+    m = _NAME.search(demangled)
+    return m.group(1) if m else demangled.split("(")[0][:60]
+
+
+def classify(demangled: str):
+    """(family or bare kernel name, is the family's main launch)."""
+    k = kernel_name(demangled)
+    return _KERNEL_FAMILY.get(k, (k, False))
 
 
 def trace_summary(path):
-    fam_ns = defaultdict(float)
-    fam_n = defaultdict(int)
+    k_ns, k_n = defaultdict(float), defaultdict(int)
+    fam_ns, fam_main = defaultdict(float), defaultdict(int)
     for r in _rows(path):
         ns = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
-        f = kernel_family(r["Kernel_Name"])
-        fam_ns[f] += ns
-        fam_n[f] += 1
-    n_main = fam_n.get(MAIN, 0)
-    conv_ns = fam_ns.get(MAIN, 0.0) + fam_ns.get(REDUCE, 0.0)
+        k = kernel_name(r["Kernel_Name"])
+        k_ns[k] += ns
+        k_n[k] += 1
+        fam, main = classify(r["Kernel_Name"])
+        if fam in FAMILIES:
+            fam_ns[fam] += ns
+            fam_main[fam] += int(main)
     return {
-        "families": {f: {"calls": fam_n[f], "total_ms": round(fam_ns[f] / 1e6, 4),
-                         "avg_us": round(fam_ns[f] / fam_n[f] / 1e3, 3)}
-                     for f in sorted(fam_ns, key=lambda k: -fam_ns[k])},
-        "conv_ops": n_main,
-        "conv_avg_op_ms": conv_ns / n_main / 1e6 if n_main else None,
-        "conv_main_avg_ms": fam_ns.get(MAIN, 0.0) / n_main / 1e6 if n_main else None,
+        "kernels": {k: {"calls": k_n[k], "total_ms": round(k_ns[k] / 1e6, 4),
+                        "avg_us": round(k_ns[k] / k_n[k] / 1e3, 3)}
+                    for k in sorted(k_ns, key=lambda q: -k_ns[q])},
+        "families": {f: {"ops": fam_main[f], "total_ms": round(fam_ns[f] / 1e6, 4),
+                         "avg_op_ms": fam_ns[f] / fam_main[f] / 1e6 if fam_main[f] else None}
+                     for f in sorted(fam_ns, key=lambda q: -fam_ns[q])},
     }
 
 
-def counter_total(path, counter):
-    """Sum of a counter over conv kernels (main + reduce) and the main-launch count."""
-    tot = 0.0
-    seen = set()
+def counter_by_family(path, counter):
+    """Per family: sum of ``counter`` over its kernels and its main-launch count."""
+    tot = defaultdict(float)
+    seen = defaultdict(set)
     for r in _rows(path):
         if r.get("Counter_Name") != counter:
             continue
-        f = kernel_family(r["Kernel_Name"])
-        if f in (MAIN, REDUCE):
-            tot += float(r["Counter_Value"])
-            if f == MAIN:
-                seen.add(r["Dispatch_Id"])
-    return tot, len(seen)
+        fam, main = classify(r["Kernel_Name"])
+        if fam in FAMILIES:
+            tot[fam] += float(r["Counter_Value"])
+            if main:
+                seen[fam].add(r["Dispatch_Id"])
+    return {f: (tot[f], len(seen[f])) for f in tot}
 
 
 def main():
@@ -80,34 +101,42 @@ def main():
     ap.add_argument("--trace", required=True)
     ap.add_argument("--fetch")
     ap.add_argument("--write")
-    ap.add_argument("--bench", help="bench.py JSON line to compare the event average with")
+    ap.add_argument("--bench", help="bench.py JSON line to compare the event averages with")
     ap.add_argument("--out")
-    ap.add_argument("--traffic-out", help="write bench.py's profiles/conv_traffic.json")
+    ap.add_argument("--traffic-out", help="write bench.py's profiles/traffic.json")
     ap.add_argument("--workload", default="v2,16,65536", help="config,batch,samples of the passes")
+    ap.add_argument("--precision", default="auto", help="bench.py --precision of the passes")
     a = ap.parse_args()
     s = trace_summary(a.trace)
     if a.fetch and a.write:
-        fkb, nf = counter_total(a.fetch, "FETCH_SIZE")
-        wkb, nw = counter_total(a.write, "WRITE_SIZE")
-        s["traffic"] = {
-            "fetch_bytes_per_op": 2.0 * fkb * 1024 / nf,
-            "write_bytes_per_op": wkb * 1024 / nw,
-            "bytes_per_op": 2.0 * fkb * 1024 / nf + wkb * 1024 / nw,
-            "ops_fetch_pass": nf, "ops_write_pass": nw,
-            "note": "FETCH_SIZE x2 (gfx950 correction); KB -> bytes; conv main + split-K reduce",
-        }
+        fe = counter_by_family(a.fetch, "FETCH_SIZE")
+        wr = counter_by_family(a.write, "WRITE_SIZE")
+        tr = {}
+        for f in sorted(set(fe) & set(wr)):
+            (fkb, nf), (wkb, nw) = fe[f], wr[f]
+            if nf and nw:
+                fb, wb = 2.0 * fkb * 1024 / nf, wkb * 1024 / nw
+                tr[f] = {"bytes_per_launch": round(fb + wb), "fetch_bytes_per_launch": round(fb),
+                         "write_bytes_per_launch": round(wb), "launches_fetch_pass": nf,
+                         "launches_write_pass": nw}
+        s["traffic"] = {"families": tr,
+                        "note": "FETCH_SIZE x2 (gfx950 correction); KB -> bytes; main kernel + "
+                                "its split-K reduce, per main launch"}
     if a.bench:
         with open(a.bench) as fh:
             b = json.loads(fh.read().strip().splitlines()[-1])
-        ev = b["roofline"]["avg_launch_ms"]
-        s["bench_event_avg_op_ms"] = ev
-        s["rocprof_vs_event"] = s["conv_avg_op_ms"] / ev if ev else None
+        cmp = {}
+        for f, v in (b.get("roofline") or {}).get("families", {}).items():
+            rp = s["families"].get(f, {}).get("avg_op_ms")
+            ev = v.get("avg_launch_ms")
+            cmp[f] = {"event_avg_op_ms": ev, "rocprof_avg_op_ms": rp,
+                      "rocprof_over_event": rp / ev if rp and ev else None}
+        s["rocprof_vs_event"] = cmp
     if a.traffic_out and "traffic" in s:
-        cfg, b, t = a.workload.split(",")
+        cfg, bb, t = a.workload.split(",")
         with open(a.traffic_out, "w") as fh:
-            json.dump({"workload": [cfg, int(b), int(t)], "bytes_per_op": round(s["traffic"]["bytes_per_op"]),
-                       "fetch_bytes_per_op": round(s["traffic"]["fetch_bytes_per_op"]),
-                       "write_bytes_per_op": round(s["traffic"]["write_bytes_per_op"]),
+            json.dump({"workload": [cfg, int(bb), int(t)], "precision": a.precision,
+                       "families": s["traffic"]["families"],
                        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of bench.py "
                                  "(tools/profile_round.sh); FETCH_SIZE x2 gfx950 correction"}, fh, indent=1)
     txt = json.dumps(s, indent=1)
