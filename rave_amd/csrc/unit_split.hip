@@ -360,7 +360,7 @@ static int us_launch(USArgs k, int B, bool snake, hipStream_t st) {
     return launch_status("unit_split_kernel");
 }
 
-static bool us_supported(int C) { return C == 64 || C == 128; }
+static bool us_supported(int C) { return C == 64 || C == 128 || C == 256; }
 
 // Power-of-two row exponent: max |w * 2^e| in [8, 16) (e = 0 for an all-zero row).
 static int us_row_exponent(double amax) {
@@ -386,7 +386,7 @@ extern "C" int64_t rave_unit_split_packed_size(int C) {
 extern "C" int rave_unit_split_pack_weight(const float* w1, const float* w2, int C, float* packed) {
     RAVE_CHECK_ARG(w1 && w2 && packed, "unit_split_pack_weight: null pointer");
     if (!us_supported(C)) {
-        set_error("unit_split_pack_weight: split16 fused residual unit supports C in {64, 128}");
+        set_error("unit_split_pack_weight: split16 fused residual unit supports C in {64, 128, 256}");
         return RAVE_ERR_UNSUPPORTED;
     }
     const int S1 = 3 * C / 16, ST = 4 * C / 16, CG = C / 16;
@@ -439,7 +439,7 @@ namespace rave {
 int residual_unit_split(const rave_unit_args& a, void* stream) {
     const int C = a.channels;
     if (!us_supported(C)) {
-        set_error("residual_unit(split16): fused unit supports C in {64, 128}");
+        set_error("residual_unit(split16): fused unit supports C in {64, 128, 256}");
         return RAVE_ERR_UNSUPPORTED;
     }
     USArgs k{};
@@ -463,8 +463,13 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
         k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
         return us_launch<64, 2>(k, a.batch, snake, st);
     }
-    k.XW = USGeo<128, 1>::BN + 2 * a.dilation;
+    if (C == 128) {
+        k.XW = USGeo<128, 1>::BN + 2 * a.dilation;
+        k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
+        return us_launch<128, 1>(k, a.batch, snake, st);
+    }
+    k.XW = USGeo<256, 1>::BN + 2 * a.dilation;
     k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
-    return us_launch<128, 1>(k, a.batch, snake, st);
+    return us_launch<256, 1>(k, a.batch, snake, st);
 }
 }  // namespace rave
