@@ -113,7 +113,7 @@ struct LaunchCfg {
     int bm, bn, S;
 };
 
-// rave_conv1d_args.config: 0 = heuristic, else 1 + tile + 8 (S - 1) + 256 sep
+// rave_conv1d_args.config: 0 = heuristic, else 1 + tile + 16 (S - 1) + 512 sep
 // (tile: index into the precision's tile table; S: K-splits; sep: split-K
 // combine in a separate reduce launch instead of in-launch)
 struct ConfigCode {
@@ -122,12 +122,12 @@ struct ConfigCode {
 static inline bool decode_config(int cfg, ConfigCode& c) {
     if (cfg <= 0) return false;
     const int v = cfg - 1;
-    c.tile = v & 7;
-    c.S = ((v >> 3) & 31) + 1;
-    c.sep = (v >> 8) & 1;
-    return (v >> 9) == 0;
+    c.tile = v & 15;
+    c.S = ((v >> 4) & 31) + 1;
+    c.sep = (v >> 9) & 1;
+    return (v >> 10) == 0;
 }
-static inline int encode_config(int tile, int S, int sep) { return 1 + tile + 8 * (S - 1) + 256 * sep; }
+static inline int encode_config(int tile, int S, int sep) { return 1 + tile + 16 * (S - 1) + 512 * sep; }
 // K-split counts the autotuner tries (an S whose chunks per split equal a smaller S's is skipped)
 constexpr int kSplitCands[] = {1, 2, 3, 4, 6, 8, 12, 16};
 static inline bool split_count_distinct(int S, int nchunks) {

@@ -132,17 +132,20 @@ __device__ __forceinline__ u32x4_t raw_rsrc(const void* p, int bytes) {
 
 // Workgroup tile: BN time columns x BM GEMM rows.  A wave owns WM rows x WN
 // columns (WM = 32: 128 columns; WM = 64: 64 columns), four 32x32 blocks.
-template <int KT, int BM, int BN, int WM, bool XV = true> struct SGeo {
+// KG = 2: two waves per output tile ("K-groups"), each taking part of every
+// chunk's K-steps (group 0 the first ceil(KSC/2)); summed through LDS at the end.
+template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1> struct SGeo {
     using F = SFam<KT>;
     static constexpr int Q = F::Q, S = F::S, VC = F::VC;
     static constexpr int KSC = Q * VC / 16, CPC = VC / S;
     static constexpr int WN = 4096 / WM, NJ = WM / 32, NI = WN / 32;
-    static constexpr int WGM = BM / WM, WGN = BN / WN, NW = WGM * WGN, NT = 64 * NW;
+    static constexpr int WGM = BM / WM, WGN = BN / WN, NWT = WGM * WGN, NW = NWT * KG, NT = 64 * NW;
+    static constexpr int KS0 = (KSC + KG - 1) / KG, KS1 = KSC - KS0;   // K-steps of group 0 / 1
     // window rows: columns + tap reach (+1: ConvT phase group 1 reads one row later)
     static constexpr int XW_MAX = BN + (Q - 1) * F::DMAX + (KT == 2 ? 1 : 0);
     static constexpr int PH = VC + 8;                        // halves per plane row (conflict-free b128)
     static constexpr int XPLANE = XW_MAX * PH * 2;           // bytes per f16 plane
-    static constexpr int WR = KSC * NJ * 2;                  // weight fragment loads per wave per chunk
+    static constexpr int WR = KS0 * NJ * 2;                  // weight fragment loads per wave per chunk (max)
     // raw window rows: XV = 16-byte pieces from a 4-sample-aligned start (row
     // stride rounded up to 4 samples), else 4-byte pieces
     static constexpr int RS_MAX = XV ? ((XW_MAX * S + 3 + 3) / 4) * 4 : XW_MAX * S;
@@ -162,14 +165,19 @@ template <int KT, int BM, int BN, int WM, bool XV = true> struct SGeo {
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;   // convert tasks per thread
     static_assert(XPLANE % 16 == 0 && STAGE % 16 == 0, "16-byte LDS alignment");
     static_assert(NI * NJ == 4 && NW >= 1 && NW <= 8, "tile");
+    static_assert(KG == 1 || (KG == 2 && KS1 >= 1), "K-groups");
     static_assert(WR + XI <= 63, "vmcnt range");
 };
 
-template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV>
-__global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_split_kernel(ConvKArgs a) {
-    using G = SGeo<KT, BM, BN, WM, XV>;
+template <int V> struct IC {
+    static constexpr int value = V;
+};
+
+template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM)) * KG) void conv1d_split_kernel(ConvKArgs a) {
+    using G = SGeo<KT, BM, BN, WM, XV, KG>;
     constexpr int S = G::S, VC = G::VC, KSC = G::KSC, CPC = G::CPC, PH = G::PH;
-    constexpr int NT = G::NT, NW = G::NW, WGM = G::WGM, G8 = G::G8, XT = G::XT;
+    constexpr int NT = G::NT, NW = G::NW, NWT = G::NWT, WGM = G::WGM, G8 = G::G8, XT = G::XT;
     constexpr int NI = G::NI, NJ = G::NJ, WN = G::WN;
     constexpr int HPS = VC / 16;                 // K-steps per tap
     constexpr unsigned kOOB = 0xFFFFFFF0u;
@@ -191,7 +199,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
     stamp(0);
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave % WGM, wn = wave / WGM;
+    const int kg = wave / NWT;                   // K-group
+    const int twave = wave - kg * NWT;           // wave within the output tile
+    const int wm = twave % WGM, wn = twave / WGM;
     const int h = lane >> 5, l32 = lane & 31;
 
     // 1-D grid, logical id remapped so that consecutive ids -- a tile's K-splits,
@@ -277,14 +287,15 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
     };
     // this wave's weight fragments: register ring, one chunk ahead (chunks past
     // the packed image read zeros)
-    u32x4_t wr[KSC][NJ][2];
-    auto load_w = [&](int c, int st) __attribute__((always_inline)) {
+    // (slot = this group's local K-step; st = the chunk's K-step)
+    u32x4_t wr[G::KS0][NJ][2];
+    auto load_w = [&](int c, int slot, int st) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int pl = 0; pl < 2; ++pl)
-                wr[st][j][pl] = bload16(wrs, wbase + (unsigned)c * wcstride +
-                                                 (unsigned)(((j * KSC + st) * 2 + pl) * 1024));
+                wr[slot][j][pl] = bload16(wrs, wbase + (unsigned)c * wcstride +
+                                                   (unsigned)(((j * KSC + st) * 2 + pl) * 1024));
     };
     // raw window of a stage -> activation -> (hi, lo) f16 planes
     auto convert_task = [&](int c, int stage, int pb, int i) __attribute__((always_inline)) {
@@ -341,81 +352,117 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
         }
     };
 
-    // ------------------------------------------------------------ prologue
+    // ------------------------------------------------------------ prologue + K loop
     // vmcnt bookkeeping (every load below is hand-counted asm): per chunk a
-    // wave issues XI window DMAs, then per K-step 2*NJ weight loads.
-    constexpr int WR = G::WR, XI = G::XI;
-    issue(c_begin, 0);
-    issue(c_begin + 1, 1);
+    // wave issues XI window DMAs, then per own K-step 2*NJ weight loads.  The
+    // body is instantiated per K-group (its K-step range fixes the counts);
+    // both groups pass the same barriers.
+    auto body = [&](auto gtag) __attribute__((always_inline)) {
+        constexpr int GG = decltype(gtag)::value;
+        constexpr int KS = GG == 0 ? G::KS0 : G::KS1;   // own K-steps per chunk
+        constexpr int ST0 = GG == 0 ? 0 : G::KS0;       // first own K-step
+        constexpr int WR = KS * NJ * 2, XI = G::XI;
+        issue(c_begin, 0);
+        issue(c_begin + 1, 1);
 #pragma unroll
-    for (int st = 0; st < KSC; ++st) load_w(c_begin, st);
-    wait_vm<XI + WR>();                     // window c_begin landed
-    __syncthreads();
-    convert(c_begin, 0, 0);
-    wait_vm<WR>();                          // window c_begin+1 landed
-    __syncthreads();
-    stamp(1);
-
-    // per chunk c: DMA window c+2 | K-steps (weights of c from the ring, refill
-    // with c+1) | split window c+1 into the other plane pair | wait + barrier
-    int stage = 0;
-    for (int c = c_begin; c < c_end; ++c) {
-        const int pb = (c - c_begin) & 1;
-        const int s1 = stage == 2 ? 0 : stage + 1;
-        const int s2 = s1 == 2 ? 0 : s1 + 1;
-        issue(c + 2, s2);
-        AFrag f[2];
-        read_a(pb, 0, f[0]);
-#pragma unroll
-        for (int st = 0; st < KSC; ++st) {
-            if (st + 1 < KSC) read_a(pb, st + 1, f[(st + 1) & 1]);   // next reads in flight
-            // weights of (c, st): issued one chunk ago; younger: the rest of that
-            // chunk's weights, this chunk's window DMA and this chunk's earlier refills
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) wait_vm_regs<2 * (WR / 2 - NJ) + XI>(wr[st][j][0], wr[st][j][1]);
-            __builtin_amdgcn_sched_barrier(0);
-            const AFrag& g = f[st & 1];
-            s_h8 bh[NJ], bl[NJ], b2[NJ];
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                bh[j] = __builtin_bit_cast(s_h8, wr[st][j][0]);
-                bl[j] = __builtin_bit_cast(s_h8, wr[st][j][1]);
-                b2[j] = bh[j] * (_Float16)2048.0f;
-            }
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.h[i], b2[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.l[i], bh[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.h[i], bl[j], acc[i][j], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            load_w(c + 1, st);              // refill the slot one chunk ahead
-            // split part of window c+1 into the other plane pair (VALU beside the MFMAs)
-            if (c + 1 < c_end) {
-#pragma unroll
-                for (int i = st; i < XT; i += KSC) convert_task(c + 1, s1, pb ^ 1, i);
-            }
-        }
-        wait_vm<WR>();                      // window c+2 landed (weights of c+1 may fly)
+        for (int k = 0; k < KS; ++k) load_w(c_begin, k, ST0 + k);
+        wait_vm<XI + WR>();                     // window c_begin landed
         __syncthreads();
-        stage = s1;
-        if (c == c_begin) stamp(2);
-    }
+        convert(c_begin, 0, 0);
+        wait_vm<WR>();                          // window c_begin+1 landed
+        __syncthreads();
+        stamp(1);
+
+        // per chunk c: DMA window c+2 | own K-steps (weights of c from the ring,
+        // refill with c+1) | split window c+1 into the other plane pair | wait + barrier
+        int stage = 0;
+        for (int c = c_begin; c < c_end; ++c) {
+            const int pb = (c - c_begin) & 1;
+            const int s1 = stage == 2 ? 0 : stage + 1;
+            const int s2 = s1 == 2 ? 0 : s1 + 1;
+            issue(c + 2, s2);
+            AFrag f[2];
+            read_a(pb, ST0, f[0]);
+#pragma unroll
+            for (int k = 0; k < KS; ++k) {
+                if (k + 1 < KS) read_a(pb, ST0 + k + 1, f[(k + 1) & 1]);   // next reads in flight
+                // weights of (c, k): issued one chunk ago; younger: the rest of that
+                // chunk's weights, this chunk's window DMA and this chunk's earlier refills
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) wait_vm_regs<2 * (WR / 2 - NJ) + XI>(wr[k][j][0], wr[k][j][1]);
+                __builtin_amdgcn_sched_barrier(0);
+                const AFrag& g = f[k & 1];
+                s_h8 bh[NJ], bl[NJ], b2[NJ];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    bh[j] = __builtin_bit_cast(s_h8, wr[k][j][0]);
+                    bl[j] = __builtin_bit_cast(s_h8, wr[k][j][1]);
+                    b2[j] = bh[j] * (_Float16)2048.0f;
+                }
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.h[i], b2[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.l[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.h[i], bl[j], acc[i][j], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                load_w(c + 1, k, ST0 + k);      // refill the slot one chunk ahead
+                // split part of window c+1 into the other plane pair (VALU beside the MFMAs)
+                if (c + 1 < c_end) {
+#pragma unroll
+                    for (int i = k; i < XT; i += KS) convert_task(c + 1, s1, pb ^ 1, i);
+                }
+            }
+            wait_vm<WR>();                      // window c+2 landed (weights of c+1 may fly)
+            __syncthreads();
+            stage = s1;
+            if (c == c_begin) stamp(2);
+        }
+    };
+    if (KG == 1 || kg == 0) body(IC<0>{});
+    else body(IC<1>{});
     stamp(3);
     wait_vm<0>();                           // drain the ring before the epilogue's own loads
+    if constexpr (KG == 2) {
+        // group 1 hands its partial tile to group 0 through LDS (ring and planes
+        // are dead); group 0 adds it in a fixed order.  Group 1 then runs the
+        // epilogue's barriers with its stores muted ("live" below).
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(smem) + (size_t)wave * WM * G::EROW;
+        if (kg == 1) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) red[((i * NJ + j) * 16 + r) * 64 + lane] = acc[i][j][r];
+        }
+        __syncthreads();
+        if (kg == 0) {
+            const float* o = reinterpret_cast<const float*>(smem) + (size_t)(wave + NWT) * WM * G::EROW;
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[i][j][r] += o[((i * NJ + j) * 16 + r) * 64 + lane];
+        }
+        __syncthreads();                    // partner areas read before the epilogue reuses LDS
+    }
 
     // ---------------------------------------------------------------- epilogue
     // lane = one GEMM row per m-block; registers 4g..4g+3 of a block = 4 consecutive columns
     const bool partial = a.S > 1;
+    const bool live = KG == 1 || kg == 0;   // the wave that stores its tile
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
 #pragma unroll
@@ -449,6 +496,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
                 a.partial + ((int64_t)split * a.B + b) * (int64_t)a.M * a.U, a.M * a.U * 4);
 #pragma unroll
             for (int it = 0; it < WM / RPI; ++it) {
+                if (!live) break;
                 const int r = it * RPI + rr;
                 const int m = mw + r;
                 const float* vp = et + r * G::EROW + cc;
@@ -492,6 +540,10 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
             if (!*last_s) {
                 stamp(4);
                 return;
+            }
+            if (!live) {
+                stamp(4);
+                return;                             // (no barrier follows)
             }
             constexpr int IT = WM / RPI;
             s_f32x4 sum[IT];
@@ -549,6 +601,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
             stamp(4);
             return;
         }
+        if (!live) return;                          // (no barrier follows)
         const __amdgpu_buffer_rsrc_t yrs = make_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
         const __amdgpu_buffer_rsrc_t rrs = make_rsrc(a.res ? a.res + (int64_t)b * a.r_sb : a.y, a.res ? a.r_bytes : 0);
         if (a.vec_y) {
@@ -600,6 +653,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM))) void conv1d_sp
         stamp(4);
         return;
     }
+    if (!live) return;
     const __amdgpu_buffer_rsrc_t yrs = make_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
     {   // ConvTranspose: phase-interleaved columns t = n*R + q, one store per element
 #pragma unroll
@@ -647,25 +701,47 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(ConvKArgs a) {
 
 // --------------------------------------------------------------------- host side
 struct SplitCfg {
-    int bm, bn, wm, S, sep;
+    int tile, S, sep;     // kSplitTiles index, K-splits, separate reduce launch
 };
 
-// Tile + split-K choice.  Tiles (BM rows x BN columns, wave WM x 4096/WM):
-// least padding with the most waves per workgroup that still fills the chip;
-// K split over workgroups (fp32 slabs + a fixed-order reduce) when the output
-// alone cannot give every SIMD a wave.
-constexpr int kSplitTiles[6][3] = {{128, 128, 32}, {64, 256, 32}, {64, 128, 32},
-                                   {256, 64, 64}, {128, 64, 64}, {64, 64, 64}};
-template <int KT>
-static bool split_tile_fits(int idx) {   // the 4-byte-DMA variant is the larger one
-    switch (idx) {
-        case 0: return SGeo<KT, 128, 128, 32, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 128, 128, 32, false>::LDS_ALL <= 160 * 1024;
-        case 1: return SGeo<KT, 64, 256, 32, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 64, 256, 32, false>::LDS_ALL <= 160 * 1024;
-        case 2: return SGeo<KT, 64, 128, 32, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 64, 128, 32, false>::LDS_ALL <= 160 * 1024;
-        case 3: return SGeo<KT, 256, 64, 64, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 256, 64, 64, false>::LDS_ALL <= 160 * 1024;
-        case 4: return SGeo<KT, 128, 64, 64, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 128, 64, 64, false>::LDS_ALL <= 160 * 1024;
-        default: return SGeo<KT, 64, 64, 64, true>::LDS_ALL <= 160 * 1024 && SGeo<KT, 64, 64, 64, false>::LDS_ALL <= 160 * 1024;
+// Tile + split-K choice.  Tiles (BM rows x BN columns, wave WM x 4096/WM,
+// KG waves per output tile): least padding with the most waves per workgroup
+// that still fills the chip; K split over workgroups (fp32 slabs, fixed-order
+// combine) when the output alone cannot give every SIMD a wave.
+constexpr int kNumSplitTiles = 10;
+constexpr int kSplitTiles[kNumSplitTiles][4] = {
+    {128, 128, 32, 1}, {64, 256, 32, 1}, {64, 128, 32, 1}, {256, 64, 64, 1}, {128, 64, 64, 1},
+    {64, 64, 64, 1},   {128, 64, 64, 2}, {64, 128, 32, 2}, {128, 128, 32, 2}, {256, 64, 64, 2}};
+
+// Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>) for tile index ti (compile-time dispatch).
+template <typename Fn>
+static auto with_tile(int ti, Fn&& f) {
+    switch (ti) {
+        case 0: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<1>{});
+        case 1: return f(IC<64>{}, IC<256>{}, IC<32>{}, IC<1>{});
+        case 2: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{});
+        case 3: return f(IC<256>{}, IC<64>{}, IC<64>{}, IC<1>{});
+        case 4: return f(IC<128>{}, IC<64>{}, IC<64>{}, IC<1>{});
+        case 5: return f(IC<64>{}, IC<64>{}, IC<64>{}, IC<1>{});
+        case 6: return f(IC<128>{}, IC<64>{}, IC<64>{}, IC<2>{});
+        case 7: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{});
+        case 8: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<2>{});
+        default: return f(IC<256>{}, IC<64>{}, IC<64>{}, IC<2>{});
     }
+}
+static inline int tile_waves(int ti) {   // waves per workgroup
+    const int* t = kSplitTiles[ti];
+    return (t[0] / t[2]) * (t[1] / (4096 / t[2])) * t[3];
+}
+
+template <int KT>
+static bool split_tile_fits(int idx) {   // both DMA variants must fit
+    return with_tile(idx, [](auto bm, auto bn, auto wm, auto kg) {
+        constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
+                      KG = decltype(kg)::value;
+        return SGeo<KT, BM, BN, WM, true, KG>::LDS_ALL <= 160 * 1024 &&
+               SGeo<KT, BM, BN, WM, false, KG>::LDS_ALL <= 160 * 1024;
+    });
 }
 static bool split_fits(int taps, int idx) {
     switch (taps) {
@@ -683,22 +759,22 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
     auto waste = [&](int bm, int bn) {
         return double(ceil_div(M, bm) * bm) * double(ceil_div(U, bn) * bn) / (double(M) * double(U));
     };
-    SplitCfg best{64, 64, 64, 1, 0};
+    SplitCfg best{5, 1, 0};
     double bscore = 1e30;
-    for (int ti = 0; ti < 6; ++ti) {
+    for (int ti = 0; ti < 6; ++ti) {                // the heuristic keeps to the KG = 1 tiles
         const int* c = all[ti];
         if (!split_fits(taps, ti)) continue;
         if (split_row < M && split_row % c[2] != 0) continue;      // a wave never straddles ConvT groups
-        const int nw = (c[0] / c[2]) * (c[1] / (4096 / c[2]));
+        const int nw = tile_waves(ti);
         const int64_t wgs = (int64_t)ceil_div(M, c[0]) * ceil_div(U, c[1]) * B;
         const int64_t waves = wgs * nw;
         double score = waste(c[0], c[1]);
         if (waves < 1024) score *= 1.0 + 0.5 * (1024.0 / waves - 1.0) / std::max(1, nchunks / 8);
         score *= 1.0 + 0.03 * (4 - nw);                                 // prefer fat workgroups
-        if (score < bscore) { bscore = score; best = {c[0], c[1], c[2], 1, 0}; }
+        if (score < bscore) { bscore = score; best = {ti, 1, 0}; }
     }
-    const int nw = (best.bm / best.wm) * (best.bn / (4096 / best.wm));
-    const int64_t waves = (int64_t)ceil_div(M, best.bm) * ceil_div(U, best.bn) * B * nw;
+    const int* bt = all[best.tile];
+    const int64_t waves = (int64_t)ceil_div(M, bt[0]) * ceil_div(U, bt[1]) * B * tile_waves(best.tile);
     if (waves < 1024 && nchunks >= 8) {
         int S = (int)std::min<int64_t>(16, ceil_div64(2048, waves));
         S = std::min(S, nchunks / 4);
@@ -707,9 +783,9 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
     return best;
 }
 
-template <int KT, int BM, int BN, int WM, bool XV>
+template <int KT, int BM, int BN, int WM, int KG, bool XV>
 static int split_launch_xv(ConvKArgs k, hipStream_t st) {
-    using G = SGeo<KT, BM, BN, WM, XV>;
+    using G = SGeo<KT, BM, BN, WM, XV, KG>;
     if constexpr (G::LDS_ALL > 160 * 1024) {
         set_error("conv1d(split16): tile exceeds LDS");
         return RAVE_ERR_UNSUPPORTED;
@@ -722,7 +798,8 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
     static_assert(lds <= 160 * 1024, "LDS budget");
     dim3 grid(k.gx * k.gy * k.B * k.S);
     const bool snake = k.act == RAVE_ACT_SNAKE;
-    auto kern = snake ? conv1d_split_kernel<KT, BM, BN, WM, true, XV> : conv1d_split_kernel<KT, BM, BN, WM, false, XV>;
+    auto kern = snake ? conv1d_split_kernel<KT, BM, BN, WM, true, XV, KG>
+                      : conv1d_split_kernel<KT, BM, BN, WM, false, XV, KG>;
     if (lds > 64 * 1024) {
         static bool done[2] = {false, false};
         if (!done[snake]) {
@@ -736,23 +813,19 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
     }
 }
 
-template <int KT, int BM, int BN, int WM>
-static int split_launch_k(ConvKArgs k, hipStream_t st) {
-    return k.x_vec ? split_launch_xv<KT, BM, BN, WM, true>(k, st) : split_launch_xv<KT, BM, BN, WM, false>(k, st);
-}
-
 template <int KT>
 static int split_launch_family(ConvKArgs k, const SplitCfg& c, hipStream_t st) {
-    k.XW = c.bn + (SFam<KT>::Q - 1) * k.d + (k.transposed ? 1 : 0);
+    const int* t = kSplitTiles[c.tile];
+    k.XW = t[1] + (SFam<KT>::Q - 1) * k.d + (k.transposed ? 1 : 0);
     k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
     const unsigned rl = (unsigned)(k.XW * SFam<KT>::S);
     k.rl_magic = (unsigned)((0x100000000ull + rl - 1) / rl);
-    if (c.bm == 128 && c.bn == 128) return split_launch_k<KT, 128, 128, 32>(k, st);
-    if (c.bm == 64 && c.bn == 256) return split_launch_k<KT, 64, 256, 32>(k, st);
-    if (c.bm == 64 && c.bn == 128) return split_launch_k<KT, 64, 128, 32>(k, st);
-    if (c.bm == 256 && c.bn == 64) return split_launch_k<KT, 256, 64, 64>(k, st);
-    if (c.bm == 128 && c.bn == 64) return split_launch_k<KT, 128, 64, 64>(k, st);
-    return split_launch_k<KT, 64, 64, 64>(k, st);
+    return with_tile(c.tile, [&](auto bm, auto bn, auto wm, auto kg) {
+        constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
+                      KG = decltype(kg)::value;
+        return k.x_vec ? split_launch_xv<KT, BM, BN, WM, KG, true>(k, st)
+                       : split_launch_xv<KT, BM, BN, WM, KG, false>(k, st);
+    });
 }
 
 static int split_prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
@@ -776,7 +849,7 @@ static int split_prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
 }
 
 static bool split_tile_ok(int taps, int ti, int M, int split_row) {
-    return ti >= 0 && ti < 6 && split_fits(taps, ti) &&
+    return ti >= 0 && ti < kNumSplitTiles && split_fits(taps, ti) &&
            (split_row >= M || split_row % kSplitTiles[ti][2] == 0);   // a wave never straddles ConvT groups
 }
 
@@ -790,7 +863,7 @@ static int split_resolve(const rave_conv1d_args& a, const ConvKArgs& k, int taps
     RAVE_CHECK_ARG(decode_config(a.config, cc) && split_tile_ok(taps, cc.tile, k.M, k.split_row) &&
                        split_count_distinct(cc.S, k.nchunks),
                    "conv1d(split16): config not valid for these args (see rave_conv1d_configs)");
-    c = {kSplitTiles[cc.tile][0], kSplitTiles[cc.tile][1], kSplitTiles[cc.tile][2], cc.S, cc.sep};
+    c = {cc.tile, cc.S, cc.sep};
     return RAVE_OK;
 }
 
@@ -804,16 +877,17 @@ int conv1d_split_configs(const rave_conv1d_args& a, int32_t* cfgs, int max_cfgs)
         if (n < max_cfgs && cfgs) cfgs[n] = v;
         ++n;
     };
-    for (int ti = 0; ti < 6; ++ti) {
+    for (int ti = 0; ti < kNumSplitTiles; ++ti) {
         if (!split_tile_ok(taps, ti, k.M, k.split_row)) continue;
         const int* t = kSplitTiles[ti];
-        const int nw = (t[0] / t[2]) * (t[1] / (4096 / t[2]));
+        const int nw = tile_waves(ti);
         const int64_t ntiles = (int64_t)ceil_div(k.M, t[0]) * ceil_div(k.U, t[1]) * k.B;
         for (int S : kSplitCands) {
             if (!split_count_distinct(S, k.nchunks)) continue;
             const int64_t waves = ntiles * nw * S;
             if (S > 1 && (waves > 16384 || ntiles * nw >= 4096)) continue;   // enough waves unsplit
-            if (S == 1 || ntiles <= kSplitTickets) put(encode_config(ti, S, 0));
+            // in-launch combine: the last split reads S slabs serially -- only for few splits
+            if (S == 1 || (S <= 4 && ntiles <= kSplitTickets)) put(encode_config(ti, S, 0));
             if (S > 1) put(encode_config(ti, S, 1));
         }
     }
@@ -845,8 +919,8 @@ int conv1d_split(const rave_conv1d_args& a, void* stream) {
     k.tickets = reinterpret_cast<int*>(a.partial);
     k.partial = a.partial ? a.partial + kSplitTickets : nullptr;   // slabs after the counters
     k.vec_p = (k.U % 4 == 0) && (!k.partial || reinterpret_cast<uintptr_t>(k.partial) % 16 == 0);
-    k.gx = ceil_div(k.U, c.bn);
-    k.gy = ceil_div(k.M, c.bm);
+    k.gx = ceil_div(k.U, kSplitTiles[c.tile][1]);
+    k.gy = ceil_div(k.M, kSplitTiles[c.tile][0]);
     const int64_t ntiles = (int64_t)k.gx * k.gy * k.B;
     RAVE_CHECK_ARG(ntiles * k.S < (1ll << 31), "conv1d(split16): grid too large");
     // the last-arriving split sums the tile's slabs (16-byte slab rows, counters for every tile)

@@ -98,7 +98,7 @@ def cfg_str(c):
     if c == 0:
         return "heuristic"
     v = c - 1
-    return f"tile{v & 7} S{((v >> 3) & 31) + 1}{' sep' if (v >> 8) & 1 else ''}"
+    return f"tile{v & 15} S{((v >> 4) & 31) + 1}{' sep' if (v >> 9) & 1 else ''}"
 
 
 def run(name, B, iters, dev, config=0):
