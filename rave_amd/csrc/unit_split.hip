@@ -18,7 +18,7 @@
 //   seam      h = act2(h * rs1 + b1) -> (hi, lo) planes over the dead window
 //   phase 2   y = W2 (C x C) . h, ring running on from W1 into W2
 //   epilogue  y * rs2 + b2 + x (residual re-read, L2-hot) -> HBM
-// Each wave owns 64 rows x 64 columns (2 x 2 blocks of 32x32).
+// Each wave owns 32 rows x 64 columns (1 x 2 blocks of 32x32).
 #include "common.h"
 
 #include <algorithm>
@@ -35,6 +35,9 @@ typedef float us_f32x4 __attribute__((ext_vector_type(4)));
 typedef float us_f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kUSMaxDil = 16;
+template <int V> struct IC {
+    static constexpr int value = V;
+};
 
 #ifdef RAVE_STAMPS
 // diagnostic build only: 8 clock stamps per workgroup (tools/layer_bench.py --stamps)
@@ -83,9 +86,10 @@ __device__ __forceinline__ float us_act(float v, float slope, float alpha) {
     }
 }
 
-// C channels; WGN waves along time (each 64 columns); C/64 waves along rows.
-template <int C, int WGN> struct USGeo {
-    static constexpr int WGM = C / 64, NW = WGM * WGN, NT = 64 * NW;
+// C channels; WGN waves along time (each 64 columns); C/(32 MI) waves along
+// rows (each MI 32-row blocks).
+template <int C, int WGN, int MI> struct USGeo {
+    static constexpr int WGM = C / (32 * MI), NW = WGM * WGN, NT = 64 * NW;
     static constexpr int BN = 64 * WGN;
     static constexpr int S1 = 3 * C / 16, S2 = C / 16, ST = S1 + S2;   // K-steps
     static constexpr int PH = C + 8;                  // halves per LDS row (conflict-free b128)
@@ -97,12 +101,12 @@ template <int C, int WGN> struct USGeo {
     static constexpr int G8 = C / 8;                  // 8-channel groups per window row
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;
     static constexpr int R = 3;                       // weight ring depth (K-steps)
-    static_assert(C % 64 == 0, "C multiple of 64");
+    static_assert(C % 64 == 0 && (MI == 1 || MI == 2) && NW <= 16, "geometry");
 };
 
-template <int C, int WGN, bool SNAKE>
-__global__ __launch_bounds__(64 * (C / 64) * WGN) void unit_split_kernel(USArgs a) {
-    using G = USGeo<C, WGN>;
+template <int C, int WGN, int MI, bool SNAKE>
+__global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN) void unit_split_kernel(USArgs a) {
+    using G = USGeo<C, WGN, MI>;
     constexpr int NT = G::NT, PH = G::PH, G8 = G::G8, XT = G::XT, R = G::R;
     constexpr int S1 = G::S1, ST = G::ST, CG = C / 16;
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -127,12 +131,12 @@ __global__ __launch_bounds__(64 * (C / 64) * WGN) void unit_split_kernel(USArgs 
     const auto wrs = us_rsrc(a.w, a.w_bytes);
 
     // ------------------------------------------------------------ weight ring
-    // this wave's m-blocks 2wm, 2wm+1; fragment (mb, s, plane) at ((mb*ST + s)*2 + plane) KB
-    us_h8 ring[R][2][2];
-    const unsigned abase = (unsigned)((2 * wm) * ST * 2) * 1024u + (unsigned)lane * 16u;
+    // this wave's m-blocks MI*wm .. MI*wm+MI-1; fragment (mb, s, plane) at ((mb*ST + s)*2 + plane) KB
+    us_h8 ring[R][MI][2];
+    const unsigned abase = (unsigned)((MI * wm) * ST * 2) * 1024u + (unsigned)lane * 16u;
     auto load_a = [&](int s) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int p = 0; p < 2; ++p)
                 ring[s % R][i][p] = __builtin_bit_cast(us_h8, __builtin_amdgcn_raw_buffer_load_b128(
@@ -189,9 +193,9 @@ __global__ __launch_bounds__(64 * (C / 64) * WGN) void unit_split_kernel(USArgs 
     US_STAMP(1);
 
     // ------------------------------------------------------------ K loop (both phases)
-    us_f32x16 acc[2][2];
+    us_f32x16 acc[MI][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -220,30 +224,30 @@ __global__ __launch_bounds__(64 * (C / 64) * WGN) void unit_split_kernel(USArgs 
         }
     };
     auto step = [&](int s, const BF& f) __attribute__((always_inline)) {
-        us_h8 ah[2], al[2], a2[2];
+        us_h8 ah[MI], al[MI], a2[MI];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < MI; ++i) {
             ah[i] = ring[s % R][i][0];
             al[i] = ring[s % R][i][1];
             a2[i] = ah[i] * (_Float16)2048.0f;
         }
         load_a(s + R);                               // refill the slot (runs on into W2)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], f.h[j], acc[i][j], 0, 0, 0);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], f.l[j], acc[i][j], 0, 0, 0);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], f.h[j], acc[i][j], 0, 0, 0);
     };
 
-    // per-lane rows of the accumulators: m = 64wm + 32i + 8g + 4hh + e
-    const int mrow0 = 64 * wm + 4 * hh;
+    // per-lane rows of the accumulators: m = 32 MI wm + 32i + 8g + 4hh + e
+    const int mrow0 = 32 * MI * wm + 4 * hh;
     {
         BF f[2];
         read_b(0, f[0]);
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(64 * (C / 64) * WGN) void unit_split_kernel(USArgs 
     // ------------------------------------------------------------ seam: h = act2(h*rs1 + b1) -> planes
     {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int m = mrow0 + 32 * i + 8 * g;
@@ -280,7 +284,7 @@ __global__ __launch_bounds__(64 * (C / 64) * WGN) void unit_split_kernel(USArgs 
                 }
             }
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -305,13 +309,13 @@ __global__ __launch_bounds__(64 * (C / 64) * WGN) void unit_split_kernel(USArgs 
     // every residual load issued before the first store (one exposed latency)
     {
         const auto yrs = us_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
-        float res[2][2][16];
+        float res[MI][2][16];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int n = n0 + col0 + 32 * j;
             const bool nok = n < a.T;
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < MI; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = mrow0 + 32 * i + 8 * (r >> 2) + (r & 3);
@@ -320,7 +324,7 @@ __global__ __launch_bounds__(64 * (C / 64) * WGN) void unit_split_kernel(USArgs 
                 }
         }
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int m = mrow0 + 32 * i + 8 * g;
@@ -341,15 +345,15 @@ __global__ __launch_bounds__(64 * (C / 64) * WGN) void unit_split_kernel(USArgs 
     US_STAMP(5);
 }
 
-template <int C, int WGN>
+template <int C, int WGN, int MI>
 static int us_launch(USArgs k, int B, bool snake, hipStream_t st) {
-    using G = USGeo<C, WGN>;
+    using G = USGeo<C, WGN, MI>;
     if (k.XW > G::XW_MAX) {
         set_error("residual_unit(split16): dilation too large");
         return RAVE_ERR_UNSUPPORTED;
     }
     k.ntiles = ceil_div(k.T, G::BN);
-    auto kern = snake ? unit_split_kernel<C, WGN, true> : unit_split_kernel<C, WGN, false>;
+    auto kern = snake ? unit_split_kernel<C, WGN, MI, true> : unit_split_kernel<C, WGN, MI, false>;
     static bool attr[2] = {false, false};
     if (G::LDS > 65536 && !attr[snake]) {
         RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -458,18 +462,17 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
     k.bias_bytes = a.bias1 ? C * 4 : 0;
     const bool snake = a.act == RAVE_ACT_SNAKE;
     hipStream_t st = as_stream(stream);
-    if (C == 64) {
-        k.XW = USGeo<64, 2>::BN + 2 * a.dilation;
+    // one 32-row block per wave (MI = 1): C/32 waves along rows, 64 columns each
+    // (measured against two row blocks per wave and other column counts:
+    // tools/layer_bench.py unit_64/128/256)
+    auto go = [&](auto cc, auto wgn, auto mi) {
+        constexpr int CC = decltype(cc)::value, WGN = decltype(wgn)::value, MI = decltype(mi)::value;
+        k.XW = USGeo<CC, WGN, MI>::BN + 2 * a.dilation;
         k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
-        return us_launch<64, 2>(k, a.batch, snake, st);
-    }
-    if (C == 128) {
-        k.XW = USGeo<128, 1>::BN + 2 * a.dilation;
-        k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
-        return us_launch<128, 1>(k, a.batch, snake, st);
-    }
-    k.XW = USGeo<256, 1>::BN + 2 * a.dilation;
-    k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
-    return us_launch<256, 1>(k, a.batch, snake, st);
+        return us_launch<CC, WGN, MI>(k, a.batch, snake, st);
+    };
+    if (C == 64) return go(IC<64>{}, IC<2>{}, IC<1>{});
+    if (C == 128) return go(IC<128>{}, IC<1>{}, IC<1>{});
+    return go(IC<256>{}, IC<1>{}, IC<1>{});
 }
 }  // namespace rave
