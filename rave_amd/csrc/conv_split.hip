@@ -28,9 +28,10 @@
 //     activation applied and split once per element on the way in, so each
 //     B-fragment (8 channels of one column) is one ds_read_b128.
 // Double-buffered (one barrier per chunk): chunk c+2's loads are in flight
-// while chunk c+1 is multiplied.  Each wave owns a 64x64 output tile (2x2
-// blocks of 32x32).  Split-K over grid.z for short-N layers (fp32 slabs,
-// fixed-order reduce: deterministic).
+// while chunk c+1 is multiplied.  Each wave owns 2 or 4 blocks of 32x32
+// (32x64, 64x64 or 32x128 outputs); optionally two waves ("K-groups") share a
+// tile's K-steps.  Split-K over workgroups for short-N layers (fp32 slabs,
+// fixed-order combine: deterministic).  The autotuner picks the tile.
 #include "conv_shared.h"
 
 #include <cmath>
@@ -134,11 +135,11 @@ __device__ __forceinline__ u32x4_t raw_rsrc(const void* p, int bytes) {
 // columns (WM = 32: 128 columns; WM = 64: 64 columns), four 32x32 blocks.
 // KG = 2: two waves per output tile ("K-groups"), each taking part of every
 // chunk's K-steps (group 0 the first ceil(KSC/2)); summed through LDS at the end.
-template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1> struct SGeo {
+template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 4096 / WM> struct SGeo {
     using F = SFam<KT>;
     static constexpr int Q = F::Q, S = F::S, VC = F::VC;
     static constexpr int KSC = Q * VC / 16, CPC = VC / S;
-    static constexpr int WN = 4096 / WM, NJ = WM / 32, NI = WN / 32;
+    static constexpr int WN = WN_, NJ = WM / 32, NI = WN / 32;
     static constexpr int WGM = BM / WM, WGN = BN / WN, NWT = WGM * WGN, NW = NWT * KG, NT = 64 * NW;
     static constexpr int KS0 = (KSC + KG - 1) / KG, KS1 = KSC - KS0;   // K-steps of group 0 / 1
     // window rows: columns + tap reach (+1: ConvT phase group 1 reads one row later)
@@ -164,7 +165,7 @@ template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1> struct SGe
     static constexpr int G8 = VC / 8;                        // 8-channel groups per row
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;   // convert tasks per thread
     static_assert(XPLANE % 16 == 0 && STAGE % 16 == 0, "16-byte LDS alignment");
-    static_assert(NI * NJ == 4 && NW >= 1 && NW <= 8, "tile");
+    static_assert((NI * NJ == 4 || NI * NJ == 2) && NW >= 1 && NW <= 8, "tile");
     static_assert(KG == 1 || (KG == 2 && KS1 >= 1), "K-groups");
     static_assert(WR + XI <= 63, "vmcnt range");
 };
@@ -173,9 +174,9 @@ template <int V> struct IC {
     static constexpr int value = V;
 };
 
-template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG>
-__global__ __launch_bounds__(64 * (BM / WM) * (BN / (4096 / WM)) * KG) void conv1d_split_kernel(ConvKArgs a) {
-    using G = SGeo<KT, BM, BN, WM, XV, KG>;
+template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split_kernel(ConvKArgs a) {
+    using G = SGeo<KT, BM, BN, WM, XV, KG, WN_>;
     constexpr int S = G::S, VC = G::VC, KSC = G::KSC, CPC = G::CPC, PH = G::PH;
     constexpr int NT = G::NT, NW = G::NW, NWT = G::NWT, WGM = G::WGM, G8 = G::G8, XT = G::XT;
     constexpr int NI = G::NI, NJ = G::NJ, WN = G::WN;
@@ -704,43 +705,49 @@ struct SplitCfg {
     int tile, S, sep;     // kSplitTiles index, K-splits, separate reduce launch
 };
 
-// Tile + split-K choice.  Tiles (BM rows x BN columns, wave WM x 4096/WM,
+// Tile + split-K choice.  Tiles (BM rows x BN columns, wave WM x WN,
 // KG waves per output tile): least padding with the most waves per workgroup
 // that still fills the chip; K split over workgroups (fp32 slabs, fixed-order
 // combine) when the output alone cannot give every SIMD a wave.
-constexpr int kNumSplitTiles = 10;
-constexpr int kSplitTiles[kNumSplitTiles][4] = {
-    {128, 128, 32, 1}, {64, 256, 32, 1}, {64, 128, 32, 1}, {256, 64, 64, 1}, {128, 64, 64, 1},
-    {64, 64, 64, 1},   {128, 64, 64, 2}, {64, 128, 32, 2}, {128, 128, 32, 2}, {256, 64, 64, 2}};
+constexpr int kNumSplitTiles = 14;
+constexpr int kSplitTiles[kNumSplitTiles][5] = {   // BM, BN, WM, KG, WN
+    {128, 128, 32, 1, 128}, {64, 256, 32, 1, 128}, {64, 128, 32, 1, 128}, {256, 64, 64, 1, 64},
+    {128, 64, 64, 1, 64},   {64, 64, 64, 1, 64},   {128, 64, 64, 2, 64},  {64, 128, 32, 2, 128},
+    {128, 128, 32, 2, 128}, {256, 64, 64, 2, 64},  {128, 64, 32, 1, 64},  {64, 128, 32, 1, 64},
+    {256, 64, 32, 1, 64},   {128, 128, 32, 1, 64}};
 
-// Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>) for tile index ti (compile-time dispatch).
+// Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>, IC<WN>) for tile index ti (compile-time dispatch).
 template <typename Fn>
 static auto with_tile(int ti, Fn&& f) {
     switch (ti) {
-        case 0: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<1>{});
-        case 1: return f(IC<64>{}, IC<256>{}, IC<32>{}, IC<1>{});
-        case 2: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{});
-        case 3: return f(IC<256>{}, IC<64>{}, IC<64>{}, IC<1>{});
-        case 4: return f(IC<128>{}, IC<64>{}, IC<64>{}, IC<1>{});
-        case 5: return f(IC<64>{}, IC<64>{}, IC<64>{}, IC<1>{});
-        case 6: return f(IC<128>{}, IC<64>{}, IC<64>{}, IC<2>{});
-        case 7: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{});
-        case 8: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<2>{});
-        default: return f(IC<256>{}, IC<64>{}, IC<64>{}, IC<2>{});
+        case 0: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<128>{});
+        case 1: return f(IC<64>{}, IC<256>{}, IC<32>{}, IC<1>{}, IC<128>{});
+        case 2: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<128>{});
+        case 3: return f(IC<256>{}, IC<64>{}, IC<64>{}, IC<1>{}, IC<64>{});
+        case 4: return f(IC<128>{}, IC<64>{}, IC<64>{}, IC<1>{}, IC<64>{});
+        case 5: return f(IC<64>{}, IC<64>{}, IC<64>{}, IC<1>{}, IC<64>{});
+        case 6: return f(IC<128>{}, IC<64>{}, IC<64>{}, IC<2>{}, IC<64>{});
+        case 7: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<128>{});
+        case 8: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<128>{});
+        case 9: return f(IC<256>{}, IC<64>{}, IC<64>{}, IC<2>{}, IC<64>{});
+        case 10: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});
+        case 11: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{});
+        case 12: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});
+        default: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{});
     }
 }
 static inline int tile_waves(int ti) {   // waves per workgroup
     const int* t = kSplitTiles[ti];
-    return (t[0] / t[2]) * (t[1] / (4096 / t[2])) * t[3];
+    return (t[0] / t[2]) * (t[1] / t[4]) * t[3];
 }
 
 template <int KT>
 static bool split_tile_fits(int idx) {   // both DMA variants must fit
-    return with_tile(idx, [](auto bm, auto bn, auto wm, auto kg) {
+    return with_tile(idx, [](auto bm, auto bn, auto wm, auto kg, auto wn) {
         constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
-                      KG = decltype(kg)::value;
-        return SGeo<KT, BM, BN, WM, true, KG>::LDS_ALL <= 160 * 1024 &&
-               SGeo<KT, BM, BN, WM, false, KG>::LDS_ALL <= 160 * 1024;
+                      KG = decltype(kg)::value, WN = decltype(wn)::value;
+        return SGeo<KT, BM, BN, WM, true, KG, WN>::LDS_ALL <= 160 * 1024 &&
+               SGeo<KT, BM, BN, WM, false, KG, WN>::LDS_ALL <= 160 * 1024;
     });
 }
 static bool split_fits(int taps, int idx) {
@@ -783,9 +790,9 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
     return best;
 }
 
-template <int KT, int BM, int BN, int WM, int KG, bool XV>
+template <int KT, int BM, int BN, int WM, int KG, int WN, bool XV>
 static int split_launch_xv(ConvKArgs k, hipStream_t st) {
-    using G = SGeo<KT, BM, BN, WM, XV, KG>;
+    using G = SGeo<KT, BM, BN, WM, XV, KG, WN>;
     if constexpr (G::LDS_ALL > 160 * 1024) {
         set_error("conv1d(split16): tile exceeds LDS");
         return RAVE_ERR_UNSUPPORTED;
@@ -798,8 +805,8 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
     static_assert(lds <= 160 * 1024, "LDS budget");
     dim3 grid(k.gx * k.gy * k.B * k.S);
     const bool snake = k.act == RAVE_ACT_SNAKE;
-    auto kern = snake ? conv1d_split_kernel<KT, BM, BN, WM, true, XV, KG>
-                      : conv1d_split_kernel<KT, BM, BN, WM, false, XV, KG>;
+    auto kern = snake ? conv1d_split_kernel<KT, BM, BN, WM, true, XV, KG, WN>
+                      : conv1d_split_kernel<KT, BM, BN, WM, false, XV, KG, WN>;
     if (lds > 64 * 1024) {
         static bool done[2] = {false, false};
         if (!done[snake]) {
@@ -820,11 +827,11 @@ static int split_launch_family(ConvKArgs k, const SplitCfg& c, hipStream_t st) {
     k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
     const unsigned rl = (unsigned)(k.XW * SFam<KT>::S);
     k.rl_magic = (unsigned)((0x100000000ull + rl - 1) / rl);
-    return with_tile(c.tile, [&](auto bm, auto bn, auto wm, auto kg) {
+    return with_tile(c.tile, [&](auto bm, auto bn, auto wm, auto kg, auto wn) {
         constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
-                      KG = decltype(kg)::value;
-        return k.x_vec ? split_launch_xv<KT, BM, BN, WM, KG, true>(k, st)
-                       : split_launch_xv<KT, BM, BN, WM, KG, false>(k, st);
+                      KG = decltype(kg)::value, WN = decltype(wn)::value;
+        return k.x_vec ? split_launch_xv<KT, BM, BN, WM, KG, WN, true>(k, st)
+                       : split_launch_xv<KT, BM, BN, WM, KG, WN, false>(k, st);
     });
 }
 

@@ -88,8 +88,8 @@ __device__ __forceinline__ float us_act(float v, float slope, float alpha) {
 
 // C channels; WGN waves along time (each 64 columns); C/(32 MI) waves along
 // rows (each MI 32-row blocks).
-template <int C, int WGN, int MI> struct USGeo {
-    static constexpr int WGM = C / (32 * MI), NW = WGM * WGN, NT = 64 * NW;
+template <int C, int WGN, int MI, int KG = 1> struct USGeo {
+    static constexpr int WGM = C / (32 * MI), NWT = WGM * WGN, NW = NWT * KG, NT = 64 * NW;
     static constexpr int BN = 64 * WGN;
     static constexpr int S1 = 3 * C / 16, S2 = C / 16, ST = S1 + S2;   // K-steps
     static constexpr int PH = C + 8;                  // halves per LDS row (conflict-free b128)
@@ -101,12 +101,15 @@ template <int C, int WGN, int MI> struct USGeo {
     static constexpr int G8 = C / 8;                  // 8-channel groups per window row
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;
     static constexpr int R = 3;                       // weight ring depth (K-steps)
+    // K-groups: two waves per output tile take alternate K-steps (both phases)
+    static constexpr int RED = NWT * MI * 2 * 16 * 64 * 4;   // partial-sum hand-off (bytes)
     static_assert(C % 64 == 0 && (MI == 1 || MI == 2) && NW <= 16, "geometry");
+    static_assert(KG == 1 || (KG == 2 && S1 % 2 == 0 && S2 % 2 == 0 && RED <= PLANES), "K-groups");
 };
 
-template <int C, int WGN, int MI, bool SNAKE>
-__global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN) void unit_split_kernel(USArgs a) {
-    using G = USGeo<C, WGN, MI>;
+template <int C, int WGN, int MI, int KG, bool SNAKE>
+__global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_kernel(USArgs a) {
+    using G = USGeo<C, WGN, MI, KG>;
     constexpr int NT = G::NT, PH = G::PH, G8 = G::G8, XT = G::XT, R = G::R;
     constexpr int S1 = G::S1, ST = G::ST, CG = C / 16;
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -118,7 +121,9 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN) void unit_split_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave % G::WGM, wn = wave / G::WGM;
+    const int kg = wave / G::NWT;                    // K-group
+    const int twave = wave - kg * G::NWT;
+    const int wm = twave % G::WGM, wn = twave / G::WGM;
     const int hh = lane >> 5, l32 = lane & 31;
     const int b = blockIdx.x / a.ntiles;
     const int n0 = (blockIdx.x - b * a.ntiles) * G::BN;
@@ -132,18 +137,19 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN) void unit_split_kernel(
 
     // ------------------------------------------------------------ weight ring
     // this wave's m-blocks MI*wm .. MI*wm+MI-1; fragment (mb, s, plane) at ((mb*ST + s)*2 + plane) KB
+    // (ring slot = this wave's local step t % R; s = the global K-step, t*KG + kg)
     us_h8 ring[R][MI][2];
     const unsigned abase = (unsigned)((MI * wm) * ST * 2) * 1024u + (unsigned)lane * 16u;
-    auto load_a = [&](int s) __attribute__((always_inline)) {
+    auto load_a = [&](int slot, int s) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int p = 0; p < 2; ++p)
-                ring[s % R][i][p] = __builtin_bit_cast(us_h8, __builtin_amdgcn_raw_buffer_load_b128(
+                ring[slot][i][p] = __builtin_bit_cast(us_h8, __builtin_amdgcn_raw_buffer_load_b128(
                     wrs, s < ST ? abase + (unsigned)(((i * ST + s) * 2 + p) * 1024) : kUSOOB, 0, 0));
     };
 #pragma unroll
-    for (int s = 0; s < R; ++s) load_a(s);
+    for (int t = 0; t < R; ++t) load_a(t, t * KG + kg);
 
     // ------------------------------------------------------------ per-row table -> LDS
     for (int i = tid; i < 6 * C; i += NT) {
@@ -223,15 +229,15 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN) void unit_split_kernel(
             f.l[j] = *reinterpret_cast<const us_h8*>(pl + off);
         }
     };
-    auto step = [&](int s, const BF& f) __attribute__((always_inline)) {
+    auto step = [&](int t, int s, const BF& f) __attribute__((always_inline)) {
         us_h8 ah[MI], al[MI], a2[MI];
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
-            ah[i] = ring[s % R][i][0];
-            al[i] = ring[s % R][i][1];
+            ah[i] = ring[t % R][i][0];
+            al[i] = ring[t % R][i][1];
             a2[i] = ah[i] * (_Float16)2048.0f;
         }
-        load_a(s + R);                               // refill the slot (runs on into W2)
+        load_a(t % R, s + R * KG);                   // refill the slot (runs on into W2)
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -248,21 +254,52 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN) void unit_split_kernel(
 
     // per-lane rows of the accumulators: m = 32 MI wm + 32i + 8g + 4hh + e
     const int mrow0 = 32 * MI * wm + 4 * hh;
-    {
+    // own K-steps [t0, t1) of this wave's group: global step t*KG + GG
+    auto kloop = [&](auto gtag, auto t0tag, auto t1tag) __attribute__((always_inline)) {
+        constexpr int GG = decltype(gtag)::value;
+        constexpr int T0 = decltype(t0tag)::value, T1 = decltype(t1tag)::value;
         BF f[2];
-        read_b(0, f[0]);
+        read_b(T0 * KG + GG, f[0]);
 #pragma unroll
-        for (int s = 0; s < S1; ++s) {
-            if (s + 1 < S1) read_b(s + 1, f[(s + 1) & 1]);
+        for (int t = T0; t < T1; ++t) {
+            if (t + 1 < T1) read_b((t + 1) * KG + GG, f[(t + 1 - T0) & 1]);
             __builtin_amdgcn_sched_barrier(0);
-            step(s, f[s & 1]);
+            step(t, t * KG + GG, f[(t - T0) & 1]);
         }
-    }
-    __syncthreads();                                 // window dead
+    };
+    // group 1 hands its partial sums to group 0 through LDS (over the dead planes)
+    float* red = reinterpret_cast<float*>(lds);
+    auto combine = [&]() __attribute__((always_inline)) {
+        if constexpr (KG == 2) {
+            __syncthreads();                         // planes dead
+            float* mine = red + twave * (MI * 2 * 16 * 64);
+            if (kg == 1) {
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) mine[((i * 2 + j) * 16 + r) * 64 + lane] = acc[i][j][r];
+            }
+            __syncthreads();
+            if (kg == 0) {
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) acc[i][j][r] += mine[((i * 2 + j) * 16 + r) * 64 + lane];
+            }
+        }
+    };
+    if (KG == 1 || kg == 0) kloop(IC<0>{}, IC<0>{}, IC<S1 / KG>{});
+    else kloop(IC<1>{}, IC<0>{}, IC<S1 / KG>{});
+    combine();
+    __syncthreads();                                 // window (and hand-off area) dead
     US_STAMP(2);
 
     // ------------------------------------------------------------ seam: h = act2(h*rs1 + b1) -> planes
-    {
+    if (KG == 1 || kg == 0) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -283,26 +320,20 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN) void unit_split_kernel(
                     *reinterpret_cast<us_h4*>(pl + (col0 + 32 * j) * PH + m) = lv;
                 }
             }
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     __syncthreads();
     US_STAMP(3);
 
-    {
-        BF f[2];
-        read_b(S1, f[0]);
-#pragma unroll
-        for (int s = S1; s < ST; ++s) {
-            if (s + 1 < ST) read_b(s + 1, f[(s + 1 - S1) & 1]);
-            __builtin_amdgcn_sched_barrier(0);
-            step(s, f[(s - S1) & 1]);
-        }
-    }
+    if (KG == 1 || kg == 0) kloop(IC<0>{}, IC<S1 / KG>{}, IC<ST / KG>{});
+    else kloop(IC<1>{}, IC<S1 / KG>{}, IC<ST / KG>{});
+    combine();
+    if (KG == 2 && kg == 1) return;                  // (no barrier follows)
 
     US_STAMP(4);
     // ------------------------------------------------------------ epilogue: y*rs2 + b2 + x
@@ -345,15 +376,15 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN) void unit_split_kernel(
     US_STAMP(5);
 }
 
-template <int C, int WGN, int MI>
+template <int C, int WGN, int MI, int KG>
 static int us_launch(USArgs k, int B, bool snake, hipStream_t st) {
-    using G = USGeo<C, WGN, MI>;
+    using G = USGeo<C, WGN, MI, KG>;
     if (k.XW > G::XW_MAX) {
         set_error("residual_unit(split16): dilation too large");
         return RAVE_ERR_UNSUPPORTED;
     }
     k.ntiles = ceil_div(k.T, G::BN);
-    auto kern = snake ? unit_split_kernel<C, WGN, MI, true> : unit_split_kernel<C, WGN, MI, false>;
+    auto kern = snake ? unit_split_kernel<C, WGN, MI, KG, true> : unit_split_kernel<C, WGN, MI, KG, false>;
     static bool attr[2] = {false, false};
     if (G::LDS > 65536 && !attr[snake]) {
         RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -463,16 +494,18 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
     const bool snake = a.act == RAVE_ACT_SNAKE;
     hipStream_t st = as_stream(stream);
     // one 32-row block per wave (MI = 1): C/32 waves along rows, 64 columns each
-    // (measured against two row blocks per wave and other column counts:
-    // tools/layer_bench.py unit_64/128/256)
-    auto go = [&](auto cc, auto wgn, auto mi) {
-        constexpr int CC = decltype(cc)::value, WGN = decltype(wgn)::value, MI = decltype(mi)::value;
-        k.XW = USGeo<CC, WGN, MI>::BN + 2 * a.dilation;
+    // (measured against two row blocks per wave, other column counts and
+    // K-groups: tools/layer_bench.py unit_64/128/256)
+    auto go = [&](auto cc, auto wgn, auto mi, auto kgt) {
+        constexpr int CC = decltype(cc)::value, WGN = decltype(wgn)::value, MI = decltype(mi)::value,
+                      KG = decltype(kgt)::value;
+        k.XW = USGeo<CC, WGN, MI, KG>::BN + 2 * a.dilation;
         k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
-        return us_launch<CC, WGN, MI>(k, a.batch, snake, st);
+        return us_launch<CC, WGN, MI, KG>(k, a.batch, snake, st);
     };
-    if (C == 64) return go(IC<64>{}, IC<2>{}, IC<1>{});
-    if (C == 128) return go(IC<128>{}, IC<1>{}, IC<1>{});
-    return go(IC<256>{}, IC<1>{}, IC<1>{});
+    // (K-groups, KG = 2, measured slower for every C: 13.3/11.6/19.5 -> 16.8/12.0/21.5 us)
+    if (C == 64) return go(IC<64>{}, IC<2>{}, IC<1>{}, IC<1>{});
+    if (C == 128) return go(IC<128>{}, IC<1>{}, IC<1>{}, IC<1>{});
+    return go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{});
 }
 }  // namespace rave
