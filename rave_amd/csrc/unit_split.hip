@@ -88,9 +88,9 @@ __device__ __forceinline__ float us_act(float v, float slope, float alpha) {
 
 // C channels; WGN waves along time (each 64 columns); C/(32 MI) waves along
 // rows (each MI 32-row blocks).
-template <int C, int WGN, int MI, int KG = 1> struct USGeo {
+template <int C, int WGN, int MI, int KG = 1, int CB = 2> struct USGeo {
     static constexpr int WGM = C / (32 * MI), NWT = WGM * WGN, NW = NWT * KG, NT = 64 * NW;
-    static constexpr int BN = 64 * WGN;
+    static constexpr int BN = 32 * CB * WGN;           // CB 32-column blocks per wave
     static constexpr int S1 = 3 * C / 16, S2 = C / 16, ST = S1 + S2;   // K-steps
     static constexpr int PH = C + 8;                  // halves per LDS row (conflict-free b128)
     static constexpr int XW_MAX = BN + 2 * kUSMaxDil;
@@ -102,14 +102,14 @@ template <int C, int WGN, int MI, int KG = 1> struct USGeo {
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;
     static constexpr int R = 3;                       // weight ring depth (K-steps)
     // K-groups: two waves per output tile take alternate K-steps (both phases)
-    static constexpr int RED = NWT * MI * 2 * 16 * 64 * 4;   // partial-sum hand-off (bytes)
+    static constexpr int RED = NWT * MI * CB * 16 * 64 * 4;  // partial-sum hand-off (bytes)
     static_assert(C % 64 == 0 && (MI == 1 || MI == 2) && NW <= 16, "geometry");
     static_assert(KG == 1 || (KG == 2 && S1 % 2 == 0 && S2 % 2 == 0 && RED <= PLANES), "K-groups");
 };
 
-template <int C, int WGN, int MI, int KG, bool SNAKE>
+template <int C, int WGN, int MI, int KG, int CB, bool SNAKE>
 __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_kernel(USArgs a) {
-    using G = USGeo<C, WGN, MI, KG>;
+    using G = USGeo<C, WGN, MI, KG, CB>;
     constexpr int NT = G::NT, PH = G::PH, G8 = G::G8, XT = G::XT, R = G::R;
     constexpr int S1 = G::S1, ST = G::ST, CG = C / 16;
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -199,18 +199,18 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     US_STAMP(1);
 
     // ------------------------------------------------------------ K loop (both phases)
-    us_f32x16 acc[MI][2];
+    us_f32x16 acc[MI][CB];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < CB; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     // B fragments: column wn*64 + j*32 + l32, 8 channels at 8*hh
-    const int col0 = wn * 64 + l32;
+    const int col0 = wn * 32 * CB + l32;
     struct BF {
-        us_h8 h[2], l[2];
+        us_h8 h[CB], l[CB];
     };
     auto read_b = [&](int s, BF& f) __attribute__((always_inline)) {
         int row, ch;
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
             ch = (s - S1) * 16;
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < CB; ++j) {
             const int off = (row + j * 32) * PH + ch + 8 * hh;
             f.h[j] = *reinterpret_cast<const us_h8*>(ph + off);
             f.l[j] = *reinterpret_cast<const us_h8*>(pl + off);
@@ -241,15 +241,15 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], f.h[j], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < CB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], f.h[j], acc[i][j], 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], f.l[j], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < CB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], f.l[j], acc[i][j], 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], f.h[j], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < CB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], f.h[j], acc[i][j], 0, 0, 0);
     };
 
     // per-lane rows of the accumulators: m = 32 MI wm + 32i + 8g + 4hh + e
@@ -272,23 +272,23 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     auto combine = [&]() __attribute__((always_inline)) {
         if constexpr (KG == 2) {
             __syncthreads();                         // planes dead
-            float* mine = red + twave * (MI * 2 * 16 * 64);
+            float* mine = red + twave * (MI * CB * 16 * 64);
             if (kg == 1) {
 #pragma unroll
                 for (int i = 0; i < MI; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j)
+                    for (int j = 0; j < CB; ++j)
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) mine[((i * 2 + j) * 16 + r) * 64 + lane] = acc[i][j][r];
+                        for (int r = 0; r < 16; ++r) mine[((i * CB + j) * 16 + r) * 64 + lane] = acc[i][j][r];
             }
             __syncthreads();
             if (kg == 0) {
 #pragma unroll
                 for (int i = 0; i < MI; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j)
+                    for (int j = 0; j < CB; ++j)
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) acc[i][j][r] += mine[((i * 2 + j) * 16 + r) * 64 + lane];
+                        for (int r = 0; r < 16; ++r) acc[i][j][r] += mine[((i * CB + j) * 16 + r) * 64 + lane];
             }
         }
     };
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
                 us_f32x4 al = {0.f, 0.f, 0.f, 0.f};
                 if constexpr (SNAKE) al = *reinterpret_cast<const us_f32x4*>(tab + 2 * C + m);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
+                for (int j = 0; j < CB; ++j) {
                     us_f32x4 v;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] = us_act<SNAKE>(acc[i][j][4 * g + e] * rs[e] + bb[e], slope, al[e]);
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < CB; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     __syncthreads();
@@ -340,9 +340,9 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     // every residual load issued before the first store (one exposed latency)
     {
         const auto yrs = us_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
-        float res[MI][2][16];
+        float res[MI][CB][16];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < CB; ++j) {
             const int n = n0 + col0 + 32 * j;
             const bool nok = n < a.T;
 #pragma unroll
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
                 const us_f32x4 rs = *reinterpret_cast<const us_f32x4*>(tab + 3 * C + m);
                 const us_f32x4 bb = *reinterpret_cast<const us_f32x4*>(tab + 4 * C + m);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
+                for (int j = 0; j < CB; ++j) {
                     const int n = n0 + col0 + 32 * j;
                     const bool nok = n < a.T;
 #pragma unroll
@@ -376,15 +376,15 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     US_STAMP(5);
 }
 
-template <int C, int WGN, int MI, int KG>
+template <int C, int WGN, int MI, int KG, int CB>
 static int us_launch(USArgs k, int B, bool snake, hipStream_t st) {
-    using G = USGeo<C, WGN, MI, KG>;
+    using G = USGeo<C, WGN, MI, KG, CB>;
     if (k.XW > G::XW_MAX) {
         set_error("residual_unit(split16): dilation too large");
         return RAVE_ERR_UNSUPPORTED;
     }
     k.ntiles = ceil_div(k.T, G::BN);
-    auto kern = snake ? unit_split_kernel<C, WGN, MI, KG, true> : unit_split_kernel<C, WGN, MI, KG, false>;
+    auto kern = snake ? unit_split_kernel<C, WGN, MI, KG, CB, true> : unit_split_kernel<C, WGN, MI, KG, CB, false>;
     static bool attr[2] = {false, false};
     if (G::LDS > 65536 && !attr[snake]) {
         RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -395,7 +395,7 @@ static int us_launch(USArgs k, int B, bool snake, hipStream_t st) {
     return launch_status("unit_split_kernel");
 }
 
-static bool us_supported(int C) { return C == 64 || C == 128 || C == 256; }
+static bool us_supported(int C) { return C == 64 || C == 128 || C == 256 || C == 512; }
 
 // Power-of-two row exponent: max |w * 2^e| in [8, 16) (e = 0 for an all-zero row).
 static int us_row_exponent(double amax) {
@@ -421,7 +421,7 @@ extern "C" int64_t rave_unit_split_packed_size(int C) {
 extern "C" int rave_unit_split_pack_weight(const float* w1, const float* w2, int C, float* packed) {
     RAVE_CHECK_ARG(w1 && w2 && packed, "unit_split_pack_weight: null pointer");
     if (!us_supported(C)) {
-        set_error("unit_split_pack_weight: split16 fused residual unit supports C in {64, 128, 256}");
+        set_error("unit_split_pack_weight: split16 fused residual unit supports C in {64, 128, 256, 512}");
         return RAVE_ERR_UNSUPPORTED;
     }
     const int S1 = 3 * C / 16, ST = 4 * C / 16, CG = C / 16;
@@ -474,7 +474,7 @@ namespace rave {
 int residual_unit_split(const rave_unit_args& a, void* stream) {
     const int C = a.channels;
     if (!us_supported(C)) {
-        set_error("residual_unit(split16): fused unit supports C in {64, 128, 256}");
+        set_error("residual_unit(split16): fused unit supports C in {64, 128, 256, 512}");
         return RAVE_ERR_UNSUPPORTED;
     }
     USArgs k{};
@@ -496,16 +496,19 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
     // one 32-row block per wave (MI = 1): C/32 waves along rows, 64 columns each
     // (measured against two row blocks per wave, other column counts and
     // K-groups: tools/layer_bench.py unit_64/128/256)
-    auto go = [&](auto cc, auto wgn, auto mi, auto kgt) {
+    auto go = [&](auto cc, auto wgn, auto mi, auto kgt, auto cb) {
         constexpr int CC = decltype(cc)::value, WGN = decltype(wgn)::value, MI = decltype(mi)::value,
-                      KG = decltype(kgt)::value;
-        k.XW = USGeo<CC, WGN, MI, KG>::BN + 2 * a.dilation;
+                      KG = decltype(kgt)::value, CB = decltype(cb)::value;
+        k.XW = USGeo<CC, WGN, MI, KG, CB>::BN + 2 * a.dilation;
         k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
-        return us_launch<CC, WGN, MI, KG>(k, a.batch, snake, st);
+        return us_launch<CC, WGN, MI, KG, CB>(k, a.batch, snake, st);
     };
     // (K-groups, KG = 2, measured slower for every C: 13.3/11.6/19.5 -> 16.8/12.0/21.5 us)
-    if (C == 64) return go(IC<64>{}, IC<2>{}, IC<1>{}, IC<1>{});
-    if (C == 128) return go(IC<128>{}, IC<1>{}, IC<1>{}, IC<1>{});
-    return go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{});
+    // (WGN, CB) per C, measured (tools/layer_bench.py unit_*): C=256 with one
+    // column block per wave 19.6 -> 14.4 us; C=128 11.6 -> 11.3 us
+    if (C == 64) return go(IC<64>{}, IC<2>{}, IC<1>{}, IC<1>{}, IC<2>{});
+    if (C == 128) return go(IC<128>{}, IC<2>{}, IC<1>{}, IC<1>{}, IC<1>{});
+    if (C == 256) return go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{});
+    return go(IC<512>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{});
 }
 }  // namespace rave

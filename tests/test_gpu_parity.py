@@ -585,7 +585,7 @@ def test_residual_unit_kernel(N, dev, case, precision):
     assert maxabs(got, ref) <= 2e-5 * max(1.0, float(np.abs(ref).max()))
 
 
-@pytest.mark.parametrize("precision,n_fused", [("f32", 22), ("split16", 18), ("auto", 22)])
+@pytest.mark.parametrize("precision,n_fused", [("f32", 22), ("split16", 22), ("auto", 22)])
 def test_fused_units_match_unfused_model(dev, precision, n_fused):
     """The v2 plan with fused residual units equals the conv-by-conv plan."""
     from rave_amd import config as rcfg
