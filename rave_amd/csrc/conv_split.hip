@@ -167,7 +167,9 @@ template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 
     static_assert(XPLANE % 16 == 0 && STAGE % 16 == 0, "16-byte LDS alignment");
     static_assert((NI * NJ == 4 || NI * NJ == 2) && NW >= 1 && NW <= 8, "tile");
     static_assert(KG == 1 || (KG == 2 && KS1 >= 1), "K-groups");
-    static_assert(WR + XI <= 63, "vmcnt range");
+    // a configuration is built only if its hand-counted waits fit the vmcnt
+    // field and its LDS fits the CU
+    static constexpr bool VALID = WR + XI <= 63 && LDS_ALL <= 160 * 1024;
 };
 
 template <int V> struct IC {
@@ -746,8 +748,7 @@ static bool split_tile_fits(int idx) {   // both DMA variants must fit
     return with_tile(idx, [](auto bm, auto bn, auto wm, auto kg, auto wn) {
         constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
                       KG = decltype(kg)::value, WN = decltype(wn)::value;
-        return SGeo<KT, BM, BN, WM, true, KG, WN>::LDS_ALL <= 160 * 1024 &&
-               SGeo<KT, BM, BN, WM, false, KG, WN>::LDS_ALL <= 160 * 1024;
+        return SGeo<KT, BM, BN, WM, true, KG, WN>::VALID && SGeo<KT, BM, BN, WM, false, KG, WN>::VALID;
     });
 }
 static bool split_fits(int taps, int idx) {
@@ -793,8 +794,8 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
 template <int KT, int BM, int BN, int WM, int KG, int WN, bool XV>
 static int split_launch_xv(ConvKArgs k, hipStream_t st) {
     using G = SGeo<KT, BM, BN, WM, XV, KG, WN>;
-    if constexpr (G::LDS_ALL > 160 * 1024) {
-        set_error("conv1d(split16): tile exceeds LDS");
+    if constexpr (!G::VALID) {
+        set_error("conv1d(split16): tile exceeds LDS or the vmcnt range");
         return RAVE_ERR_UNSUPPORTED;
     } else {
     if (k.XW > G::XW_MAX) {
