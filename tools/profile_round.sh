@@ -32,7 +32,7 @@ KT=$(find "$OUT/kt" -name '*kernel_trace.csv' | head -n 1)
 FE=$(find "$OUT/fetch" -name '*counter_collection.csv' | head -n 1)
 WR=$(find "$OUT/write" -name '*counter_collection.csv' | head -n 1)
 python3 "$R/tools/rocprof_summary.py" --trace "$KT" --fetch "$FE" --write "$WR" \
-    --bench "$OUT/bench_kt.json" --out "$OUT/summary.json" --traffic-out "$OUT/traffic.json" \
+    --bench "$OUT/bench.json" --out "$OUT/summary.json" --traffic-out "$OUT/traffic.json" \
     --precision auto
 find "$OUT" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
 # counter CSVs are large; keep the GEMM-family rows only
