@@ -320,14 +320,16 @@ def test_v2_full_clip_vs_oracle(dev, precision):
     assert ey < TOL
 
 
-def test_batch_independence_and_determinism(dev):
-    """At BASELINE config 2 size (16 x 65536): each clip of the batch equals the
-    same clip run alone (no cross-sample coupling), and reruns are bitwise equal."""
+@pytest.mark.parametrize("precision", ["f32", "auto"])
+def test_batch_independence_and_determinism(dev, precision):
+    """At BASELINE config 2 size (16 x 65536), in the bench's precision mode too:
+    each clip of the batch equals the same clip run alone (no cross-sample
+    coupling), and reruns are bitwise equal."""
     from rave_amd import config as rcfg
     from rave_amd.model import RAVE
     from rave_amd.weights import init_params, init_speaker
     cfg = rcfg.v2()
-    m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev)
+    m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=precision)
     g = torch.Generator(device="cpu").manual_seed(0)
     x = (0.1 * torch.randn(16, 1, 65536, generator=g)).to(dev)
     y1 = m.forward(x)
@@ -340,14 +342,15 @@ def test_batch_independence_and_determinism(dev):
 
 
 # ------------------------------------------------------------------ streaming (BASELINE config 3)
-def test_causal_streaming_golden(dev, golden):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_causal_streaming_golden(dev, golden, precision):
     """Block streaming (2048-sample blocks, persistent caches) reproduces the
     reference's cached_conv streaming outputs block for block."""
     from rave_amd import config as rcfg
     from rave_amd.streaming import StreamingRAVE
     cfg = rcfg.causal()
     g = golden("causal_stream")
-    m = _model(cfg, g, dev, golden)
+    m = _model(cfg, g, dev, golden, precision)
     blk = int(g["block"])
     s = StreamingRAVE(m, batch=1, block=blk)
     x = torch.from_numpy(g["x"]).to(dev)
@@ -389,13 +392,14 @@ def test_streaming_matches_oneshot_long(dev):
 
 
 # ------------------------------------------------------------------ v3 noise / AdaIN (BASELINE config 5)
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name,capacity", [("v3_noise", None), ("v3_noise_small_layers", 8)])
-def test_v3_noise_golden(dev, golden, name, capacity):
+def test_v3_noise_golden(dev, golden, name, capacity, precision):
     """Snake + NoiseGeneratorV2 decode with the reference's injected uniform noise."""
     from rave_amd import config as rcfg
     cfg = rcfg.v3_noise() if capacity is None else rcfg.v3_noise(capacity=capacity)
     g = golden(name)
-    m = _model(cfg, g, dev, golden)
+    m = _model(cfg, g, dev, golden, precision)
     x = torch.from_numpy(g["x"]).to(dev)
     u = torch.from_numpy(g["noise_u"]).to(dev)
     if "z" in g:
@@ -458,14 +462,15 @@ def test_v3_noise_decode_c5_shard_vs_oracle(dev):
     assert torch.isfinite(y_rand).all() and float(d.max()) < 0.05   # noise is a small additive term
 
 
-def test_adain_style_transfer_golden(dev, golden):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_adain_style_transfer_golden(dev, golden, precision):
     """learn_y -> learn_x -> transfer -> learn_x(bs=1) against the reference's
     AdaIN run, including the device-resident buffers and counters."""
     from rave_amd import config as rcfg
     from tests.test_oracle_golden import adain_sequence
     for name, cfg in [("v3_adain_small", rcfg.v3(capacity=8)), ("v3_adain", rcfg.v3())]:
         g = golden(name)
-        m = _model(cfg, g, dev, golden)
+        m = _model(cfg, g, dev, golden, precision)
         assert not m.adain.active
         for i, (tag, lx, ly, x) in enumerate(adain_sequence(g)):
             m.adain.set_learn(lx, ly)
