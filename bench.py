@@ -47,6 +47,8 @@ FAMILIES = {
                      PEAK_SPLIT16_TFLOPS),
     "unit_f32": ("residual_unit_kernel, fp32 MFMA 32x32x2", PEAK_FP32_TFLOPS),
     "unit_split16": ("unit_split_kernel, split-f16 MFMA 32x32x16 (3 per fp32 MAC)", PEAK_SPLIT16_TFLOPS),
+    "stack_split16": ("stack_split_kernel (3 residual units per launch), split-f16 MFMA 32x32x16",
+                      PEAK_SPLIT16_TFLOPS),
     "pqmf_analysis": ("pqmf_analysis_kernel, fp32 MFMA 16x16x4", PEAK_FP32_TFLOPS),
     "pqmf_synthesis": ("pqmf_synthesis_kernel, fp32 MFMA 16x16x4", PEAK_FP32_TFLOPS),
 }
@@ -59,6 +61,8 @@ def op_family(kind: int, scalars: dict) -> str:
         return "conv_" + prec
     if kind == N.OP_UNIT:
         return "unit_" + prec
+    if kind == N.OP_STACK:
+        return "stack_split16"
     if kind == N.OP_PQMF_ANALYSIS:
         return "pqmf_analysis"
     if kind == N.OP_PQMF_SYNTHESIS:

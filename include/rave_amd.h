@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 5
+#define RAVE_ABI_VERSION 6
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 
@@ -305,6 +305,31 @@ int64_t rave_unit_split_packed_size(int channels);
 int rave_unit_split_pack_weight(const float* w1, const float* w2, int channels, float* packed);
 int rave_residual_unit(const rave_unit_args* a, void* stream);
 
+/* ---------------------------------------------------------------- residual stack
+ * RAVE_STACK_UNITS consecutive Residual(DilatedUnit)s of one width (an
+ * EncoderV2 / GeneratorV2 residual stack, rave/blocks.py:533-558, 647-664,
+ * dilations e.g. 1, 3, 9) in one launch, split-f16 arithmetic: the input is
+ * read once, the intermediate unit outputs stay on chip (a tile recomputes a
+ * 32-column margin on each side), the stack output is written once.
+ * y[:, :, t] = U3(U2(U1(x)))[:, :, t]; weights are rave_unit_split_pack_weight
+ * images.  C in {64, 128}; dilation <= 16, pad_left <= 2*dilation.  x and y
+ * must not overlap.  Other shapes return RAVE_ERR_UNSUPPORTED. */
+#define RAVE_STACK_UNITS 3
+typedef struct rave_stack_args {
+    int32_t channels, batch, t_len, act;
+    float leaky_slope; int32_t _pad0;
+    int32_t dilation[RAVE_STACK_UNITS], pad_left[RAVE_STACK_UNITS];
+    const float* x; int64_t x_sb, x_sc;
+    float* y;       int64_t y_sb, y_sc;
+    const float* weight[RAVE_STACK_UNITS];
+    const float* bias1[RAVE_STACK_UNITS];
+    const float* bias2[RAVE_STACK_UNITS];
+    const float* alpha0[RAVE_STACK_UNITS];
+    const float* alpha2[RAVE_STACK_UNITS];
+} rave_stack_args;
+int rave_stack_supported(int channels);
+int rave_residual_stack(const rave_stack_args* a, void* stream);
+
 /* ---------------------------------------------------------------- plans
  * A plan is a recorded sequence of the ops above (the module graph of
  * RAVE.encode/decode).  Pointer fields inside an op's args may be relocated at
@@ -323,7 +348,8 @@ enum {
     RAVE_OP_COPY = 8,
     RAVE_OP_NOISE = 9,
     RAVE_OP_ADAIN = 10,
-    RAVE_OP_UNIT = 11
+    RAVE_OP_UNIT = 11,
+    RAVE_OP_STACK = 12
 };
 
 #define RAVE_OP_PAYLOAD 240
@@ -340,6 +366,7 @@ typedef struct rave_plan_op {
         rave_noise_args noise;
         rave_adain_args adain;
         rave_unit_args unit;
+        rave_stack_args stack;
         unsigned char raw[RAVE_OP_PAYLOAD];
     } u;
 } rave_plan_op;

@@ -35,7 +35,8 @@ OP_COPY = 8
 OP_NOISE = 9
 OP_ADAIN = 10
 OP_UNIT = 11
-ABI_VERSION = 5
+OP_STACK = 12
+ABI_VERSION = 6
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 
 # GEMM arithmetic of conv / unit ops (include/rave_amd.h RAVE_PREC_*)
@@ -124,6 +125,19 @@ class UnitArgs(C.Structure):
                 ("weight", vp), ("bias1", vp), ("bias2", vp), ("alpha0", vp), ("alpha2", vp)]
 
 
+STACK_UNITS = 3
+
+
+class StackArgs(C.Structure):
+    _fields_ = ([("channels", i32), ("batch", i32), ("t_len", i32), ("act", i32),
+                 ("leaky_slope", f32), ("_pad0", i32)]
+                + [(f"dilation{u}", i32) for u in range(STACK_UNITS)]
+                + [(f"pad_left{u}", i32) for u in range(STACK_UNITS)]
+                + [("x", vp), ("x_sb", i64), ("x_sc", i64), ("y", vp), ("y_sb", i64), ("y_sc", i64)]
+                + [(f"{f}{u}", vp) for f in ("weight", "bias1", "bias2", "alpha0", "alpha2")
+                   for u in range(STACK_UNITS)])
+
+
 PAYLOAD = 240
 
 
@@ -137,7 +151,7 @@ class Reloc(C.Structure):
 
 
 STRUCTS = [ConvArgs, AnalysisArgs, SynthesisArgs, FillArgs, RvqArgs, ShiftArgs, PlanOp, Reloc,
-           CopyArgs, NoiseArgs, AdainArgs, UnitArgs]
+           CopyArgs, NoiseArgs, AdainArgs, UnitArgs, StackArgs]
 
 # every exported symbol of include/rave_amd.h
 EXPORTS = [
@@ -148,6 +162,7 @@ EXPORTS = [
     "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
     "rave_unit_packed_size", "rave_unit_pack_weight", "rave_residual_unit",
     "rave_unit_split_packed_size", "rave_unit_split_pack_weight",
+    "rave_stack_supported", "rave_residual_stack",
     "rave_plan_create", "rave_plan_run", "rave_plan_destroy", "rave_plan_size",
     "rave_plan_profile", "rave_plan_op_times",
 ]
@@ -179,6 +194,7 @@ def _load():
     lib.rave_unit_packed_size.restype = i64
     lib.rave_unit_pack_weight.argtypes = [vp, vp, C.c_int, vp]
     lib.rave_unit_split_packed_size.argtypes = [C.c_int]
+    lib.rave_stack_supported.argtypes = [C.c_int]
     lib.rave_unit_split_packed_size.restype = i64
     lib.rave_unit_split_pack_weight.argtypes = [vp, vp, C.c_int, vp]
     lib.rave_conv1d_workspace.restype = i64
@@ -187,7 +203,7 @@ def _load():
                      ("rave_rvq_encode", RvqArgs), ("rave_rvq_decode", RvqArgs),
                      ("rave_shift_history", ShiftArgs), ("rave_copy", CopyArgs),
                      ("rave_noise_synth", NoiseArgs), ("rave_adain", AdainArgs),
-                     ("rave_residual_unit", UnitArgs)]:
+                     ("rave_residual_unit", UnitArgs), ("rave_residual_stack", StackArgs)]:
         getattr(lib, name).argtypes = [C.POINTER(st), vp]
     lib.rave_plan_create.argtypes = [C.POINTER(PlanOp), C.c_int, C.POINTER(Reloc), C.c_int,
                                      C.POINTER(vp)]
@@ -257,6 +273,11 @@ def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed, out_s
     check(pack_fn(w.ctypes.data, c_in, c_out, kernel, stride, dilation,
                   int(transposed), int(out_shift), out.ctypes.data), "pack_weight")
     return out
+
+
+def stack_supported(channels: int) -> bool:
+    """Fused split-f16 residual stack (rave_residual_stack) available at this width."""
+    return bool(lib.rave_stack_supported(int(channels)))
 
 
 def unit_supported(channels: int, precision: int = PREC_F32) -> bool:

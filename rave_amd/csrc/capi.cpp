@@ -36,6 +36,7 @@ extern "C" int rave_struct_sizes(int64_t* out, int n) {
         (int64_t)sizeof(rave_plan_op),           (int64_t)sizeof(rave_reloc),
         (int64_t)sizeof(rave_copy_args),         (int64_t)sizeof(rave_noise_args),
         (int64_t)sizeof(rave_adain_args),        (int64_t)sizeof(rave_unit_args),
+        (int64_t)sizeof(rave_stack_args),
     };
     const int cnt = (int)(sizeof(sizes) / sizeof(sizes[0]));
     if (!out) return cnt;
@@ -153,6 +154,7 @@ extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, v
             case RAVE_OP_NOISE: rc = rave_noise_synth(&op.u.noise, stream); break;
             case RAVE_OP_ADAIN: rc = rave_adain(&op.u.adain, stream); break;
             case RAVE_OP_UNIT: rc = rave_residual_unit(&op.u.unit, stream); break;
+            case RAVE_OP_STACK: rc = rave_residual_stack(&op.u.stack, stream); break;
             default:
                 rave::set_error("plan_run: unknown op kind " + std::to_string(op.kind));
                 return RAVE_ERR_STATE;

@@ -1,0 +1,411 @@
+// Fused residual stack on the f16 matrix cores (split-f16 arithmetic, as
+// unit_split.hip): RAVE_STACK_UNITS consecutive Residual(DilatedUnit)s of one
+// width -- the residual stacks of EncoderV2 (rave/blocks.py:533-558) and
+// GeneratorV2 (rave/blocks.py:647-664), each unit
+//
+//     y_u = y_{u-1} + conv1x1_u(act2_u(conv3_{d_u}(act0_u(y_{u-1})) + b1_u)) + b2_u
+//
+// (rave/blocks.py:32-46, 84-113) -- in one launch.
+//
+// A workgroup owns BN output columns of one batch item and computes every unit
+// over an extended range of BN + 64 columns (one 32-column block of margin per
+// side).  The input window is read from HBM once; between units the running
+// sum y stays in registers (each wave keeps its own 32 rows x 32*CB columns for
+// the whole stack) and act0(y) goes back into the LDS planes.  Margin columns
+// go stale unit by unit (their windows reach past the staged rows), but the
+// receptive field of the centre columns stays inside the margin as long as
+// pad_2 + pad_3 <= 32 and (2 d_2 - pad_2) + (2 d_3 - pad_3) <= 32 (host check).
+// Sequence-boundary zero padding: planes hold 0 at columns outside [0, T).
+#include "common.h"
+
+#include <algorithm>
+
+namespace rave {
+
+typedef _Float16 ss_h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 ss_h4 __attribute__((ext_vector_type(4)));
+typedef float ss_f32x8 __attribute__((ext_vector_type(8)));
+typedef float ss_f32x4 __attribute__((ext_vector_type(4)));
+typedef float ss_f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kSSUnits = RAVE_STACK_UNITS;
+constexpr unsigned kSSOOB = 0xFFFFFFF0u;
+
+struct SSArgs {
+    const float* x; float* y;
+    const float* w[kSSUnits];
+    const float* rs1[kSSUnits]; const float* rs2[kSSUnits];
+    const float* b1[kSSUnits]; const float* b2[kSSUnits];
+    const float* a0[kSSUnits]; const float* a2[kSSUnits];
+    int64_t x_sb, x_sc, y_sb, y_sc;
+    int T, ntiles, act, x_bytes, y_bytes, w_bytes, has_bias;
+    int d[kSSUnits], pad[kSSUnits];
+    float slope;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ss_rsrc(const void* p, int bytes) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const uint64_t u = ((uint64_t)hi << 32) | lo;
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(u), (short)0,
+                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+template <bool SNAKE>
+__device__ __forceinline__ float ss_act(float v, float slope, float alpha) {
+    if constexpr (SNAKE) {
+        const float r = 1.0f / (alpha + 1e-9f);
+        return v + r * sin_squared(alpha * v);
+    } else {
+        return v > 0.f ? v : v * slope;     // slope 1 == no activation
+    }
+}
+
+// C channels (C/32 waves along rows, one 32-row block each); NB centre blocks
+// of 32 columns + 2 margin blocks, CB blocks per wave.
+template <int C, int NB, int CB> struct SSGeo {
+    static constexpr int WGM = C / 32, NBX = NB + 2, WGN = NBX / CB, NW = WGM * WGN, NT = 64 * NW;
+    static constexpr int BN = 32 * NB;
+    static constexpr int OFF = 32;                     // plane row of extended column 0
+    static constexpr int XR = NBX * 32 + 64;           // plane rows: extended range + 32 each side
+    static constexpr int PH = C + 8;                   // halves per row (conflict-free b128 reads)
+    static constexpr int PLANE = XR * PH;              // halves per plane
+    static constexpr int S1 = 3 * C / 16, S2 = C / 16, ST = S1 + S2, CG = C / 16;
+    static constexpr int R = 4;                        // weight ring depth (K-steps); divides ST
+    static constexpr int G8 = C / 8;
+    static constexpr int XT = (XR * G8 + NT - 1) / NT; // window staging tasks per thread
+    static constexpr int TAB = kSSUnits * 6 * C;       // per unit: rs1 b1 a2 rs2 b2 a0
+    static constexpr int LDS = 2 * PLANE * 2 + TAB * 4;
+    static_assert(NBX % CB == 0 && ST % R == 0 && NT <= 1024, "geometry");
+};
+
+template <int C, int NB, int CB, bool SNAKE>
+__global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_kernel(SSArgs a) {
+    using G = SSGeo<C, NB, CB>;
+    constexpr int NT = G::NT, PH = G::PH, XR = G::XR, G8 = G::G8, XT = G::XT, R = G::R;
+    constexpr int S1 = G::S1, ST = G::ST, CG = G::CG, OFF = G::OFF;
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    _Float16* ph = reinterpret_cast<_Float16*>(lds);
+    _Float16* pl = ph + G::PLANE;
+    float* tab = reinterpret_cast<float*>(lds + 4 * G::PLANE);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % G::WGM, wn = wave / G::WGM;
+    const int hh = lane >> 5, l32 = lane & 31;
+    const int b = blockIdx.x / a.ntiles;
+    const int n0 = (blockIdx.x - b * a.ntiles) * G::BN;
+    const int ext0 = n0 - 32;                       // absolute column of extended column 0
+    const int r0 = ext0 - OFF;                      // absolute column of plane row 0
+    const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
+    const auto xrs = ss_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);
+
+    // ------------------------------------------------------------ per-unit row tables -> LDS
+#pragma unroll
+    for (int u = 0; u < kSSUnits; ++u) {
+        for (int i = tid; i < 6 * C; i += NT) {
+            const int k = i / C, m = i - k * C;
+            const float* src = k == 0 ? a.rs1[u] : k == 1 ? a.b1[u] : k == 2 ? a.a2[u]
+                             : k == 3 ? a.rs2[u] : k == 4 ? a.b2[u] : a.a0[u];
+            const bool has = (k == 1 || k == 4) ? a.has_bias != 0 : (k == 2 || k == 5) ? SNAKE : true;
+            tab[u * 6 * C + i] = has ? src[m] : 0.f;
+        }
+    }
+
+    // ------------------------------------------------------------ weight ring (crosses units)
+    ss_h8 ring[R][2];
+    const unsigned abase = (unsigned)(wm * ST * 2) * 1024u + (unsigned)lane * 16u;
+    auto wrs_of = [&](int u) __attribute__((always_inline)) {
+        const float* w = u == 0 ? a.w[0] : u == 1 ? a.w[1] : a.w[2];
+        return ss_rsrc(w, u < kSSUnits ? a.w_bytes : 0);
+    };
+    // step s of the current unit; s >= ST: step s - ST of the next unit
+    auto load_a = [&](int slot, __amdgpu_buffer_rsrc_t cur, __amdgpu_buffer_rsrc_t nxt, int s)
+        __attribute__((always_inline)) {
+        const bool here = s < ST;
+        const int ss = here ? s : s - ST;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+            ring[slot][p] = __builtin_bit_cast(ss_h8, __builtin_amdgcn_raw_buffer_load_b128(
+                here ? cur : nxt, abase + (unsigned)((ss * 2 + p) * 1024), 0, 0));
+    };
+    {
+        const auto w0 = wrs_of(0), w1 = wrs_of(1);
+#pragma unroll
+        for (int s = 0; s < R; ++s) load_a(s, w0, w1, s);
+    }
+    __syncthreads();                                   // tables visible
+
+    // ------------------------------------------------------------ unit 0 input window
+    {
+        float rx[XT][8];
+#pragma unroll
+        for (int i = 0; i < XT; ++i) {
+            const int e = tid + i * NT;
+            const int g = e / XR, w = e - g * XR;
+            const int t = min(max(r0 + w, 0), a.T - 1);
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                const int c = min(g * 8 + v, C - 1);
+                rx[i][v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                    xrs, (unsigned)(c * a.x_sc + t) * 4u, 0, 0));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < XT; ++i) {
+            const int e = tid + i * NT;
+            const int g = e / XR, w = e - g * XR;
+            const bool ok = (e < XR * G8) && (r0 + w >= 0) && (r0 + w < a.T);
+            ss_f32x8 v8;
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                const float al = SNAKE ? tab[5 * C + min(g * 8 + v, C - 1)] : 0.f;
+                v8[v] = ok ? ss_act<SNAKE>(rx[i][v], slope, al) : 0.f;
+            }
+            const ss_h8 hi = __builtin_convertvector(v8, ss_h8);
+            const ss_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, ss_f32x8)) * 2048.0f, ss_h8);
+            if (e < XR * G8) {
+                *reinterpret_cast<ss_h8*>(ph + w * PH + g * 8) = hi;
+                *reinterpret_cast<ss_h8*>(pl + w * PH + g * 8) = lo;
+            }
+        }
+    }
+
+    // running sum y (fp32): lane column col0 + 32j, rows mrow0 + 8(r>>2) + (r&3)
+    const int col0 = wn * 32 * CB + l32;               // extended column of this lane
+    const int mrow0 = 32 * wm + 4 * hh;
+    float yv[CB][16];
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+        const int t = ext0 + col0 + 32 * j;
+        const bool ok = t >= 0 && t < a.T;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = mrow0 + 8 * (r >> 2) + (r & 3);
+            yv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                xrs, ok ? (unsigned)(m * a.x_sc + t) * 4u : kSSOOB, 0, 0));
+        }
+    }
+    __syncthreads();
+
+    struct BF {
+        ss_h8 h[CB], l[CB];
+    };
+    auto read_b = [&](int row, int ch, BF& f) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < CB; ++j) {
+            const int off = (row + j * 32) * PH + ch + 8 * hh;
+            f.h[j] = *reinterpret_cast<const ss_h8*>(ph + off);
+            f.l[j] = *reinterpret_cast<const ss_h8*>(pl + off);
+        }
+    };
+    ss_f32x16 acc[CB];
+    auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < CB; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    };
+    zero_acc();
+    // act(v) -> (hi, lo) planes at extended column col0 + 32j (zero outside [0, T) if mask)
+    auto write_planes = [&](const float (*v)[16], const float* al_tab, bool mask)
+        __attribute__((always_inline)) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int m = mrow0 + 8 * g;
+            ss_f32x4 al = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (SNAKE) al = *reinterpret_cast<const ss_f32x4*>(al_tab + m);
+#pragma unroll
+            for (int j = 0; j < CB; ++j) {
+                const int t = ext0 + col0 + 32 * j;
+                const bool ok = !mask || (t >= 0 && t < a.T);
+                ss_f32x4 w4;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) w4[e] = ok ? ss_act<SNAKE>(v[j][4 * g + e], slope, al[e]) : 0.f;
+                const ss_h4 hv = __builtin_convertvector(w4, ss_h4);
+                const ss_h4 lv = __builtin_convertvector((w4 - __builtin_convertvector(hv, ss_f32x4)) * 2048.0f, ss_h4);
+                *reinterpret_cast<ss_h4*>(ph + (OFF + col0 + 32 * j) * PH + m) = hv;
+                *reinterpret_cast<ss_h4*>(pl + (OFF + col0 + 32 * j) * PH + m) = lv;
+            }
+        }
+    };
+
+#pragma unroll 1
+    for (int u = 0; u < kSSUnits; ++u) {
+        const auto wcur = wrs_of(u), wnxt = wrs_of(u + 1);
+        const float* tu = tab + u * 6 * C;
+        const int du = u == 0 ? a.d[0] : u == 1 ? a.d[1] : a.d[2];
+        const int pu = u == 0 ? a.pad[0] : u == 1 ? a.pad[1] : a.pad[2];
+        auto step = [&](int s, const BF& f) __attribute__((always_inline)) {
+            const ss_h8 ah = ring[s % R][0], al = ring[s % R][1];
+            const ss_h8 a2 = ah * (_Float16)2048.0f;
+            load_a(s % R, wcur, wnxt, s + R);            // refill (runs on into the next unit)
+#pragma unroll
+            for (int j = 0; j < CB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2, f.h[j], acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < CB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f.l[j], acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < CB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f.h[j], acc[j], 0, 0, 0);
+        };
+        // phase 1: h = W1 . window (taps at row shifts q*d - pad)
+        {
+            const int rowb = OFF - pu + col0;
+            BF f[2];
+            read_b(rowb, 8 * 0, f[0]);
+#pragma unroll
+            for (int s = 0; s < S1; ++s) {
+                if (s + 1 < S1) {
+                    const int tap = (s + 1) / CG;
+                    read_b(rowb + tap * du, ((s + 1) - tap * CG) * 16, f[(s + 1) & 1]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                step(s, f[s & 1]);
+            }
+        }
+        __syncthreads();                               // window dead
+        // seam: h = act2(h * rs1 + b1) -> planes
+        {
+            float hv[CB][16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int m = mrow0 + 8 * g;
+                const ss_f32x4 rs = *reinterpret_cast<const ss_f32x4*>(tu + m);
+                const ss_f32x4 bb = *reinterpret_cast<const ss_f32x4*>(tu + C + m);
+#pragma unroll
+                for (int j = 0; j < CB; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) hv[j][4 * g + e] = acc[j][4 * g + e] * rs[e] + bb[e];
+            }
+            write_planes(hv, tu + 2 * C, false);
+            zero_acc();
+        }
+        __syncthreads();
+        // phase 2: y += W2 . h
+        {
+            BF f[2];
+            read_b(OFF + col0, 0, f[0]);
+#pragma unroll
+            for (int s = S1; s < ST; ++s) {
+                if (s + 1 < ST) read_b(OFF + col0, (s + 1 - S1) * 16, f[(s + 1 - S1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+                step(s, f[(s - S1) & 1]);
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int m = mrow0 + 8 * g;
+            const ss_f32x4 rs = *reinterpret_cast<const ss_f32x4*>(tu + 3 * C + m);
+            const ss_f32x4 bb = *reinterpret_cast<const ss_f32x4*>(tu + 4 * C + m);
+#pragma unroll
+            for (int j = 0; j < CB; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    yv[j][4 * g + e] = acc[j][4 * g + e] * rs[e] + bb[e] + yv[j][4 * g + e];
+        }
+        zero_acc();
+        if (u + 1 < kSSUnits) {
+            __syncthreads();                           // h dead
+            write_planes(yv, tu + 6 * C + 5 * C, true);    // next unit's act0(y)
+            __syncthreads();
+        }
+    }
+
+    // ------------------------------------------------------------ centre blocks -> y
+    const auto yrs = ss_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+        const int blk = wn * CB + j;                   // extended block: 1..NB are the centre
+        const int t = ext0 + col0 + 32 * j;
+        const bool ok = blk >= 1 && blk <= NB && t < a.T;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = mrow0 + 8 * (r >> 2) + (r & 3);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, yv[j][r]), yrs,
+                                                  ok ? (unsigned)(m * a.y_sc + t) * 4u : kSSOOB, 0, 0);
+        }
+    }
+}
+
+template <int C, int NB, int CB>
+static int ss_launch(const SSArgs& k0, int B, bool snake, hipStream_t st) {
+    using G = SSGeo<C, NB, CB>;
+    SSArgs k = k0;
+    k.ntiles = ceil_div(k.T, G::BN);
+    auto kern = snake ? stack_split_kernel<C, NB, CB, true> : stack_split_kernel<C, NB, CB, false>;
+    static bool attr[2] = {false, false};
+    if (G::LDS > 65536 && !attr[snake]) {
+        RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr[snake] = true;
+    }
+    static_assert(G::LDS <= 160 * 1024, "LDS budget");
+    launch(kern, dim3(k.ntiles * B), dim3(G::NT), (uint32_t)G::LDS, st, k);
+    return launch_status("stack_split_kernel");
+}
+
+}  // namespace rave
+
+using namespace rave;
+
+extern "C" int rave_stack_supported(int channels) { return channels == 64 || channels == 128; }
+
+extern "C" int rave_residual_stack(const rave_stack_args* p, void* stream) {
+    RAVE_CHECK_ARG(p, "residual_stack: null args");
+    const int C = p->channels;
+    if (!rave_stack_supported(C)) {
+        set_error("residual_stack: C in {64, 128}");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    RAVE_CHECK_ARG(p->x && p->y && p->batch > 0 && p->t_len > 0, "residual_stack: empty shape or null tensor");
+    RAVE_CHECK_ARG(p->act == RAVE_ACT_LEAKY || p->act == RAVE_ACT_SNAKE || p->act == RAVE_ACT_NONE,
+                   "residual_stack: unknown activation");
+    const bool snake = p->act == RAVE_ACT_SNAKE;
+    const bool has_bias = p->bias1[0] != nullptr;
+    int reach_l = 0, reach_r = 0;
+    for (int u = 0; u < kSSUnits; ++u) {
+        const int d = p->dilation[u], pl = p->pad_left[u];
+        RAVE_CHECK_ARG(p->weight[u], "residual_stack: null weight");
+        RAVE_CHECK_ARG(d >= 1 && d <= 16 && pl >= 0 && pl <= 2 * d, "residual_stack: dilation / padding out of range");
+        RAVE_CHECK_ARG((p->bias1[u] != nullptr) == has_bias && (p->bias2[u] != nullptr) == has_bias,
+                       "residual_stack: biases on every unit or on none");
+        RAVE_CHECK_ARG(!snake || (p->alpha0[u] && p->alpha2[u]), "residual_stack: snake needs alphas");
+        if (u > 0) {
+            reach_l += pl;
+            reach_r += 2 * d - pl;
+        }
+    }
+    if (reach_l > 32 || reach_r > 32) {
+        set_error("residual_stack: units 2..3 reach past the 32-column margin (run the units separately)");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    const int64_t xb = ((int64_t)(C - 1) * p->x_sc + p->t_len) * 4;
+    const int64_t yb = ((int64_t)(C - 1) * p->y_sc + p->t_len) * 4;
+    RAVE_CHECK_ARG(xb < (1ll << 31) && yb < (1ll << 31), "residual_stack: tensors beyond 2 GiB per item");
+    SSArgs k{};
+    k.x = p->x; k.y = p->y;
+    const int64_t frag = (int64_t)(C / 32) * (4 * C / 16) * 2 * 256;   // rave_unit_split_pack_weight
+    for (int u = 0; u < kSSUnits; ++u) {
+        k.w[u] = p->weight[u];
+        k.rs1[u] = p->weight[u] + frag;
+        k.rs2[u] = p->weight[u] + frag + C;
+        k.b1[u] = has_bias ? p->bias1[u] : p->weight[u];
+        k.b2[u] = has_bias ? p->bias2[u] : p->weight[u];
+        k.a0[u] = snake ? p->alpha0[u] : p->weight[u];
+        k.a2[u] = snake ? p->alpha2[u] : p->weight[u];
+        k.d[u] = p->dilation[u];
+        k.pad[u] = p->pad_left[u];
+    }
+    k.x_sb = p->x_sb; k.x_sc = p->x_sc; k.y_sb = p->y_sb; k.y_sc = p->y_sc;
+    k.T = p->t_len; k.act = p->act; k.slope = p->leaky_slope;
+    k.x_bytes = (int)xb; k.y_bytes = (int)yb; k.w_bytes = (int)(frag * 4);
+    k.has_bias = has_bias;
+    hipStream_t st = as_stream(stream);
+    // geometry measured with tools/stack_bench.py (v2 sizes, B = 16): C = 64 with
+    // 8 centre blocks, 5 blocks per wave (2 column waves share each weight row
+    // block): 40.0 us against 46.5 us for the three unit launches; C = 128 (2
+    // centre blocks, 2 per wave) 43.6 against 43.1 -- the autotuner keeps the units
+    if (C == 64) return ss_launch<64, 8, 5>(k, p->batch, snake, st);
+    return ss_launch<128, 2, 2>(k, p->batch, snake, st);
+}

@@ -505,7 +505,8 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
     };
     // (K-groups, KG = 2, measured slower for every C: 13.3/11.6/19.5 -> 16.8/12.0/21.5 us)
     // (WGN, CB) per C, measured (tools/layer_bench.py unit_*): C=256 with one
-    // column block per wave 19.6 -> 14.4 us; C=128 11.6 -> 11.3 us
+    // column block per wave 19.6 -> 14.4 us; C=128 11.6 -> 11.3 us; wider waves
+    // (CB 3-4, one column wave) measured slower for C=64 and C=128
     if (C == 64) return go(IC<64>{}, IC<2>{}, IC<1>{}, IC<1>{}, IC<2>{});
     if (C == 128) return go(IC<128>{}, IC<2>{}, IC<1>{}, IC<1>{}, IC<1>{});
     if (C == 256) return go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{});

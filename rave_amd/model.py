@@ -391,6 +391,85 @@ class RAVE:
             self._tuned[key] = (fused_ms <= split_ms, min(fused_ms, split_ms))
         return bool(self._tuned[key][0])
 
+    def _unit_best_ms(self, k3: ConvNode, k1: ConvNode, B: int, T: int) -> float:
+        """Measured time of a unit as the plan would run it (fused or two convs)."""
+        if len(self.precs) > 1:
+            self._fuse_unit(k3, k1, B, T, View("t", 0, k3.c_in * T, T))
+            return float(self._tuned[("fuse", k3.name, B, T)][1])
+        return self._unit_time(k3, k1, B, T)
+
+    def _stack_runs(self, nodes: List[ConvNode]) -> Dict[str, List[Tuple[ConvNode, ConvNode]]]:
+        """Runs of N.STACK_UNITS consecutive Residual(DilatedUnit)s of one width
+        (the residual stacks of EncoderV2 / GeneratorV2, rave/blocks.py:533-558,
+        647-664) that rave_residual_stack can run: first k=3 node name -> units."""
+        pairs, out, i, U = self._unit_pairs(nodes), {}, 0, N.STACK_UNITS
+        adain_on = self.adain is not None and self.adain.active
+        while i + U <= len(pairs):
+            run = pairs[i:i + U]
+            a0 = run[0][0]
+            ok = (all(run[k + 1][0].src == run[k][1].dst for k in range(U - 1))
+                  and all(k3.c_in == a0.c_in and k3.act == a0.act and k3.bias == a0.bias for k3, _ in run)
+                  and N.stack_supported(a0.c_in)
+                  and all((k3.name, N.PREC_SPLIT16) in self.unit_pack for k3, _ in run)
+                  and not (adain_on and any(k3.adain for k3, _ in run)))
+            if ok:
+                out[a0.name] = run
+                i += U
+            else:
+                i += 1
+        return out
+
+    def _stack_parts(self, run: List[Tuple[ConvNode, ConvNode]], B: int, T: int):
+        """(scalars, pointer views, timing run) of one residual-stack op."""
+        arena = lambda o: View("arena", o, 0, 0) if o is not None else None  # noqa: E731
+        C_ = run[0][0].c_in
+        s = dict(channels=C_, batch=B, t_len=T, act=N.ACT[run[0][0].act], leaky_slope=self.cfg.leaky_slope)
+        p: Dict[str, Optional[View]] = {}
+        for u, (k3, k1) in enumerate(run):
+            _, b1, a0 = self.w_off[k3.name]
+            _, b2, a2 = self.w_off[k1.name]
+            s[f"dilation{u}"], s[f"pad_left{u}"] = k3.dilation, k3.pad[0]
+            p.update({f"weight{u}": arena(self.unit_pack[(k3.name, N.PREC_SPLIT16)]),
+                      f"bias1{u}": arena(b1), f"bias2{u}": arena(b2),
+                      f"alpha0{u}": arena(a0), f"alpha2{u}": arena(a2)})
+
+        def run_t():
+            args = N.StackArgs(**s, x_sb=C_ * T, x_sc=T, y_sb=C_ * T, y_sc=T)
+            keep: list = []
+            self._bind_scratch(args, dict(p, x=View("t", 0, 0, 0), y=View("t", 0, 0, 0)),
+                               {"x": (B, C_, T), "y": (B, C_, T)}, keep)
+            return self._time_native(N.lib.rave_residual_stack, args)
+
+        return s, p, run_t
+
+    def _use_stack(self, run: List[Tuple[ConvNode, ConvNode]], B: int, T: int) -> bool:
+        """One rave_residual_stack launch instead of the units: always in
+        split16-only mode, else when it measures faster than the units' best."""
+        if N.PREC_SPLIT16 not in self.precs:
+            return False
+        if len(self.precs) == 1 and not self.autotune:
+            return True
+        key = ("stack", run[0][0].name, B, T)
+        if key not in self._tuned:
+            try:
+                st_ms = self._stack_parts(run, B, T)[2]()
+            except (NotImplementedError, ValueError):
+                self._tuned[key] = (0, 0.0)
+                return False
+            units_ms = sum(self._unit_best_ms(k3, k1, B, T) for k3, k1 in run)
+            self._tuned[key] = (int(st_ms <= units_ms), min(st_ms, units_ms))
+        return bool(self._tuned[key][0])
+
+    def _stack(self, plan: Plan, run: List[Tuple[ConvNode, ConvNode]], B: int, T: int, src: View,
+               dst: View) -> None:
+        s, p, _ = self._stack_parts(run, B, T)
+        s.update(x_sb=src.sb, x_sc=src.sc, y_sb=dst.sb, y_sc=dst.sc)
+        C_ = run[0][0].c_in
+        plan.add(N.OP_STACK, N.StackArgs, s, dict(p, x=src, y=dst),
+                 label=run[0][0].name.rsplit(".net.", 2)[0] + ".stack",
+                 flops=2.0 * B * T * C_ * C_ * 4 * len(run),
+                 nbytes=4.0 * (2 * B * C_ * T + 4 * C_ * C_ * len(run)))
+
     def _unit_parts(self, k3: ConvNode, k1: ConvNode, B: int, T: int):
         """(descriptor builder, fused-kernel precisions, timing run) of one unit."""
         _, b1, a0 = self.w_off[k3.name]
@@ -557,6 +636,7 @@ class RAVE:
                 last_use[n.residual] = i
         tensors: Dict[str, Tuple[View, int, int]] = {k: (v, t, -1) for k, (v, t) in inputs.items()}
         fused = {a.name: b for a, b in self._unit_pairs(nodes) if a.name in self.unit_off}
+        stacks = self._stack_runs(nodes) if self.unit_off else {}
         skip = set()
         for i, n in enumerate(nodes):
             if n.name in skip:
@@ -564,6 +644,24 @@ class RAVE:
             src, t_in, _ = tensors[n.src]
             if n.adain and self.adain is not None and self.adain.active:
                 self._adain_op(plan, n.adain, B, n.c_in, t_in, src)
+            if n.name in stacks and self._use_stack(stacks[n.name], B, t_in):
+                # the whole residual stack in one kernel; unit outputs never reach HBM
+                run = stacks[n.name]
+                last = run[-1][1]
+                for k3, k1 in run:
+                    skip.update((k3.name, k1.name))
+                if last.dst in outputs:
+                    dst, size = outputs[last.dst], -1
+                else:
+                    size = B * last.c_out * t_in
+                    dst = View("ws", plan.ws.alloc(size), last.c_out * t_in, t_in)
+                self._stack(plan, run, B, t_in, src, dst)
+                tensors[last.dst] = (dst, t_in, size)
+                if last_use.get(n.src, -1) <= i + 2 * len(run) - 1 and n.src in tensors:
+                    v, _, sz = tensors[n.src]
+                    if sz > 0 and v.slot == "ws" and n.src not in outputs:
+                        plan.ws.release(v.off, sz)
+                continue
             if n.name in fused and self._fuse_unit(n, fused[n.name], B, t_in, src):
                 # Residual(DilatedUnit) in one kernel; the k=3 output never exists in HBM
                 k1 = fused[n.name]

@@ -631,3 +631,70 @@ def test_auto_tuning_roundtrip(dev):
     torch.cuda.synchronize()
     assert m2.tuning() == m1.tuning()
     assert torch.equal(y1, y2)
+
+
+STACK_CASES = [
+    # C, dilations, act, causal, B, T
+    (64, (1, 3, 9), "leaky", False, 2, 1000),
+    (64, (1, 3, 9), "snake", True, 1, 300),
+    (128, (1, 3, 9), "leaky", False, 2, 257),
+    (128, (1, 3, 9), "snake", False, 1, 64),
+    (64, (1, 3, 9), "leaky", True, 3, 20),
+    (128, (2, 5, 11), "leaky", False, 1, 500),
+]
+
+
+@pytest.mark.parametrize("case", STACK_CASES, ids=[str(c) for c in STACK_CASES])
+def test_residual_stack_kernel(N, dev, case):
+    """rave_residual_stack == the three units one after the other (oracle,
+    float64, and the split16 unit kernel run three times)."""
+    from oracle.rave_oracle import conv1d, leaky_relu, snake
+    C, dils, act, causal, B, T = case
+    rng = np.random.default_rng(C + sum(dils) + T)
+    x = rng.standard_normal((B, C, T)).astype(np.float32)
+    xd = torch.from_numpy(x).to(dev)
+    units, args = [], N.StackArgs(channels=C, batch=B, t_len=T, act=N.ACT[act], leaky_slope=0.2)
+    keep = []
+    for u, d in enumerate(dils):
+        w1 = (rng.standard_normal((C, C, 3)) / np.sqrt(3 * C)).astype(np.float32)
+        w2 = (rng.standard_normal((C, C, 1)) / np.sqrt(C)).astype(np.float32)
+        b1 = (rng.standard_normal(C) * 0.1).astype(np.float32)
+        b2 = (rng.standard_normal(C) * 0.1).astype(np.float32)
+        a0 = (1 + 0.3 * rng.standard_normal(C)).astype(np.float32)
+        a2 = (1 + 0.3 * rng.standard_normal(C)).astype(np.float32)
+        pad = (2 * d, 0) if causal else (d, d)
+        units.append((w1, w2, b1, b2, a0, a2, d, pad))
+        tens = [torch.from_numpy(N.pack_unit_weight(w1, w2, C, precision=N.PREC_SPLIT16)).to(dev)] + \
+               [torch.from_numpy(v).to(dev) for v in (b1, b2, a0, a2)]
+        keep += tens
+        setattr(args, f"dilation{u}", d)
+        setattr(args, f"pad_left{u}", pad[0])
+        for f, t in zip(("weight", "bias1", "bias2", "alpha0", "alpha2"), tens):
+            setattr(args, f"{f}{u}", t.data_ptr())
+    y = torch.full_like(xd, float("nan"))
+    args.x, args.x_sb, args.x_sc = xd.data_ptr(), C * T, T
+    args.y, args.y_sb, args.y_sc = y.data_ptr(), C * T, T
+    st = C_.c_void_p(torch.cuda.current_stream().cuda_stream)
+    N.check(N.lib.rave_residual_stack(C_.byref(args), st), "residual_stack")
+    # the same three units through the single-unit kernel
+    cur = xd
+    for u, (w1, w2, b1, b2, a0, a2, d, pad) in enumerate(units):
+        nxt = torch.empty_like(xd)
+        ua = N.UnitArgs(channels=C, batch=B, t_len=T, dilation=d, pad_left=pad[0], act=N.ACT[act],
+                        leaky_slope=0.2, precision=N.PREC_SPLIT16, x=cur.data_ptr(), x_sb=C * T, x_sc=T,
+                        y=nxt.data_ptr(), y_sb=C * T, y_sc=T, weight=getattr(args, f"weight{u}"),
+                        bias1=getattr(args, f"bias1{u}"), bias2=getattr(args, f"bias2{u}"),
+                        alpha0=getattr(args, f"alpha0{u}"), alpha2=getattr(args, f"alpha2{u}"))
+        N.check(N.lib.rave_residual_unit(C_.byref(ua), st), "residual_unit")
+        cur = nxt
+    torch.cuda.synchronize()
+    got, seq = y.cpu().numpy(), cur.cpu().numpy()
+    ref = x.astype(np.float64)
+    for w1, w2, b1, b2, a0, a2, d, pad in units:
+        xa = snake(ref, a0[:, None]) if act == "snake" else leaky_relu(ref, 0.2)
+        h = conv1d(xa, w1, b1, 1, d, pad)
+        h = snake(h, a2[:, None]) if act == "snake" else leaky_relu(h, 0.2)
+        ref = ref + conv1d(h, w2, b2, 1, 1, (0, 0))
+    assert np.isfinite(got).all()
+    assert maxabs(got, seq) <= 1e-5 * max(1.0, np.abs(seq).max())
+    assert maxabs(got, ref) <= 2e-5 * max(1.0, np.abs(ref).max())

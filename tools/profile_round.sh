@@ -37,7 +37,7 @@ python3 "$R/tools/rocprof_summary.py" --trace "$KT" --fetch "$FE" --write "$WR" 
 find "$OUT" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
 # counter CSVs are large; keep the GEMM-family rows only
 for f in "$FE" "$WR"; do
-    head -n 1 "$f" > "$f.gemm"; grep -E 'conv1d|split_reduce|unit_kernel|unit_split|pqmf' "$f" >> "$f.gemm" || true
+    head -n 1 "$f" > "$f.gemm"; grep -E 'conv1d|split_reduce|unit_kernel|unit_split|stack_split|pqmf' "$f" >> "$f.gemm" || true
     rm -f "$f"
 done
 ls -la "$OUT"

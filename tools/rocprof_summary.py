@@ -30,6 +30,7 @@ FAMILIES = {
     "conv_split16": ("conv1d_split_kernel", ("split_reduce_kernel",)),
     "unit_f32": ("residual_unit_kernel", ()),
     "unit_split16": ("unit_split_kernel", ()),
+    "stack_split16": ("stack_split_kernel", ()),
     "pqmf_analysis": ("pqmf_analysis_kernel", ()),
     "pqmf_synthesis": ("pqmf_synthesis_kernel", ()),
 }
