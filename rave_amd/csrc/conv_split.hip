@@ -679,27 +679,42 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
 }
 
 // Sum the split-K slabs in split order (fixed order: deterministic), then
-// bias / residual / ConvT interleave.  One thread = 4 consecutive columns of
-// one (b, m) row; grid.y = B * M rows.
+// bias / residual / ConvT interleave.  One thread = 4 consecutive floats of
+// the flat [B][M][U] slab image (U % 4 == 0 when vec_p), grid-stride: every
+// lane busy whatever the row length (short-N layers have U = 64..128).
 __global__ __launch_bounds__(256) void split_reduce_kernel(ConvKArgs a) {
-    const int row = blockIdx.y;                     // b * M + m
-    const int b = row / a.M, m = row - b * a.M;
-    const int n = (blockIdx.x * 256 + threadIdx.x) * 4;
-    if (n >= a.U) return;
     const int64_t total = (int64_t)a.B * a.M * a.U;
-    const float* p = a.partial + (int64_t)row * a.U + n;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    const int cnt = min(4, a.U - n);
-    if (a.vec_p && cnt == 4) {
-        for (int s = 0; s < a.S; ++s) {
-            const s_f32x4 t = *reinterpret_cast<const s_f32x4*>(p + s * total);
-            v[0] += t[0]; v[1] += t[1]; v[2] += t[2]; v[3] += t[3];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    if (a.vec_p) {
+        for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < (total >> 2); q += stride) {
+            const int64_t i = q << 2;
+            s_f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+            for (int s = 0; s < a.S; ++s) v += *reinterpret_cast<const s_f32x4*>(a.partial + s * total + i);
+            const int64_t row = i / a.U;
+            const int n = (int)(i - row * a.U);
+            const int b = (int)(row / a.M), m = (int)(row - (int64_t)b * a.M);
+            if (!a.transposed && a.vec_y) {
+                if (a.bias) v += a.bias[m];
+                if (a.res) v += *reinterpret_cast<const s_f32x4*>(a.res + (int64_t)b * a.r_sb + (int64_t)m * a.r_sc + n);
+                *reinterpret_cast<s_f32x4*>(a.y + (int64_t)b * a.y_sb + (int64_t)m * a.y_sc + n) = v;
+            } else {
+                float vv[4];
+                *reinterpret_cast<s_f32x4*>(vv) = v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) store_out(a, b, m, n + e, vv[e]);
+            }
         }
-    } else {
-        for (int s = 0; s < a.S; ++s)
-            for (int e = 0; e < cnt; ++e) v[e] += p[s * total + e];
+        return;
     }
-    for (int e = 0; e < cnt; ++e) store_out(a, b, m, n + e, v[e]);
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += stride) {
+        float v = 0.f;
+        for (int s = 0; s < a.S; ++s) v += a.partial[s * total + i];
+        const int64_t row = i / a.U;
+        const int n = (int)(i - row * a.U);
+        const int b = (int)(row / a.M), m = (int)(row - (int64_t)b * a.M);
+        store_out(a, b, m, n, v);
+    }
 }
 
 // --------------------------------------------------------------------- host side
@@ -947,8 +962,8 @@ int conv1d_split(const rave_conv1d_args& a, void* stream) {
         default: set_error("conv1d: unsupported kernel size"); return RAVE_ERR_UNSUPPORTED;
     }
     if (rc != RAVE_OK || k.S <= 1 || k.inlaunch) return rc;
-    RAVE_CHECK_ARG((int64_t)k.B * k.M <= 65535, "conv1d(split16): too many rows for the split-K reduce");
-    launch(split_reduce_kernel, dim3(ceil_div(k.U, 1024), k.B * k.M), dim3(256), 0, st, k);
+    const int64_t work = k.vec_p ? ((int64_t)k.B * k.M * k.U) >> 2 : (int64_t)k.B * k.M * k.U;
+    launch(split_reduce_kernel, dim3((unsigned)std::min<int64_t>(ceil_div64(work, 256), 4096)), dim3(256), 0, st, k);
     return launch_status("split_reduce_kernel");
 }
 
