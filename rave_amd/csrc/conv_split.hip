@@ -27,8 +27,8 @@
 //   * the activation window [rows][VC] channels-last as two f16 planes (hi, lo),
 //     activation applied and split once per element on the way in, so each
 //     B-fragment (8 channels of one column) is one ds_read_b128.
-// Double-buffered (one barrier per chunk): chunk c+2's loads are in flight
-// while chunk c+1 is multiplied.  Each wave owns 2 or 4 blocks of 32x32
+// Double-buffered planes (one barrier per chunk); window DMAs three chunks
+// ahead in a 4-deep ring.  Each wave owns 2 or 4 blocks of 32x32
 // (32x64, 64x64 or 32x128 outputs); optionally two waves ("K-groups") share a
 // tile's K-steps.  Split-K over workgroups for short-N layers (fp32 slabs,
 // fixed-order combine: deterministic).  The autotuner picks the tile.
@@ -155,7 +155,10 @@ template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 
     static constexpr int XI = (RAW_F + 64 * PF * NW - 1) / (64 * PF * NW);   // window DMA pieces per wave
     static constexpr int RAW = XI * NW * 256 * PF;           // raw window bytes (with slack)
     static constexpr int STAGE = RAW;
-    static constexpr int NS = 3;                             // window DMA ring depth
+    // window DMA ring depth: a chunk's window is issued three chunks ahead and
+    // waited for one chunk before its split pass, so its load has two chunks of
+    // K-steps to land
+    static constexpr int NS = 4;
     static constexpr int ALPHA = 4096;                       // Snake alphas (<= 1024 channels)
     static constexpr int EROW = WN + 4;                      // epilogue transpose row stride (floats)
     static constexpr int EPI = NW * WM * EROW * 4;           // epilogue transpose area (reuses the ring)
@@ -169,7 +172,7 @@ template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 
     static_assert(KG == 1 || (KG == 2 && KS1 >= 1), "K-groups");
     // a configuration is built only if its hand-counted waits fit the vmcnt
     // field and its LDS fits the CU
-    static constexpr bool VALID = WR + XI <= 63 && LDS_ALL <= 160 * 1024;
+    static constexpr bool VALID = 2 * WR + 2 * XI <= 63 && LDS_ALL <= 160 * 1024;
 };
 
 template <int V> struct IC {
@@ -367,23 +370,24 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
         constexpr int WR = KS * NJ * 2, XI = G::XI;
         issue(c_begin, 0);
         issue(c_begin + 1, 1);
+        issue(c_begin + 2, 2);
 #pragma unroll
         for (int k = 0; k < KS; ++k) load_w(c_begin, k, ST0 + k);
-        wait_vm<XI + WR>();                     // window c_begin landed
+        wait_vm<2 * XI + WR>();                 // window c_begin landed
         __syncthreads();
         convert(c_begin, 0, 0);
-        wait_vm<WR>();                          // window c_begin+1 landed
+        wait_vm<XI + WR>();                     // window c_begin+1 landed
         __syncthreads();
         stamp(1);
 
-        // per chunk c: DMA window c+2 | own K-steps (weights of c from the ring,
+        // per chunk c: DMA window c+3 | own K-steps (weights of c from the ring,
         // refill with c+1) | split window c+1 into the other plane pair | wait + barrier
         int stage = 0;
         for (int c = c_begin; c < c_end; ++c) {
             const int pb = (c - c_begin) & 1;
-            const int s1 = stage == 2 ? 0 : stage + 1;
-            const int s2 = s1 == 2 ? 0 : s1 + 1;
-            issue(c + 2, s2);
+            const int s1 = (stage + 1) & 3;
+            const int s3 = (stage + 3) & 3;
+            issue(c + 3, s3);
             AFrag f[2];
             read_a(pb, ST0, f[0]);
 #pragma unroll
@@ -425,7 +429,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                     for (int i = k; i < XT; i += KS) convert_task(c + 1, s1, pb ^ 1, i);
                 }
             }
-            wait_vm<WR>();                      // window c+2 landed (weights of c+1 may fly)
+            // window c+2 landed (window c+3 and the weights of c+1 and c+2 may fly)
+            wait_vm<2 * WR + XI>();
             __syncthreads();
             stage = s1;
             if (c == c_begin) stamp(2);
@@ -726,12 +731,12 @@ struct SplitCfg {
 // KG waves per output tile): least padding with the most waves per workgroup
 // that still fills the chip; K split over workgroups (fp32 slabs, fixed-order
 // combine) when the output alone cannot give every SIMD a wave.
-constexpr int kNumSplitTiles = 14;
+constexpr int kNumSplitTiles = 16;
 constexpr int kSplitTiles[kNumSplitTiles][5] = {   // BM, BN, WM, KG, WN
     {128, 128, 32, 1, 128}, {64, 256, 32, 1, 128}, {64, 128, 32, 1, 128}, {256, 64, 64, 1, 64},
     {128, 64, 64, 1, 64},   {64, 64, 64, 1, 64},   {128, 64, 64, 2, 64},  {64, 128, 32, 2, 128},
     {128, 128, 32, 2, 128}, {256, 64, 64, 2, 64},  {128, 64, 32, 1, 64},  {64, 128, 32, 1, 64},
-    {256, 64, 32, 1, 64},   {128, 128, 32, 1, 64}};
+    {256, 64, 32, 1, 64},   {128, 128, 32, 1, 64}, {128, 64, 32, 2, 64},  {64, 128, 32, 2, 64}};
 
 // Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>, IC<WN>) for tile index ti (compile-time dispatch).
 template <typename Fn>
@@ -750,7 +755,9 @@ static auto with_tile(int ti, Fn&& f) {
         case 10: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});
         case 11: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{});
         case 12: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});
-        default: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{});
+        case 13: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{});
+        case 14: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{});
+        default: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{});
     }
 }
 static inline int tile_waves(int ti) {   // waves per workgroup

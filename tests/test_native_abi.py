@@ -132,7 +132,7 @@ def test_conv_configs_listing(precision):
     for c in cfgs:
         a.config = c
         assert N.lib.rave_conv1d_workspace(C.byref(a)) >= 0
-    a.config = 1 + 15         # tile index 15: no such tile
+    a.config = 1 + 16 * 30    # 31 K-splits: more than the layer has chunks
     assert N.lib.rave_conv1d_workspace(C.byref(a)) == -1
     a.config = -3
     assert N.lib.rave_conv1d_workspace(C.byref(a)) == -1
