@@ -168,7 +168,7 @@ template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 
     static constexpr int G8 = VC / 8;                        // 8-channel groups per row
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;   // convert tasks per thread
     static_assert(XPLANE % 16 == 0 && STAGE % 16 == 0, "16-byte LDS alignment");
-    static_assert((NI * NJ == 4 || NI * NJ == 2) && NW >= 1 && NW <= 8, "tile");
+    static_assert((NI * NJ == 4 || NI * NJ == 2) && NW >= 1 && NW <= 16, "tile");
     static_assert(KG == 1 || (KG == 2 && KS1 >= 1), "K-groups");
     // a configuration is built only if its hand-counted waits fit the vmcnt
     // field and its LDS fits the CU
@@ -736,7 +736,7 @@ constexpr int kSplitTiles[kNumSplitTiles][5] = {   // BM, BN, WM, KG, WN
     {128, 128, 32, 1, 128}, {64, 256, 32, 1, 128}, {64, 128, 32, 1, 128}, {256, 64, 64, 1, 64},
     {128, 64, 64, 1, 64},   {64, 64, 64, 1, 64},   {128, 64, 64, 2, 64},  {64, 128, 32, 2, 128},
     {128, 128, 32, 2, 128}, {256, 64, 64, 2, 64},  {128, 64, 32, 1, 64},  {64, 128, 32, 1, 64},
-    {256, 64, 32, 1, 64},   {128, 128, 32, 1, 64}, {128, 64, 32, 2, 64},  {64, 128, 32, 2, 64}};
+    {256, 64, 32, 1, 64},   {256, 64, 32, 2, 64},  {128, 64, 32, 2, 64},  {64, 128, 32, 2, 64}};
 
 // Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>, IC<WN>) for tile index ti (compile-time dispatch).
 template <typename Fn>
@@ -755,7 +755,7 @@ static auto with_tile(int ti, Fn&& f) {
         case 10: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});
         case 11: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{});
         case 12: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});
-        case 13: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{});
+        case 13: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{});
         case 14: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{});
         default: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{});
     }
