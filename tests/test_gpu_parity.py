@@ -698,3 +698,51 @@ def test_residual_stack_kernel(N, dev, case):
     assert np.isfinite(got).all()
     assert maxabs(got, seq) <= 1e-5 * max(1.0, np.abs(seq).max())
     assert maxabs(got, ref) <= 2e-5 * max(1.0, np.abs(ref).max())
+
+
+# ------------------------------------------------------------------ streaming history shift
+def _shift_ref(a, hist, t_new):
+    """cached_conv's cache update: the newest ``hist`` columns move to the front."""
+    out = a.copy()
+    out[..., :hist] = a[..., t_new:t_new + hist]
+    return out
+
+
+def test_shift_history_batched(dev, N):
+    """rave_shift_history alone and as a run of consecutive plan ops (one
+    batched launch of up to 24 buffers, more split over launches): hist below,
+    equal to and above t_new (in-place overlap), one-channel rows with long
+    histories, padded channel strides, hist 0."""
+    from rave_amd.model import Arena, Plan, View
+    rng = np.random.default_rng(7)
+    shapes = [(1, 1, 512, 2048), (2, 64, 6, 128), (1, 512, 130, 64), (3, 16, 200, 200),
+              (1, 8, 0, 32), (2, 33, 70, 5)]
+    shapes = shapes + [(1, 4 + i, 3 + 7 * i, 11 + i) for i in range(26)]
+    bufs, refs = [], []
+    for (B, Cc, h, t) in shapes:
+        a = rng.standard_normal((B, Cc + 1, h + t + 3)).astype(np.float32)  # padded strides
+        refs.append(a.copy())
+        bufs.append(torch.from_numpy(a).to(dev))
+    # single op through the public entry point
+    b0 = bufs[2].clone()
+    B, Cc, h, t = shapes[2]
+    s = N.ShiftArgs(batch=B, channels=Cc, hist=h, t_new=t, buf=b0.data_ptr(),
+                    sb=b0.stride(0), sc=b0.stride(1))
+    N.check(N.lib.rave_shift_history(C.byref(s), C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    exp = refs[2].copy()
+    exp[:, :Cc] = _shift_ref(refs[2][:, :Cc], h, t)
+    assert np.array_equal(b0.cpu().numpy(), exp)
+    # all of them as consecutive plan ops
+    plan = Plan(Arena())
+    for (B, Cc, h, t), buf in zip(shapes, bufs):
+        plan.add(N.OP_SHIFT_HISTORY, N.ShiftArgs,
+                 dict(batch=B, channels=Cc, hist=h, t_new=t, sb=buf.stride(0), sc=buf.stride(1)),
+                 dict(buf=View("abs", buf.data_ptr(), 0, 0, 1)))
+    plan.finalize(dev)
+    plan.run([])
+    torch.cuda.synchronize()
+    for (B, Cc, h, t), buf, r in zip(shapes, bufs, refs):
+        exp = r.copy()
+        exp[:, :Cc] = _shift_ref(r[:, :Cc], h, t)
+        assert np.array_equal(buf.cpu().numpy(), exp), (B, Cc, h, t)
