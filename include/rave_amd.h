@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 6
+#define RAVE_ABI_VERSION 7
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 
@@ -209,6 +209,10 @@ int rave_copy(const rave_copy_args* a, void* stream);
  *         r -= E_q[idx];   r starts as z[b, :, t]   (first index on ties)
  * decode: y[b, :, t] = sum_q E_q[idx[b, q, t]]
  * codebooks: (n_q, codebook_size, dim) fp32; idx int64.
+ * encode runs one launch per quantizer layer (frames x code splits, so the chip
+ * fills at any batch) plus a final index reduction; `work` is caller-owned
+ * device scratch of rave_rvq_workspace(a) floats (residual double buffer and
+ * per-split best candidates), unused by decode.
  */
 typedef struct rave_rvq_args {
     int32_t n_q, codebook_size, dim, batch;
@@ -217,7 +221,10 @@ typedef struct rave_rvq_args {
     const float* z;  int64_t z_sb, z_sc;      /* encode input                     */
     int64_t* idx;    int64_t i_sb, i_sq;      /* (B, n_q, T) int64                */
     float* y;        int64_t y_sb, y_sc;      /* decode output                    */
+    float* work;                              /* encode scratch                   */
 } rave_rvq_args;
+/* floats of encode scratch for these shapes (>= 0), or a negative status */
+int64_t rave_rvq_workspace(const rave_rvq_args* a);
 int rave_rvq_encode(const rave_rvq_args* a, void* stream);
 int rave_rvq_decode(const rave_rvq_args* a, void* stream);
 

@@ -36,7 +36,7 @@ OP_NOISE = 9
 OP_ADAIN = 10
 OP_UNIT = 11
 OP_STACK = 12
-ABI_VERSION = 6
+ABI_VERSION = 7
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 
 # GEMM arithmetic of conv / unit ops (include/rave_amd.h RAVE_PREC_*)
@@ -87,7 +87,8 @@ class RvqArgs(C.Structure):
                 ("codebooks", vp),
                 ("z", vp), ("z_sb", i64), ("z_sc", i64),
                 ("idx", vp), ("i_sb", i64), ("i_sq", i64),
-                ("y", vp), ("y_sb", i64), ("y_sc", i64)]
+                ("y", vp), ("y_sb", i64), ("y_sc", i64),
+                ("work", vp)]
 
 
 class ShiftArgs(C.Structure):
@@ -159,7 +160,7 @@ EXPORTS = [
     "rave_conv1d_chunk", "rave_conv1d_packed_size", "rave_conv1d_pack_weight", "rave_conv1d",
     "rave_conv1d_workspace", "rave_conv1d_configs", "rave_conv1d_split_packed_size", "rave_conv1d_split_pack_weight",
     "rave_pqmf_analysis", "rave_pqmf_synthesis", "rave_fill_channels", "rave_copy",
-    "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
+    "rave_rvq_workspace", "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
     "rave_unit_packed_size", "rave_unit_pack_weight", "rave_residual_unit",
     "rave_unit_split_packed_size", "rave_unit_split_pack_weight",
     "rave_stack_supported", "rave_residual_stack",
@@ -198,6 +199,8 @@ def _load():
     lib.rave_unit_split_packed_size.restype = i64
     lib.rave_unit_split_pack_weight.argtypes = [vp, vp, C.c_int, vp]
     lib.rave_conv1d_workspace.restype = i64
+    lib.rave_rvq_workspace.argtypes = [C.POINTER(RvqArgs)]
+    lib.rave_rvq_workspace.restype = i64
     for name, st in [("rave_conv1d", ConvArgs), ("rave_pqmf_analysis", AnalysisArgs),
                      ("rave_pqmf_synthesis", SynthesisArgs), ("rave_fill_channels", FillArgs),
                      ("rave_rvq_encode", RvqArgs), ("rave_rvq_decode", RvqArgs),

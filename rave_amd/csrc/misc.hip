@@ -71,106 +71,218 @@ int shift_history_batch(const rave_shift_args* const* ops, int n, hipStream_t st
 }
 
 // ------------------------------------------------------------------ RVQ encode
-// One workgroup per kFT frames, all quantizer layers in sequence (the residual
-// never leaves LDS).  Each thread scores kCodes codebook rows against every
-// frame of the tile: d = |e|^2 - 2 x.e (argmin == the reference's argmax of
-// -(|x|^2 - 2 x.e + |e|^2)); ties resolve to the smallest index like
-// torch.max.  The residual update r -= E[idx] is the reference's fp32 order.
-constexpr int kFT = 8;
-constexpr int kRvqThreads = 256;
+// One launch per quantizer layer q over a (frame tiles x code splits) grid, so
+// the chip fills at any batch (the layers are sequential; a frame's argmax
+// spans every split).  Launch q, per frame tile:
+//   1. (q >= 1) reduce layer q-1's per-split candidates -> idx[q-1] (split 0
+//      stores it), and form r_q = r_{q-1} - E_{q-1}[idx] in LDS (the
+//      reference's fp32 residual update; split 0 stores r_q for launch q+1);
+//   2. score this split's kRvqCS codes against the tile: d = |e|^2 - 2 r.e
+//      (argmin == the reference's argmax of -(|r|^2 - 2 r.e + |e|^2)), the
+//      r.e dots as one 32x32 fp32 MFMA block per wave (K = DIM), |e|^2 on the
+//      VALU; argmin per frame (ties -> smaller index, like torch.max) ->
+//      best[q & 1][split][frame].
+// A last launch (q = n_q) only does step 1.  Scratch (rave_rvq_workspace):
+// resid[2][frames][DIM] | best_d[2][S][frames] | best_i[2][S][frames]; the
+// double buffers make launch q's reads and writes disjoint.
+constexpr int kRvqFT = 32;                   // frames per tile (MFMA columns)
+constexpr int kRvqCS = 64;                   // codes per split (32 MFMA rows per wave)
+constexpr int kRvqThreads = 128;
+typedef float rvq_f32x16 __attribute__((ext_vector_type(16)));
+
+struct RvqLayer {
+    int q;            // layer scored by this launch (n_q: final reduction only)
+    int n_frames;
+    int splits;
+};
+
+__device__ inline int64_t rvq_zoff(const rave_rvq_args& a, int g, int d) {
+    int b = g / a.t_len, t = g - b * a.t_len;
+    return (int64_t)b * a.z_sb + (int64_t)d * a.z_sc + t;
+}
 
 template <int DIM>
-__global__ __launch_bounds__(kRvqThreads) void rvq_encode_kernel(rave_rvq_args a, int n_frames) {
-    __shared__ __attribute__((aligned(16))) float xs[kFT][DIM];
-    __shared__ float best_d[kRvqThreads / 64][kFT];
-    __shared__ int best_i[kRvqThreads / 64][kFT];
-    __shared__ int sel[kFT];
-
-    const int f0 = blockIdx.x * kFT;
+__global__ __launch_bounds__(kRvqThreads) void rvq_encode_kernel(rave_rvq_args a, RvqLayer L) {
+    __shared__ __attribute__((aligned(16))) float xs[kRvqFT][DIM + 4];   // +4: conflict-free b128 rows
+    __shared__ __attribute__((aligned(16))) float es[kRvqCS][DIM + 4];
+    __shared__ float nrm_s[kRvqCS];
+    __shared__ float red_d[kRvqThreads / 64][kRvqFT];
+    __shared__ int red_i[kRvqThreads / 64][kRvqFT];
+    __shared__ int sel[kRvqFT];
+    const int F = L.n_frames, S = L.splits, q = L.q;
+    const int f0 = blockIdx.x * kRvqFT;
+    const int split = blockIdx.y;
     const int tid = threadIdx.x;
-    // load the residual tile (frame f -> (b, t))
-    for (int i = tid; i < kFT * DIM; i += kRvqThreads) {
-        int f = i / DIM, d = i - f * DIM;
-        int g = f0 + f;
-        float v = 0.f;
-        if (g < n_frames) {
-            int b = g / a.t_len, t = g - b * a.t_len;
-            v = a.z[(int64_t)b * a.z_sb + (int64_t)d * a.z_sc + t];
+    // this split's codewords (contiguous rows): coalesced loads issued first so
+    // they overlap the index reduction and residual update below
+    constexpr int EPER = kRvqCS * DIM / 4 / kRvqThreads;
+    float4 ev4[EPER];
+    if (q < a.n_q) {
+        const float4* src = reinterpret_cast<const float4*>(
+            a.codebooks + ((int64_t)q * a.codebook_size + (int64_t)split * kRvqCS) * DIM);
+        const int rows = min(kRvqCS, a.codebook_size - split * kRvqCS);
+#pragma unroll
+        for (int u = 0; u < EPER; ++u) {
+            int i = tid + u * kRvqThreads;               // float4 index in the block
+            ev4[u] = (i / (DIM / 4) < rows) ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        xs[f][d] = v;
     }
-    __syncthreads();
+    float* resid = a.work;
+    float* best_d = a.work + (int64_t)2 * F * DIM;
+    int* best_i = reinterpret_cast<int*>(best_d + (int64_t)2 * S * F);
 
-    const int K = a.codebook_size;
-    for (int q = 0; q < a.n_q; ++q) {
-        const float* E = a.codebooks + (int64_t)q * K * DIM;
-        float bd[kFT];
-        int bi[kFT];
+    if (q >= 1) {
+        // layer q-1's index per frame: the lexicographic min of (d, index) over
+        // the splits (order-free, so equal to the first maximum of torch.max);
+        // 8 lanes per frame, all candidate loads issued before the compares
+        {
+            constexpr int LPF = kRvqThreads / kRvqFT;          // lanes per frame
+            const int f = tid / LPF, j = tid % LPF;
+            const int g = f0 + f;
+            const float* bd = best_d + (int64_t)((q - 1) & 1) * S * F;
+            const int* bi = best_i + (int64_t)((q - 1) & 1) * S * F;
+            float d0 = FLT_MAX;
+            int i0 = 0x7fffffff;
+            if (g < F) {
+                for (int s0 = j; s0 < S; s0 += 8 * LPF) {
+                    float dd[8];
+                    int ii[8];
 #pragma unroll
-        for (int f = 0; f < kFT; ++f) { bd[f] = FLT_MAX; bi[f] = 0x7fffffff; }
-        for (int k = tid; k < K; k += kRvqThreads) {
-            const float4* e4 = reinterpret_cast<const float4*>(E + (int64_t)k * DIM);
-            float dot[kFT];
+                    for (int u = 0; u < 8; ++u) {
+                        int s = s0 + LPF * u;
+                        dd[u] = s < S ? bd[(int64_t)s * F + g] : FLT_MAX;
+                        ii[u] = s < S ? bi[(int64_t)s * F + g] : 0x7fffffff;
+                    }
 #pragma unroll
-            for (int f = 0; f < kFT; ++f) dot[f] = 0.f;
-            float nrm = 0.f;
-#pragma unroll 4
-            for (int d4 = 0; d4 < DIM / 4; ++d4) {
-                float4 e = e4[d4];
-                nrm = fmaf(e.x, e.x, nrm); nrm = fmaf(e.y, e.y, nrm);
-                nrm = fmaf(e.z, e.z, nrm); nrm = fmaf(e.w, e.w, nrm);
-#pragma unroll
-                for (int f = 0; f < kFT; ++f) {
-                    float4 x = *reinterpret_cast<const float4*>(&xs[f][d4 * 4]);
-                    dot[f] = fmaf(x.x, e.x, dot[f]); dot[f] = fmaf(x.y, e.y, dot[f]);
-                    dot[f] = fmaf(x.z, e.z, dot[f]); dot[f] = fmaf(x.w, e.w, dot[f]);
+                    for (int u = 0; u < 8; ++u)
+                        if (dd[u] < d0 || (dd[u] == d0 && ii[u] < i0)) { d0 = dd[u]; i0 = ii[u]; }
                 }
             }
 #pragma unroll
-            for (int f = 0; f < kFT; ++f) {
-                float dv = nrm - 2.f * dot[f];
-                if (dv < bd[f]) { bd[f] = dv; bi[f] = k; }   // k ascending per thread
+            for (int off = LPF / 2; off > 0; off >>= 1) {
+                float od = __shfl_xor(d0, off);
+                int oi = __shfl_xor(i0, off);
+                if (od < d0 || (od == d0 && oi < i0)) { d0 = od; i0 = oi; }
+            }
+            if (j == 0) {
+                if (g < F && split == 0) {
+                    int b = g / a.t_len, t = g - b * a.t_len;
+                    a.idx[(int64_t)b * a.i_sb + (int64_t)(q - 1) * a.i_sq + t] = (int64_t)i0;
+                }
+                sel[f] = g < F ? i0 : 0;
             }
         }
-        // wave reduction (min distance, then min index)
-#pragma unroll
-        for (int f = 0; f < kFT; ++f) {
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                float od = __shfl_xor(bd[f], off);
-                int oi = __shfl_xor(bi[f], off);
-                if (od < bd[f] || (od == bd[f] && oi < bi[f])) { bd[f] = od; bi[f] = oi; }
-            }
-        }
-        const int w = tid >> 6;
-        if ((tid & 63) == 0) {
-#pragma unroll
-            for (int f = 0; f < kFT; ++f) { best_d[w][f] = bd[f]; best_i[w][f] = bi[f]; }
-        }
+        if (q == a.n_q) return;              // final launch: indices only (grid y == 1)
         __syncthreads();
-        if (tid < kFT) {
-            float d0 = best_d[0][tid];
-            int i0 = best_i[0][tid];
-            for (int ww = 1; ww < kRvqThreads / 64; ++ww) {
-                float dd = best_d[ww][tid];
-                int ii = best_i[ww][tid];
-                if (dd < d0 || (dd == d0 && ii < i0)) { d0 = dd; i0 = ii; }
-            }
-            sel[tid] = i0;
-            int g = f0 + tid;
-            if (g < n_frames) {
-                int b = g / a.t_len, t = g - b * a.t_len;
-                a.idx[(int64_t)b * a.i_sb + (int64_t)q * a.i_sq + t] = (int64_t)i0;
-            }
-        }
-        __syncthreads();
-        for (int i = tid; i < kFT * DIM; i += kRvqThreads) {
+        const float* E = a.codebooks + (int64_t)(q - 1) * a.codebook_size * DIM;
+        const float* rp = resid + (int64_t)((q - 1) & 1) * F * DIM;
+        float* rn = resid + (int64_t)(q & 1) * F * DIM;
+        constexpr int PER = kRvqFT * DIM / kRvqThreads;
+        float rv[PER], ev[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {      // every load before any store
+            int i = tid + u * kRvqThreads;
             int f = i / DIM, d = i - f * DIM;
-            xs[f][d] = xs[f][d] - E[(int64_t)sel[f] * DIM + d];
+            int g = f0 + f;
+            rv[u] = 0.f;
+            ev[u] = 0.f;
+            if (g < F) {
+                rv[u] = (q == 1) ? a.z[rvq_zoff(a, g, d)] : rp[(int64_t)g * DIM + d];
+                ev[u] = E[(int64_t)sel[f] * DIM + d];
+            }
         }
-        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            int i = tid + u * kRvqThreads;
+            int f = i / DIM, d = i - f * DIM;
+            int g = f0 + f;
+            float v = rv[u] - ev[u];
+            if (g < F && split == 0 && q + 1 < a.n_q) rn[(int64_t)g * DIM + d] = v;
+            xs[f][d] = (g < F) ? v : 0.f;
+        }
+    } else {
+        constexpr int PER = kRvqFT * DIM / kRvqThreads;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            int i = tid + u * kRvqThreads;
+            int f = i / DIM, d = i - f * DIM;
+            int g = f0 + f;
+            xs[f][d] = (g < F) ? a.z[rvq_zoff(a, g, d)] : 0.f;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < EPER; ++u) {
+        int i = tid + u * kRvqThreads;
+        int r = i / (DIM / 4), c4 = i - r * (DIM / 4);
+        *reinterpret_cast<float4*>(&es[r][c4 * 4]) = ev4[u];
+    }
+    __syncthreads();
+
+    // dots on the fp32 MFMA: wave w scores codes [32w, 32w+32) of the split (A =
+    // codewords, rows) against the 32 frames (B = residuals, columns); lane half
+    // h takes dimensions [h*DIM/2, (h+1)*DIM/2), so each lane streams one
+    // contiguous row segment by 16-byte LDS reads
+    const int lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
+    rvq_f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const float* ea = &es[w * 32 + l32][h * (DIM / 2)];
+    const float* xb = &xs[l32][h * (DIM / 2)];
+    float nrm = 0.f;                           // |e|^2 of this lane's half row, in order
+#pragma unroll
+    for (int s4 = 0; s4 < DIM / 8; ++s4) {
+        const float4 e = *reinterpret_cast<const float4*>(ea + 4 * s4);
+        const float4 x = *reinterpret_cast<const float4*>(xb + 4 * s4);
+        nrm = fmaf(e.x, e.x, nrm); nrm = fmaf(e.y, e.y, nrm);
+        nrm = fmaf(e.z, e.z, nrm); nrm = fmaf(e.w, e.w, nrm);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(e.x, x.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(e.y, x.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(e.z, x.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(e.w, x.w, acc, 0, 0, 0);
+    }
+    {
+        const float other = __shfl_xor(nrm, 32);
+        if (h == 0) nrm_s[w * 32 + l32] = nrm + other;     // low half + high half
+    }
+    __syncthreads();                           // nrm_s
+    // d = |e|^2 - 2 r.e; per frame (column l32) the lexicographic min of
+    // (d, code) -- order-free, so ties resolve to the smallest code
+    float d0 = FLT_MAX;
+    int i0 = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int m = w * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;    // code within the split
+        const int k = split * kRvqCS + m;
+        if (k < a.codebook_size) {
+            float dv = nrm_s[m] - 2.f * acc[r];
+            if (dv < d0 || (dv == d0 && k < i0)) { d0 = dv; i0 = k; }
+        }
+    }
+    {
+        float od = __shfl_xor(d0, 32);
+        int oi = __shfl_xor(i0, 32);
+        if (od < d0 || (od == d0 && oi < i0)) { d0 = od; i0 = oi; }
+    }
+    if (h == 0) { red_d[w][l32] = d0; red_i[w][l32] = i0; }
+    __syncthreads();
+    if (tid < kRvqFT) {
+        const int g = f0 + tid;
+        float dd = red_d[0][tid];
+        int ii = red_i[0][tid];
+#pragma unroll
+        for (int ww = 1; ww < kRvqThreads / 64; ++ww) {
+            float od = red_d[ww][tid];
+            int oi = red_i[ww][tid];
+            if (od < dd || (od == dd && oi < ii)) { dd = od; ii = oi; }
+        }
+        if (g < F) {
+            best_d[(int64_t)(q & 1) * S * F + (int64_t)split * F + g] = dd;
+            best_i[(int64_t)(q & 1) * S * F + (int64_t)split * F + g] = ii;
+        }
     }
 }
+
+static int rvq_splits(const rave_rvq_args* p) { return ceil_div(p->codebook_size, kRvqCS); }
 
 __global__ void rvq_decode_kernel(rave_rvq_args a) {
     const int b = blockIdx.y;
@@ -215,18 +327,36 @@ extern "C" int rave_shift_history(const rave_shift_args* p, void* stream) {
     return shift_history_batch(&p, 1, as_stream(stream));
 }
 
+extern "C" int64_t rave_rvq_workspace(const rave_rvq_args* p) {
+    RAVE_CHECK_ARG(p && p->n_q > 0 && p->codebook_size > 0 && p->dim > 0 && p->batch >= 0 && p->t_len >= 0,
+                   "rvq_workspace: bad shape");
+    const int64_t F = (int64_t)p->batch * p->t_len;
+    return 2 * F * p->dim + 4 * (int64_t)rvq_splits(p) * F;
+}
+
 extern "C" int rave_rvq_encode(const rave_rvq_args* p, void* stream) {
-    RAVE_CHECK_ARG(p && p->z && p->idx && p->codebooks, "rvq_encode: null pointer");
+    RAVE_CHECK_ARG(p && p->z && p->idx && p->codebooks && p->work, "rvq_encode: null pointer");
     RAVE_CHECK_ARG(p->n_q > 0 && p->codebook_size > 0 && p->batch > 0 && p->t_len > 0,
                    "rvq_encode: empty shape");
-    int n_frames = p->batch * p->t_len;
-    dim3 grid(ceil_div(n_frames, kFT));
+    RAVE_CHECK_ARG((int64_t)p->batch * p->t_len <= (1 << 30), "rvq_encode: too many frames");
+    const int F = p->batch * p->t_len;
+    const int S = rvq_splits(p);
+    auto kern = rvq_encode_kernel<128>;
     switch (p->dim) {
-        case 128: launch(rvq_encode_kernel<128>, grid, dim3(kRvqThreads), 0, as_stream(stream), *p, n_frames); break;
-        case 64: launch(rvq_encode_kernel<64>, grid, dim3(kRvqThreads), 0, as_stream(stream), *p, n_frames); break;
+        case 128: kern = rvq_encode_kernel<128>; break;
+        case 64: kern = rvq_encode_kernel<64>; break;
         default: set_error("rvq_encode: dim must be 64 or 128"); return RAVE_ERR_UNSUPPORTED;
     }
-    return launch_status("rvq_encode_kernel");
+    const int tiles = ceil_div(F, kRvqFT);
+    // the op's timing (rave_plan_profile) spans all launches: launch() records the
+    // start event on the first and re-records the stop event on each
+    for (int q = 0; q <= p->n_q; ++q) {
+        launch(kern, dim3(tiles, q == p->n_q ? 1 : S), dim3(kRvqThreads), 0, as_stream(stream), *p,
+               RvqLayer{q, F, S});
+        int rc = launch_status("rvq_encode_kernel");
+        if (rc != RAVE_OK) return rc;
+    }
+    return RAVE_OK;
 }
 
 extern "C" int rave_rvq_decode(const rave_rvq_args* p, void* stream) {

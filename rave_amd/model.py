@@ -745,12 +745,16 @@ class RAVE:
         self._run_stack(plan, self.graph.encoder, B, {"enc_in": (bands, F)}, {"latent": lat})
         if codes:
             rq = cfg.rvq
-            plan.add(N.OP_RVQ_ENCODE, N.RvqArgs,
-                     dict(n_q=rq.num_quantizers, codebook_size=rq.codebook_size, dim=cfg.latent_size,
-                          batch=B, t_len=Fz, z_sb=lat.sb, z_sc=lat.sc,
-                          i_sb=rq.num_quantizers * Fz, i_sq=Fz, y_sb=0, y_sc=0),
+            sc = dict(n_q=rq.num_quantizers, codebook_size=rq.codebook_size, dim=cfg.latent_size,
+                      batch=B, t_len=Fz, z_sb=lat.sb, z_sc=lat.sc,
+                      i_sb=rq.num_quantizers * Fz, i_sq=Fz, y_sb=0, y_sc=0)
+            nw = int(N.lib.rave_rvq_workspace(C.byref(N.RvqArgs(**sc))))
+            if nw < 0:
+                N.check(nw, "rvq_workspace")
+            plan.add(N.OP_RVQ_ENCODE, N.RvqArgs, sc,
                      dict(codebooks=View("arena", self.cb_off, 0, 0), z=lat,
-                          idx=View(1, 0, 0, 0, elem=8), y=None))
+                          idx=View(1, 0, 0, 0, elem=8), y=None,
+                          work=View("ws", plan.ws.alloc(max(nw, 1)), 0, 0)))
         else:
             self._fill_speaker(plan, B, Fz, View(1, cfg.latent_size * Fz, lat.sb, Fz))
         self._plans[key] = plan.finalize(self.device)

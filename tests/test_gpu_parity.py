@@ -278,6 +278,8 @@ def test_rvq_kernels_golden(dev, golden, N):
     a = N.RvqArgs(n_q=16, codebook_size=1024, dim=D, batch=B, t_len=T, codebooks=cb.data_ptr(),
                   z=z.data_ptr(), z_sb=D * T, z_sc=T, idx=idx.data_ptr(), i_sb=16 * T, i_sq=T,
                   y=y.data_ptr(), y_sb=D * T, y_sc=T)
+    work = torch.empty(int(N.lib.rave_rvq_workspace(C.byref(a))), device=dev)
+    a.work = work.data_ptr()
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     N.check(N.lib.rave_rvq_encode(C.byref(a), st))
     N.check(N.lib.rave_rvq_decode(C.byref(a), st))
@@ -746,3 +748,56 @@ def test_shift_history_batched(dev, N):
         exp = r.copy()
         exp[:, :Cc] = _shift_ref(r[:, :Cc], h, t)
         assert np.array_equal(buf.cpu().numpy(), exp), (B, Cc, h, t)
+
+
+def _rvq_encode_np(z, cbs):
+    """float64 RVQ encode (rave/quantization.py:131-140,302-318) with each
+    layer's top-2 distance gap, for tie-tolerant index comparison."""
+    B, D, T = z.shape
+    r = z.transpose(0, 2, 1).reshape(-1, D).astype(np.float64)
+    idx, gaps = [], []
+    for E in cbs.astype(np.float64):
+        d = (E * E).sum(1)[None] - 2.0 * r @ E.T
+        o = np.argsort(d, 1, kind="stable")[:, :2]
+        i = o[:, 0]
+        gaps.append(np.take_along_axis(d, o[:, 1:2], 1)[:, 0] - np.take_along_axis(d, o[:, :1], 1)[:, 0])
+        idx.append(i)
+        r = r - E[i]
+    idx = np.stack(idx, 0).reshape(len(cbs), B, T).transpose(1, 0, 2)
+    gaps = np.stack(gaps, 0).reshape(len(cbs), B, T).transpose(1, 0, 2)
+    return idx, gaps
+
+
+@pytest.mark.parametrize("B,D,T,K,nq", [(8, 128, 64, 1024, 16), (3, 64, 37, 1000, 5), (1, 128, 1, 64, 2)])
+def test_rvq_encode_sizes_vs_numpy(dev, N, B, D, T, K, nq):
+    """The per-layer split RVQ encode at the C4 per-GPU shard (512 frames) and
+    at ragged sizes (frames not a multiple of the 32-frame tile, codebook not a
+    multiple of the 64-code split, dim 64, one frame): indices equal the float64
+    argmin wherever its top-2 gap exceeds the fp32 tie margin; decode of the
+    indices equals the sum of the selected codewords."""
+    rng = np.random.default_rng(B * 1000 + K)
+    cbs = rng.standard_normal((nq, K, D)).astype(np.float32)
+    z = rng.standard_normal((B, D, T)).astype(np.float32) * 2.0
+    cb = torch.from_numpy(cbs).to(dev)
+    zt = torch.from_numpy(z).to(dev)
+    idx = torch.full((B, nq, T), -1, dtype=torch.int64, device=dev)
+    y = torch.empty(B, D, T, device=dev)
+    a = N.RvqArgs(n_q=nq, codebook_size=K, dim=D, batch=B, t_len=T, codebooks=cb.data_ptr(),
+                  z=zt.data_ptr(), z_sb=D * T, z_sc=T, idx=idx.data_ptr(), i_sb=nq * T, i_sq=T,
+                  y=y.data_ptr(), y_sb=D * T, y_sc=T)
+    work = torch.empty(int(N.lib.rave_rvq_workspace(C.byref(a))), device=dev)
+    a.work = work.data_ptr()
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    N.check(N.lib.rave_rvq_encode(C.byref(a), st))
+    N.check(N.lib.rave_rvq_decode(C.byref(a), st))
+    torch.cuda.synchronize()
+    got = idx.cpu().numpy()
+    assert got.min() >= 0 and got.max() < K
+    ref, gap = _rvq_encode_np(z, cbs)
+    mism = got != ref
+    assert (gap[mism] < 1e-3).all()
+    # decode sums the codewords of the returned indices in layer order
+    zq = np.zeros((B, T, D), np.float32)
+    for q in range(nq):
+        zq = zq + cbs[q][got[:, q, :]]
+    assert maxabs(y.cpu().numpy(), zq.transpose(0, 2, 1)) < 1e-5
