@@ -52,27 +52,57 @@ def gather_latents(z_local: torch.Tensor, out: Optional[torch.Tensor] = None,
 
 
 class ShardedRunner:
-    """encode (local shard) -> all-gather latents -> decode (local shard).
+    """One data-parallel step on this rank's shard of the utterance batch.
 
-    ``model`` is anything with ``encode``/``decode`` (rave_amd.RAVE on GPU)."""
+    ``mode``:
+      * ``"latent"`` (C2) -- encode -> all-gather latents -> decode;
+      * ``"codes"`` (C4, DiscreteScriptedRAVE, scripts/export.py:503-517) --
+        encode_codes -> all-gather the RVQ indices -> decode_codes.  Over RCCL
+        the indices travel as int16 when the codebook fits (1024 entries: a
+        quarter of the int64 bytes) and are widened back after the gather;
+      * ``"decode"`` (C5) -- decode of the local latent shard; no exchange.
 
-    def __init__(self, model, group=None):
+    Each rank decodes its own rows of the gathered tensor.  ``model`` is
+    anything with the matching methods (rave_amd.RAVE on GPU)."""
+
+    MODES = ("latent", "codes", "decode")
+
+    def __init__(self, model, group=None, mode: str = "latent"):
+        if mode not in self.MODES:
+            raise ValueError(f"mode must be one of {self.MODES}")
         self.model = model
         self.group = group
-        self._z_all: Optional[torch.Tensor] = None
+        self.mode = mode
+        self._all: Optional[torch.Tensor] = None
+
+    def _narrow_codes(self) -> bool:
+        rvq = getattr(getattr(self.model, "cfg", None), "rvq", None)
+        return (self.mode == "codes" and rvq is not None and rvq.codebook_size <= 32767
+                and dist.get_backend(self.group) == "nccl")
+
+    def _gather(self, t: torch.Tensor) -> torch.Tensor:
+        rank, size = world()
+        if size == 1:
+            return t
+        narrow = self._narrow_codes()
+        src = t.to(torch.int16) if narrow else t
+        shape = (size * src.shape[0],) + tuple(src.shape[1:])
+        if self._all is None or tuple(self._all.shape) != shape or self._all.dtype != src.dtype:
+            self._all = torch.empty(shape, dtype=src.dtype, device=src.device)
+        out = gather_latents(src, self._all, self.group)
+        return out.to(t.dtype) if narrow else out
 
     def step(self, x_local: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(what every rank holds after the exchange, this rank's decoded audio)."""
         rank, size = world()
+        if self.mode == "decode":
+            return x_local, self.model.decode(x_local)
         if getattr(self.model, "adain", None) is not None:
             # AdaIN buffer rows follow the global batch index (rave/blocks.py:886-891)
             self.model.adain_row0 = rank * x_local.shape[0]
-        z = self.model.encode(x_local)
-        if size > 1:
-            shape = (size * z.shape[0],) + tuple(z.shape[1:])
-            if self._z_all is None or tuple(self._z_all.shape) != shape:
-                self._z_all = torch.empty(shape, dtype=z.dtype, device=z.device)
-            z_all = gather_latents(z, self._z_all, self.group)
-            zl = z_all[rank * z.shape[0]:(rank + 1) * z.shape[0]]
-        else:
-            z_all = zl = z
-        return z_all, self.model.decode(zl)
+        b = x_local.shape[0]
+        if self.mode == "codes":
+            t_all = self._gather(self.model.encode_codes(x_local))
+            return t_all, self.model.decode_codes(t_all[rank * b:(rank + 1) * b])
+        t_all = self._gather(self.model.encode(x_local))
+        return t_all, self.model.decode(t_all[rank * b:(rank + 1) * b])

@@ -38,17 +38,80 @@ class _OracleModel:
         return torch.from_numpy(self.o.decode(z.numpy()).astype(np.float32))
 
 
-def _worker(rank, size, port, x_all, q):
+class _OracleCodesModel:
+    """encode_codes/decode_codes (DiscreteScriptedRAVE, scripts/export.py:503-517)
+    through the oracle on the discrete config (test stand-in)."""
+
+    def __init__(self):
+        from oracle.rave_oracle import Oracle
+        from rave_amd import config as rcfg
+        from rave_amd.weights import init_params, init_speaker
+        self.cfg = rcfg.discrete(capacity=4)
+        self.o = Oracle(self.cfg, init_params(self.cfg, 0), init_speaker(self.cfg, 0))
+
+    def encode_codes(self, x):
+        return torch.from_numpy(self.o.rvq_encode(self.o.encode(x.numpy())).astype(np.int64))
+
+    def decode_codes(self, idx):
+        z = self.o.cat_speaker(self.o.rvq_decode(idx.numpy()))
+        return torch.from_numpy(self.o.decode(z).astype(np.float32))
+
+    def decode(self, z):
+        return torch.from_numpy(self.o.decode(z.numpy()).astype(np.float32))
+
+
+def _worker(rank, size, port, x_all, q, mode="latent"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=size)
     try:
         from rave_amd.distributed import ShardedRunner, shard_bounds
         lo, hi = shard_bounds(x_all.shape[0], rank, size)
-        runner = ShardedRunner(_OracleModel())
+        model = _OracleModel() if mode == "latent" else _OracleCodesModel()
+        runner = ShardedRunner(model, mode=mode)
         z_all, y = runner.step(x_all[lo:hi])
         q.put((rank, z_all.numpy(), y.numpy()))
     finally:
         dist.destroy_process_group()
+
+
+def _run_world2(x_all, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, x_all, q, mode)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(res, key=lambda t: t[0])
+
+
+def test_sharded_codes_gather_matches_single_process():
+    """C4's path: encode_codes per shard -> all-gather of the RVQ indices ->
+    decode_codes of the local rows; every rank holds the batch's indices."""
+    rng = np.random.default_rng(1)
+    x_all = torch.from_numpy((0.2 * rng.standard_normal((4, 1, 2048))).astype(np.float32))
+    m = _OracleCodesModel()
+    idx_ref = m.encode_codes(x_all)
+    y_ref = m.decode_codes(idx_ref)
+    for rank, idx_all, y in _run_world2(x_all, "codes"):
+        assert idx_all.dtype == np.int64
+        np.testing.assert_array_equal(idx_all, idx_ref.numpy())
+        np.testing.assert_allclose(y, y_ref.numpy()[rank * 2:(rank + 1) * 2], atol=1e-6)
+
+
+def test_sharded_decode_mode_has_no_exchange():
+    """C5's path: each rank decodes its own latent shard; nothing is gathered."""
+    from rave_amd.distributed import ShardedRunner
+    m = _OracleCodesModel()
+    z = torch.from_numpy(np.random.default_rng(2).standard_normal((1, 384, 2)).astype(np.float32))
+    held, y = ShardedRunner(m, mode="decode").step(z)
+    assert held is z
+    np.testing.assert_allclose(y.numpy(), m.decode(z).numpy(), atol=0)
+    with pytest.raises(ValueError):
+        ShardedRunner(m, mode="tokens")
 
 
 def test_sharded_encode_gather_decode_matches_single_process():

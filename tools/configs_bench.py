@@ -16,6 +16,11 @@ Prints one JSON object; the reference CPU numbers these compare with are in
 BASELINE.md (measured in the build container, 8 threads).
 
     python tools/configs_bench.py [--precision auto] [--only c3,c4,c5]
+
+C4 and C5 run through rave_amd.distributed.ShardedRunner; launched with
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1
+tools/configs_bench.py --only c4,c5`` each rank takes one shard (weak scaling)
+and the numbers are whole-job (max over ranks), as in bench.py.
 """
 import argparse
 import json
@@ -25,9 +30,11 @@ import time
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from rave_amd import config as rcfg  # noqa: E402
+from rave_amd.distributed import ShardedRunner, world  # noqa: E402
 from rave_amd.model import RAVE  # noqa: E402
 from rave_amd.weights import init_params, init_speaker  # noqa: E402
 
@@ -92,33 +99,64 @@ def c3(precision, blocks, warmup, dev):
     return out
 
 
+def sharded_steps(fn, steps, warmup):
+    """bench.py's contract: barrier + synchronize around exactly ``steps``
+    steps, the max over ranks."""
+    rank, size = world()
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if size > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if size > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if size > 1:
+        t = torch.tensor([el], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el / steps
+
+
 def c4(precision, steps, warmup, dev, B=8, T=65536):
+    """Per-GPU shard of 64: encode_codes -> all-gather of the indices (RCCL,
+    int16 on the wire) -> decode_codes (rave_amd.distributed, mode "codes")."""
+    rank, size = world()
     cfg = rcfg.discrete()
     m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=precision)
-    x = (0.2 * torch.randn(B, 1, T, generator=torch.Generator().manual_seed(0))).to(dev)
+    x = (0.2 * torch.randn(B, 1, T, generator=torch.Generator().manual_seed(rank))).to(dev)
     t_enc = timed_steps(lambda: m.encode_codes(x), steps, warmup)
     idx = m.encode_codes(x)
     t_dec = timed_steps(lambda: m.decode_codes(idx), steps, warmup)
-    t = timed_steps(lambda: m.decode_codes(m.encode_codes(x)), steps, warmup)
-    out = {"workload": f"discrete encode -> RVQ(16x1024) -> decode, {B} x {T} per GPU "
-                       "(BASELINE configs[3] per-GPU shard of 64)",
+    runner = ShardedRunner(m, mode="codes")
+    t = sharded_steps(lambda: runner.step(x), steps, warmup)
+    out = {"workload": f"discrete encode -> RVQ(16x1024) -> all-gather indices -> decode, {B} x {T} per GPU "
+                       "(BASELINE configs[3] per-GPU shard of 64)", "n_gpus": size,
            "ms_per_step": round(t * 1e3, 4), "encode_codes_ms": round(t_enc * 1e3, 4),
            "decode_codes_ms": round(t_dec * 1e3, 4),
-           "samples_per_s": round(B * T / t, 1), "x_realtime_aggregate": round(B * T / t / SR, 1)}
+           "samples_per_s": round(size * B * T / t, 1), "x_realtime_aggregate": round(size * B * T / t / SR, 1)}
     log(f"C4: {out}")
     return out
 
 
 def c5(precision, steps, warmup, dev, B=16, Fz=64):
+    """Per-GPU shard of 128: decode of the local latents, no exchange
+    (rave_amd.distributed, mode "decode")."""
+    rank, size = world()
     cfg = rcfg.v3_noise()
     m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=precision)
-    z = torch.randn(B, cfg.dec_in, Fz, generator=torch.Generator().manual_seed(0)).to(dev)
-    t = timed_steps(lambda: m.decode(z), steps, warmup)
+    z = torch.randn(B, cfg.dec_in, Fz, generator=torch.Generator().manual_seed(rank)).to(dev)
+    runner = ShardedRunner(m, mode="decode")
+    t = sharded_steps(lambda: runner.step(z), steps, warmup)
     T = Fz * cfg.hop
     out = {"workload": f"v3 Snake + noise decode, z ({B}, {cfg.dec_in}, {Fz}) -> ({B}, 1, {T}) per GPU "
-                       "(BASELINE configs[4] per-GPU shard of 128), device-drawn noise",
-           "ms_per_step": round(t * 1e3, 4), "samples_per_s": round(B * T / t, 1),
-           "x_realtime_aggregate": round(B * T / t / SR, 1)}
+                       "(BASELINE configs[4] per-GPU shard of 128), device-drawn noise", "n_gpus": size,
+           "ms_per_step": round(t * 1e3, 4), "samples_per_s": round(size * B * T / t, 1),
+           "x_realtime_aggregate": round(size * B * T / t / SR, 1)}
     log(f"C5: {out}")
     return out
 
@@ -131,17 +169,25 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--blocks", type=int, default=64)
     a = ap.parse_args()
-    dev = torch.device("cuda:0")
+    size = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if size > 1:     # torch.distributed.run, one process per GPU, RCCL
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
     which = set(a.only.split(","))
-    res = {"precision": a.precision, "device": torch.cuda.get_device_name(0), "data": "synthetic",
-           "weights": "random-init (rave_amd.weights)"}
-    if "c3" in which:
+    res = {"precision": a.precision, "device": torch.cuda.get_device_name(local), "data": "synthetic",
+           "weights": "random-init (rave_amd.weights)", "n_gpus": size}
+    if "c3" in which and size == 1:      # one stream per nn~ instance: not sharded
         res["c3"] = c3(a.precision, a.blocks, 8, dev)
     if "c4" in which:
         res["c4"] = c4(a.precision, a.steps, a.warmup, dev)
     if "c5" in which:
         res["c5"] = c5(a.precision, a.steps, a.warmup, dev)
-    print(json.dumps(res))
+    if world()[0] == 0:
+        print(json.dumps(res))
+    if size > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
