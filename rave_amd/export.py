@@ -1,0 +1,149 @@
+"""nn~ method surface over the HIP path.
+
+Restates the host-side contract of ``ScriptedRAVE`` (scripts/export.py:58-480)
+for a ``rave_amd.RAVE``:
+
+* ``register_method(name, in_channels, in_ratio, out_channels, out_ratio,
+  input_labels, output_labels)`` metadata (scripts/export.py:229-240), with the
+  upstream-style ``encode`` / ``decode`` / ``forward`` registrations (the
+  commented-out block at :172-227; the shipped ``myforward`` registration,
+  :229-240, declares 2 input channels that v2's path does not take, SURVEY.md
+  section 3);
+* attributes through ``register_attribute`` and ``get_<name>`` / ``set_<name>``
+  that store 1-tuples and return 0 from setters (:120-126, :427-479);
+* ``encode`` (:298-314), ``decode`` with the stereo duplication (:317-336) and
+  ``forward`` (:338-339), in streaming mode (cached_conv, one block per call)
+  for a causal config, offline otherwise.
+
+nn~ itself loads a TorchScript module; the kernels here are reached through
+ctypes, which TorchScript cannot script, so this is the method table and call
+semantics an nn~ host would drive, not a ``torch.jit`` export.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+_ATTRIBUTES = (("learn_target", False), ("reset_target", False), ("learn_source", False),
+               ("reset_source", False), ("speaker", 0), ("record", False))
+
+
+class NNTildeRAVE:
+    def __init__(self, model, stereo: bool = False, streaming: Optional[bool] = None,
+                 block: int = 2048, batch: int = 1):
+        cfg = model.cfg
+        self.model, self.cfg, self.stereo = model, cfg, bool(stereo)
+        self.streaming = cfg.causal if streaming is None else bool(streaming)
+        if self.streaming and not cfg.causal:
+            raise ValueError("streaming requires a causal config (causal.gin)")
+        if self.stereo and getattr(model, "adain", None) is not None:
+            raise ValueError("Stereo mode not yet supported with AdaIN")      # export.py:115-116
+        if cfg.rvq is not None:
+            raise ValueError("discrete configs export through encode_codes / decode_codes "
+                             "(DiscreteScriptedRAVE), not this method table")
+        self.block, self.batch = block, batch
+        self.sr = getattr(cfg, "sampling_rate", 48000)                       # v2.gin SAMPLING_RATE
+        self.latent_size = cfg.latent_size + cfg.speaker_size                # encode's channels
+        self._methods: Dict[str, Tuple[int, int, int, int, List[str], List[str]]] = {}
+        self._attrs: Dict[str, tuple] = {}
+        self._enc_stream = self._dec_stream = None
+        for name, default in _ATTRIBUTES:
+            self.register_attribute(name, default)
+        ratio = cfg.hop                                                      # x_len // z.shape[-1]
+        channels = ["(L)", "(R)"] if self.stereo else ["(mono)"]
+        audio_in = ["(signal) Input audio signal"]
+        audio_out = [f"(signal) Reconstructed audio signal {c}" for c in channels]
+        latents = [f"(signal) Latent dimension {i}" for i in range(self.latent_size)]
+        n_out = 2 if self.stereo else 1
+        self.register_method("encode", 1, 1, self.latent_size, ratio, audio_in, latents)
+        self.register_method("decode", self.latent_size, ratio, n_out, 1, latents, audio_out)
+        self.register_method("forward", 1, 1, n_out, 1, audio_in, audio_out)
+
+    # ------------------------------------------------------------ nn~ metadata
+    def register_method(self, name: str, in_channels: int, in_ratio: int, out_channels: int,
+                        out_ratio: int, input_labels: List[str], output_labels: List[str]) -> None:
+        if len(input_labels) != in_channels or len(output_labels) != out_channels:
+            raise ValueError(f"{name}: label counts must match the channel counts")
+        self._methods[name] = (in_channels, in_ratio, out_channels, out_ratio,
+                               list(input_labels), list(output_labels))
+
+    def get_methods(self) -> List[str]:
+        return list(self._methods)
+
+    def get_method_params(self, name: str) -> List[int]:
+        """[in_channels, in_ratio, out_channels, out_ratio], as nn~ queries them."""
+        return list(self._methods[name][:4])
+
+    def get_method_labels(self, name: str) -> Tuple[List[str], List[str]]:
+        return self._methods[name][4], self._methods[name][5]
+
+    def register_attribute(self, name: str, default) -> None:
+        self._attrs[name] = (default,)
+
+    def get_attributes(self) -> List[str]:
+        return list(self._attrs)
+
+    def get_attribute(self, name: str):
+        return self._attrs[name][0]
+
+    def set_attribute(self, name: str, value) -> int:
+        if name not in self._attrs:
+            raise KeyError(name)
+        kind = type(self._attrs[name][0])
+        self._attrs[name] = (kind(value),)
+        return 0
+
+    def __getattr__(self, item: str):
+        # get_<attr> / set_<attr>, the @torch.jit.export accessors of export.py:427-479
+        attrs = self.__dict__.get("_attrs", {})
+        if item.startswith("get_") and item[4:] in attrs:
+            return lambda: self.get_attribute(item[4:])
+        if item.startswith("set_") and item[4:] in attrs:
+            return lambda v: self.set_attribute(item[4:], v)
+        raise AttributeError(item)
+
+    # ------------------------------------------------------------ methods
+    def _streams(self, batch: int):
+        from rave_amd.streaming import StreamingRAVE
+        if self._enc_stream is None or self._enc_stream.B != batch:
+            self._enc_stream = StreamingRAVE(self.model, batch=batch, block=self.block)
+        nd = 2 * batch if self.stereo else batch
+        if self._dec_stream is None or self._dec_stream.B != nd:
+            self._dec_stream = StreamingRAVE(self.model, batch=nd, block=self.block)
+        return self._enc_stream, self._dec_stream
+
+    def _check(self, name: str, t: torch.Tensor) -> None:
+        c = self._methods[name][0]
+        if t.dim() != 3 or t.shape[1] != c:
+            raise ValueError(f"{name}: expected (B, {c}, T), got {tuple(t.shape)}")
+
+    def encode(self, x: torch.Tensor) -> torch.Tensor:
+        """scripts/export.py:298-314 (PQMF -> encoder on 6 bands -> cat speaker)."""
+        self._check("encode", x)
+        if self.streaming:
+            return self._streams(x.shape[0])[0].encode(x)
+        return self.model.encode(x)
+
+    def decode(self, z: torch.Tensor) -> torch.Tensor:
+        """scripts/export.py:317-336: stereo decodes the batch twice and puts the
+        copies side by side as channels (L, R)."""
+        self._check("decode", z)
+        B = z.shape[0]
+        if self.stereo:
+            z = torch.cat([z, z], 0)
+        y = self._streams(B)[1].decode(z.contiguous()) if self.streaming else self.model.decode(z)
+        if self.stereo:
+            y = torch.cat(y.chunk(2, 0), 1)
+        return y
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.decode(self.encode(x))
+
+    __call__ = forward
+
+    def reset(self) -> None:
+        """Zero the streaming caches (a fresh nn~ instance)."""
+        for s in (self._enc_stream, self._dec_stream):
+            if s is not None:
+                s.reset()

@@ -1,0 +1,51 @@
+"""nn~ method table and attribute accessors of rave_amd.export.NNTildeRAVE
+(scripts/export.py:120-126, 172-240, 427-479).  Metadata only: no GPU (a
+stand-in model carries the config); the GPU calls are in test_gpu_parity.py."""
+import pytest
+
+from rave_amd import config as rcfg
+from rave_amd.export import NNTildeRAVE
+
+
+class _Cfg:
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.adain = None
+
+
+def test_method_table_v2():
+    w = NNTildeRAVE(_Cfg(rcfg.v2()))
+    assert w.get_methods() == ["encode", "decode", "forward"]
+    assert w.get_method_params("encode") == [1, 1, 320, 1024]
+    assert w.get_method_params("decode") == [320, 1024, 1, 1]
+    assert w.get_method_params("forward") == [1, 1, 1, 1]
+    ins, outs = w.get_method_labels("encode")
+    assert ins == ["(signal) Input audio signal"] and len(outs) == 320
+    assert outs[3] == "(signal) Latent dimension 3"
+    assert w.streaming is False
+
+
+def test_stereo_and_causal():
+    w = NNTildeRAVE(_Cfg(rcfg.causal()), stereo=True)
+    assert w.streaming is True
+    assert w.get_method_params("decode") == [320, 1024, 2, 1]
+    assert w.get_method_labels("forward")[1] == ["(signal) Reconstructed audio signal (L)",
+                                                 "(signal) Reconstructed audio signal (R)"]
+    with pytest.raises(ValueError):
+        NNTildeRAVE(_Cfg(rcfg.v2()), streaming=True)          # offline config cannot stream
+    with pytest.raises(ValueError):
+        NNTildeRAVE(_Cfg(rcfg.discrete()))
+
+
+def test_attributes_store_one_tuples():
+    w = NNTildeRAVE(_Cfg(rcfg.v2()))
+    assert w.get_attributes() == ["learn_target", "reset_target", "learn_source", "reset_source",
+                                  "speaker", "record"]
+    assert w.get_speaker() == 0 and w.get_record() is False
+    assert w.set_speaker(3) == 0 and w.get_speaker() == 3
+    assert w.set_record(True) == 0 and w.get_record() is True
+    assert w._attrs["speaker"] == (3,)
+    with pytest.raises(AttributeError):
+        w.get_volume()
+    with pytest.raises(ValueError):
+        w.register_method("bad", 2, 1, 1, 1, ["one"], ["out"])

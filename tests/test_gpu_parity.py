@@ -801,3 +801,32 @@ def test_rvq_encode_sizes_vs_numpy(dev, N, B, D, T, K, nq):
     for q in range(nq):
         zq = zq + cbs[q][got[:, q, :]]
     assert maxabs(y.cpu().numpy(), zq.transpose(0, 2, 1)) < 1e-5
+
+
+# ------------------------------------------------------------------ nn~ method surface
+def test_nn_tilde_surface_streaming_and_stereo(dev):
+    """rave_amd.export.NNTildeRAVE (scripts/export.py:298-339): streaming
+    encode/decode/forward equal StreamingRAVE block for block; stereo decode
+    puts two identical channels side by side; offline encode == RAVE.encode."""
+    from rave_amd import config as rcfg
+    from rave_amd.export import NNTildeRAVE
+    from rave_amd.model import RAVE
+    from rave_amd.streaming import StreamingRAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.causal()
+    m = RAVE(cfg, init_params(cfg, 5), init_speaker(cfg, 5), device=dev)
+    w = NNTildeRAVE(m, stereo=True)
+    ref = StreamingRAVE(m, batch=1, block=2048)
+    gen = torch.Generator().manual_seed(3)
+    for _ in range(4):
+        x = (0.2 * torch.randn(1, 1, 2048, generator=gen)).to(dev)
+        y = w.forward(x)
+        y_ref = ref.forward(x)
+        assert tuple(y.shape) == (1, 2, 2048)
+        assert torch.equal(y[:, :1], y_ref) and torch.equal(y[:, 1:], y_ref)
+    cfg2 = rcfg.v2()
+    m2 = RAVE(cfg2, init_params(cfg2, 6), init_speaker(cfg2, 6), device=dev)
+    w2 = NNTildeRAVE(m2)
+    x = (0.2 * torch.randn(2, 1, 8192, generator=gen)).to(dev)
+    assert torch.equal(w2.encode(x), m2.encode(x))
+    assert w2.get_method_params("encode") == [1, 1, 320, 1024]
