@@ -322,6 +322,62 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
 #endif
 }
 
+// Launch of one layer family.  The kernel instantiations are spread over
+// separate translation units (the Makefile compiles this file once per family
+// with -DRAVE_F32_KT, and once without it for the host side) so the build runs
+// in parallel.
+template <int KT>
+int f32_launch_family(ConvKArgs k, const LaunchCfg& c, hipStream_t st);
+
+#ifdef RAVE_F32_KT
+template <int BM, int BN, int KT>
+static int launch_k(ConvKArgs k, hipStream_t st) {
+    using G = Geo<KT, BN>;
+    constexpr int A4 = G::BK * BM / 4;
+    constexpr int NA4 = (A4 + kThreads - 1) / kThreads;
+    constexpr int AROWS = NA4 * kThreads * 4 / BM;
+    constexpr int BUF = AROWS * BM + G::XS_FLOATS;
+    constexpr int NWT = (BM / 64) * (BN / 64);
+    constexpr int RED = (NWT < 4) ? 4 * 64 * 64 : 0;        // K-group reduction area
+    if (k.XW > G::XW_MAX) {
+        set_error("conv1d: dilation too large for the staged window");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    const size_t lds = (size_t)std::max(2 * BUF, RED) * sizeof(float);
+    static_assert((size_t)std::max(2 * BUF, RED) * sizeof(float) <= 160 * 1024, "LDS budget");
+    dim3 grid(ceil_div(k.U, BN), ceil_div(k.M, BM), k.B * k.S);
+    auto kern = (k.act == RAVE_ACT_SNAKE) ? conv1d_mfma_kernel<BM, BN, KT, true>
+                                           : conv1d_mfma_kernel<BM, BN, KT, false>;
+    if (lds > 64 * 1024) {
+        // opt in to more than 64 KiB of dynamic LDS (once per instantiation)
+        static bool done[2] = {false, false};
+        bool& d = done[k.act == RAVE_ACT_SNAKE];
+        if (!d) {
+            RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            d = true;
+        }
+    }
+    launch(kern, grid, dim3(kThreads), lds, st, k);
+    return launch_status("conv1d_mfma_kernel");
+}
+
+template <int KT>
+int f32_launch_family(ConvKArgs k, const LaunchCfg& c, hipStream_t st) {
+    k.XW = (c.bn - 1) * Family<KT>::ST + (KT - 1) * k.d + 1;
+    k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
+    if (c.bm == 128 && c.bn == 128) return launch_k<128, 128, KT>(k, st);
+    if (c.bm == 64 && c.bn == 256) return launch_k<64, 256, KT>(k, st);
+    if (c.bm == 128 && c.bn == 64) return launch_k<128, 64, KT>(k, st);
+    if (c.bm == 64 && c.bn == 128) return launch_k<64, 128, KT>(k, st);
+    return launch_k<64, 64, KT>(k, st);
+}
+
+template int f32_launch_family<RAVE_F32_KT>(ConvKArgs, const LaunchCfg&, hipStream_t);
+
+}  // namespace rave
+#else   // ------------------------------------------------------- host side
+
 // --------------------------------------------------------------------- host side
 static int family_cit(int taps) {
     switch (taps) {
@@ -362,49 +418,6 @@ static LaunchCfg choose(int M, int U, int B, int nchunks, int split_row = 1 << 3
     S = std::min(S, std::max(1, nchunks / 2));
     best.S = std::max(1, S);
     return best;
-}
-
-template <int BM, int BN, int KT>
-static int launch_k(ConvKArgs k, hipStream_t st) {
-    using G = Geo<KT, BN>;
-    constexpr int A4 = G::BK * BM / 4;
-    constexpr int NA4 = (A4 + kThreads - 1) / kThreads;
-    constexpr int AROWS = NA4 * kThreads * 4 / BM;
-    constexpr int BUF = AROWS * BM + G::XS_FLOATS;
-    constexpr int NWT = (BM / 64) * (BN / 64);
-    constexpr int RED = (NWT < 4) ? 4 * 64 * 64 : 0;        // K-group reduction area
-    if (k.XW > G::XW_MAX) {
-        set_error("conv1d: dilation too large for the staged window");
-        return RAVE_ERR_UNSUPPORTED;
-    }
-    const size_t lds = (size_t)std::max(2 * BUF, RED) * sizeof(float);
-    static_assert((size_t)std::max(2 * BUF, RED) * sizeof(float) <= 160 * 1024, "LDS budget");
-    dim3 grid(ceil_div(k.U, BN), ceil_div(k.M, BM), k.B * k.S);
-    auto kern = (k.act == RAVE_ACT_SNAKE) ? conv1d_mfma_kernel<BM, BN, KT, true>
-                                           : conv1d_mfma_kernel<BM, BN, KT, false>;
-    if (lds > 64 * 1024) {
-        // opt in to more than 64 KiB of dynamic LDS (once per instantiation)
-        static bool done[2] = {false, false};
-        bool& d = done[k.act == RAVE_ACT_SNAKE];
-        if (!d) {
-            RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            d = true;
-        }
-    }
-    launch(kern, grid, dim3(kThreads), lds, st, k);
-    return launch_status("conv1d_mfma_kernel");
-}
-
-template <int KT>
-static int launch_family(ConvKArgs k, const LaunchCfg& c, hipStream_t st) {
-    k.XW = (c.bn - 1) * Family<KT>::ST + (KT - 1) * k.d + 1;
-    k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
-    if (c.bm == 128 && c.bn == 128) return launch_k<128, 128, KT>(k, st);
-    if (c.bm == 64 && c.bn == 256) return launch_k<64, 256, KT>(k, st);
-    if (c.bm == 128 && c.bn == 64) return launch_k<128, 64, KT>(k, st);
-    if (c.bm == 64 && c.bn == 128) return launch_k<64, 128, KT>(k, st);
-    return launch_k<64, 64, KT>(k, st);
 }
 
 // exact-fp32 layout: chunks of family_cit channels, rows padded to 128
@@ -571,12 +584,12 @@ extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
 #endif
     hipStream_t st = as_stream(stream);
     switch (taps) {
-        case 1: rc = launch_family<1>(k, c, st); break;
-        case 2: rc = launch_family<2>(k, c, st); break;
-        case 3: rc = launch_family<3>(k, c, st); break;
-        case 4: rc = launch_family<4>(k, c, st); break;
-        case 7: rc = launch_family<7>(k, c, st); break;
-        case 8: rc = launch_family<8>(k, c, st); break;
+        case 1: rc = f32_launch_family<1>(k, c, st); break;
+        case 2: rc = f32_launch_family<2>(k, c, st); break;
+        case 3: rc = f32_launch_family<3>(k, c, st); break;
+        case 4: rc = f32_launch_family<4>(k, c, st); break;
+        case 7: rc = f32_launch_family<7>(k, c, st); break;
+        case 8: rc = f32_launch_family<8>(k, c, st); break;
         default: set_error("conv1d: unsupported kernel size"); return RAVE_ERR_UNSUPPORTED;
     }
     if (rc != RAVE_OK || k.S <= 1) return rc;
@@ -585,3 +598,4 @@ extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
     launch(conv1d_splitk_reduce_kernel<0>, dim3(blocks), dim3(256), 0, st, k);
     return launch_status("conv1d_splitk_reduce_kernel");
 }
+#endif  // RAVE_F32_KT

@@ -59,7 +59,7 @@ template <int KT> struct SInfo {
     static constexpr int CPC = VC / S;             // real input channels per chunk
 };
 
-static inline int split_cpc(int taps) {
+[[maybe_unused]] static inline int split_cpc(int taps) {
     switch (taps) {
         case 1: return SInfo<1>::CPC;
         case 2: return SInfo<2>::CPC;
@@ -70,7 +70,7 @@ static inline int split_cpc(int taps) {
         default: return 0;
     }
 }
-static inline int split_ksc(int taps) {
+[[maybe_unused]] static inline int split_ksc(int taps) {
     switch (taps) {
         case 1: return SInfo<1>::KSC;
         case 2: return SInfo<2>::KSC;
@@ -683,6 +683,90 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
     }
 }
 
+// --------------------------------------------------------------------- tiles
+struct SplitCfg {
+    int tile, S, sep;     // kSplitTiles index, K-splits, separate reduce launch
+};
+
+// Tiles (BM rows x BN columns, wave WM x WN, KG waves per output tile).  The
+// table index is part of the launch-configuration code, so retired shapes keep
+// their slot: only the rows marked built are instantiated (the 32 x 64 wave
+// tiles are what the autotuner picks on every RAVE layer, profiles/r01_final/
+// tuning.json; the retired 64-row / 128-column wave tiles never won).
+constexpr int kNumSplitTiles = 16;
+[[maybe_unused]] constexpr int kSplitTiles[kNumSplitTiles][5] = {   // BM, BN, WM, KG, WN
+    {128, 128, 32, 1, 128}, {64, 256, 32, 1, 128}, {64, 128, 32, 1, 128}, {256, 64, 64, 1, 64},
+    {128, 64, 64, 1, 64},   {64, 64, 64, 1, 64},   {128, 64, 64, 2, 64},  {64, 128, 32, 2, 128},
+    {128, 128, 32, 2, 128}, {256, 64, 64, 2, 64},  {128, 64, 32, 1, 64},  {64, 128, 32, 1, 64},
+    {256, 64, 32, 1, 64},   {256, 64, 32, 2, 64},  {128, 64, 32, 2, 64},  {64, 128, 32, 2, 64}};
+[[maybe_unused]] constexpr bool kSplitTileBuilt[kNumSplitTiles] = {false, false, false, false, false, false, false, false,
+                                                  false, false, true,  true,  true,  true,  true,  true};
+[[maybe_unused]] constexpr int kSplitDefaultTile = 10;
+
+// Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>, IC<WN>) for a built tile index ti
+// (compile-time dispatch; callers check kSplitTileBuilt first).
+template <typename Fn>
+static inline auto with_tile(int ti, Fn&& f) {
+    switch (ti) {
+        case 11: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{});
+        case 12: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});
+        case 13: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{});
+        case 14: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{});
+        case 15: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{});
+        default: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});   // 10
+    }
+}
+
+// Launch of one (family, activation) for a tile index.  The kernel
+// instantiations are spread over separate translation units (the Makefile
+// compiles this file once per (KT, SNAKE, XV) with -DRAVE_SPLIT_KT / _SNAKE / _XV,
+// and once without them for the host side) so the build runs in parallel.
+template <int KT, bool SNAKE, bool XV>
+int split_launch_inst(ConvKArgs k, int tile, hipStream_t st);
+
+#ifdef RAVE_SPLIT_KT
+template <int KT, int BM, int BN, int WM, int KG, int WN, bool SNAKE, bool XV>
+static int split_launch_xv(ConvKArgs k, hipStream_t st) {
+    using G = SGeo<KT, BM, BN, WM, XV, KG, WN>;
+    if constexpr (!G::VALID) {
+        set_error("conv1d(split16): tile exceeds LDS or the vmcnt range");
+        return RAVE_ERR_UNSUPPORTED;
+    } else {
+        if (k.XW > G::XW_MAX) {
+            set_error("conv1d(split16): dilation too large for the staged window");
+            return RAVE_ERR_UNSUPPORTED;
+        }
+        constexpr size_t lds = (size_t)G::LDS_ALL;
+        static_assert(lds <= 160 * 1024, "LDS budget");
+        dim3 grid(k.gx * k.gy * k.B * k.S);
+        auto kern = conv1d_split_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN>;
+        if (lds > 64 * 1024) {
+            static bool done = false;
+            if (!done) {
+                RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                done = true;
+            }
+        }
+        launch(kern, grid, dim3(G::NT), (uint32_t)lds, st, k);
+        return launch_status("conv1d_split_kernel");
+    }
+}
+
+template <int KT, bool SNAKE, bool XV>
+int split_launch_inst(ConvKArgs k, int tile, hipStream_t st) {
+    return with_tile(tile, [&](auto bm, auto bn, auto wm, auto kg, auto wn) {
+        constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
+                      KG = decltype(kg)::value, WN = decltype(wn)::value;
+        return split_launch_xv<KT, BM, BN, WM, KG, WN, SNAKE, XV>(k, st);
+    });
+}
+template int split_launch_inst<RAVE_SPLIT_KT, (RAVE_SPLIT_SNAKE != 0), (RAVE_SPLIT_XV != 0)>(ConvKArgs, int,
+                                                                                              hipStream_t);
+
+}  // namespace rave
+#else   // ------------------------------------------------------- host side
+
 // Sum the split-K slabs in split order (fixed order: deterministic), then
 // bias / residual / ConvT interleave.  One thread = 4 consecutive floats of
 // the flat [B][M][U] slab image (U % 4 == 0 when vec_p), grid-stride: every
@@ -722,44 +806,9 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(ConvKArgs a) {
     }
 }
 
-// --------------------------------------------------------------------- host side
-struct SplitCfg {
-    int tile, S, sep;     // kSplitTiles index, K-splits, separate reduce launch
-};
-
-// Tile + split-K choice.  Tiles (BM rows x BN columns, wave WM x WN,
-// KG waves per output tile): least padding with the most waves per workgroup
+// Tile + split-K choice: least padding with the most waves per workgroup
 // that still fills the chip; K split over workgroups (fp32 slabs, fixed-order
 // combine) when the output alone cannot give every SIMD a wave.
-constexpr int kNumSplitTiles = 16;
-constexpr int kSplitTiles[kNumSplitTiles][5] = {   // BM, BN, WM, KG, WN
-    {128, 128, 32, 1, 128}, {64, 256, 32, 1, 128}, {64, 128, 32, 1, 128}, {256, 64, 64, 1, 64},
-    {128, 64, 64, 1, 64},   {64, 64, 64, 1, 64},   {128, 64, 64, 2, 64},  {64, 128, 32, 2, 128},
-    {128, 128, 32, 2, 128}, {256, 64, 64, 2, 64},  {128, 64, 32, 1, 64},  {64, 128, 32, 1, 64},
-    {256, 64, 32, 1, 64},   {256, 64, 32, 2, 64},  {128, 64, 32, 2, 64},  {64, 128, 32, 2, 64}};
-
-// Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>, IC<WN>) for tile index ti (compile-time dispatch).
-template <typename Fn>
-static auto with_tile(int ti, Fn&& f) {
-    switch (ti) {
-        case 0: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<128>{});
-        case 1: return f(IC<64>{}, IC<256>{}, IC<32>{}, IC<1>{}, IC<128>{});
-        case 2: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<128>{});
-        case 3: return f(IC<256>{}, IC<64>{}, IC<64>{}, IC<1>{}, IC<64>{});
-        case 4: return f(IC<128>{}, IC<64>{}, IC<64>{}, IC<1>{}, IC<64>{});
-        case 5: return f(IC<64>{}, IC<64>{}, IC<64>{}, IC<1>{}, IC<64>{});
-        case 6: return f(IC<128>{}, IC<64>{}, IC<64>{}, IC<2>{}, IC<64>{});
-        case 7: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<128>{});
-        case 8: return f(IC<128>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<128>{});
-        case 9: return f(IC<256>{}, IC<64>{}, IC<64>{}, IC<2>{}, IC<64>{});
-        case 10: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});
-        case 11: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{});
-        case 12: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});
-        case 13: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{});
-        case 14: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{});
-        default: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{});
-    }
-}
 static inline int tile_waves(int ti) {   // waves per workgroup
     const int* t = kSplitTiles[ti];
     return (t[0] / t[2]) * (t[1] / t[4]) * t[3];
@@ -774,6 +823,7 @@ static bool split_tile_fits(int idx) {   // both DMA variants must fit
     });
 }
 static bool split_fits(int taps, int idx) {
+    if (idx < 0 || idx >= kNumSplitTiles || !kSplitTileBuilt[idx]) return false;
     switch (taps) {
         case 1: return split_tile_fits<1>(idx);
         case 2: return split_tile_fits<2>(idx);
@@ -789,10 +839,11 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
     auto waste = [&](int bm, int bn) {
         return double(ceil_div(M, bm) * bm) * double(ceil_div(U, bn) * bn) / (double(M) * double(U));
     };
-    SplitCfg best{5, 1, 0};
+    SplitCfg best{kSplitDefaultTile, 1, 0};
     double bscore = 1e30;
-    for (int ti = 0; ti < 6; ++ti) {                // the heuristic keeps to the KG = 1 tiles
+    for (int ti = 0; ti < kNumSplitTiles; ++ti) {   // the heuristic keeps to the KG = 1 tiles
         const int* c = all[ti];
+        if (c[3] != 1) continue;
         if (!split_fits(taps, ti)) continue;
         if (split_row < M && split_row % c[2] != 0) continue;      // a wave never straddles ConvT groups
         const int nw = tile_waves(ti);
@@ -813,36 +864,6 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
     return best;
 }
 
-template <int KT, int BM, int BN, int WM, int KG, int WN, bool XV>
-static int split_launch_xv(ConvKArgs k, hipStream_t st) {
-    using G = SGeo<KT, BM, BN, WM, XV, KG, WN>;
-    if constexpr (!G::VALID) {
-        set_error("conv1d(split16): tile exceeds LDS or the vmcnt range");
-        return RAVE_ERR_UNSUPPORTED;
-    } else {
-    if (k.XW > G::XW_MAX) {
-        set_error("conv1d(split16): dilation too large for the staged window");
-        return RAVE_ERR_UNSUPPORTED;
-    }
-    constexpr size_t lds = (size_t)G::LDS_ALL;
-    static_assert(lds <= 160 * 1024, "LDS budget");
-    dim3 grid(k.gx * k.gy * k.B * k.S);
-    const bool snake = k.act == RAVE_ACT_SNAKE;
-    auto kern = snake ? conv1d_split_kernel<KT, BM, BN, WM, true, XV, KG, WN>
-                      : conv1d_split_kernel<KT, BM, BN, WM, false, XV, KG, WN>;
-    if (lds > 64 * 1024) {
-        static bool done[2] = {false, false};
-        if (!done[snake]) {
-            RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            done[snake] = true;
-        }
-    }
-    launch(kern, grid, dim3(G::NT), (uint32_t)lds, st, k);
-    return launch_status("conv1d_split_kernel");
-    }
-}
-
 template <int KT>
 static int split_launch_family(ConvKArgs k, const SplitCfg& c, hipStream_t st) {
     const int* t = kSplitTiles[c.tile];
@@ -850,12 +871,10 @@ static int split_launch_family(ConvKArgs k, const SplitCfg& c, hipStream_t st) {
     k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
     const unsigned rl = (unsigned)(k.XW * SFam<KT>::S);
     k.rl_magic = (unsigned)((0x100000000ull + rl - 1) / rl);
-    return with_tile(c.tile, [&](auto bm, auto bn, auto wm, auto kg, auto wn) {
-        constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
-                      KG = decltype(kg)::value, WN = decltype(wn)::value;
-        return k.x_vec ? split_launch_xv<KT, BM, BN, WM, KG, WN, true>(k, st)
-                       : split_launch_xv<KT, BM, BN, WM, KG, WN, false>(k, st);
-    });
+    const bool snake = k.act == RAVE_ACT_SNAKE;
+    auto fn = snake ? (k.x_vec ? split_launch_inst<KT, true, true> : split_launch_inst<KT, true, false>)
+                    : (k.x_vec ? split_launch_inst<KT, false, true> : split_launch_inst<KT, false, false>);
+    return fn(k, c.tile, st);
 }
 
 static int split_prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
@@ -1095,3 +1114,4 @@ extern "C" int rave_conv1d_split_pack_weight(const float* w, int c_in, int c_out
     for (int m = 0; m < Mpad; ++m) rs[m] = (float)std::ldexp(1.0, -(ex[m] + 11));
     return RAVE_OK;
 }
+#endif  // RAVE_SPLIT_KT
