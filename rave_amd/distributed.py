@@ -14,7 +14,7 @@ list form of all_gather is used.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -62,17 +62,24 @@ class ShardedRunner:
         quarter of the int64 bytes) and are widened back after the gather;
       * ``"decode"`` (C5) -- decode of the local latent shard; no exchange.
 
-    Each rank decodes its own rows of the gathered tensor.  ``model`` is
+    Shards may differ in size (``shard_bounds`` of a batch that does not divide
+    by the world size).  ``shard_sizes`` -- every rank's shard size, identical
+    on all ranks -- fixes them up front; without it the sizes are all-gathered
+    at every step (one 8-byte collective).  Unequal shards travel padded to the
+    largest and are compacted after the gather.  Each rank decodes its own
+    rows (the local tensor, so the decode does not wait for the exchange) and
+    addresses AdaIN buffer rows by its global batch offset.  ``model`` is
     anything with the matching methods (rave_amd.RAVE on GPU)."""
 
     MODES = ("latent", "codes", "decode")
 
-    def __init__(self, model, group=None, mode: str = "latent"):
+    def __init__(self, model, group=None, mode: str = "latent", shard_sizes: Optional[List[int]] = None):
         if mode not in self.MODES:
             raise ValueError(f"mode must be one of {self.MODES}")
         self.model = model
         self.group = group
         self.mode = mode
+        self.shard_sizes = list(shard_sizes) if shard_sizes is not None else None
         self._all: Optional[torch.Tensor] = None
 
     def _narrow_codes(self) -> bool:
@@ -80,29 +87,54 @@ class ShardedRunner:
         return (self.mode == "codes" and rvq is not None and rvq.codebook_size <= 32767
                 and dist.get_backend(self.group) == "nccl")
 
-    def _gather(self, t: torch.Tensor) -> torch.Tensor:
+    def sizes(self, b: int, device) -> List[int]:
+        """Every rank's shard size."""
+        rank, size = world()
+        if size == 1:
+            return [b]
+        if self.shard_sizes is not None:
+            if len(self.shard_sizes) != size or self.shard_sizes[rank] != b:
+                raise ValueError(f"shard_sizes {self.shard_sizes} do not match rank {rank}'s batch {b} "
+                                 f"at world size {size}")
+            return self.shard_sizes
+        dev = device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        mine = torch.tensor([b], dtype=torch.int64, device=dev)
+        out = torch.empty(size, dtype=torch.int64, device=dev)
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(out, mine, group=self.group)
+        else:
+            dist.all_gather(list(out.chunk(size)), mine, group=self.group)
+        return [int(v) for v in out.tolist()]
+
+    def _gather(self, t: torch.Tensor, sizes: List[int]) -> torch.Tensor:
         rank, size = world()
         if size == 1:
             return t
         narrow = self._narrow_codes()
         src = t.to(torch.int16) if narrow else t
-        shape = (size * src.shape[0],) + tuple(src.shape[1:])
+        bmax = max(sizes)
+        if src.shape[0] < bmax:                  # unequal shards travel padded to the largest
+            pad = torch.zeros((bmax - src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+            src = torch.cat([src, pad], 0)
+        shape = (size * bmax,) + tuple(src.shape[1:])
         if self._all is None or tuple(self._all.shape) != shape or self._all.dtype != src.dtype:
             self._all = torch.empty(shape, dtype=src.dtype, device=src.device)
         out = gather_latents(src, self._all, self.group)
+        if any(n != bmax for n in sizes):
+            out = torch.cat([out[r * bmax:r * bmax + n] for r, n in enumerate(sizes)], 0)
         return out.to(t.dtype) if narrow else out
 
     def step(self, x_local: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """(what every rank holds after the exchange, this rank's decoded audio)."""
-        rank, size = world()
         if self.mode == "decode":
             return x_local, self.model.decode(x_local)
+        rank, _ = world()
+        sizes = self.sizes(x_local.shape[0], x_local.device)
         if getattr(self.model, "adain", None) is not None:
             # AdaIN buffer rows follow the global batch index (rave/blocks.py:886-891)
-            self.model.adain_row0 = rank * x_local.shape[0]
-        b = x_local.shape[0]
+            self.model.adain_row0 = sum(sizes[:rank])
         if self.mode == "codes":
-            t_all = self._gather(self.model.encode_codes(x_local))
-            return t_all, self.model.decode_codes(t_all[rank * b:(rank + 1) * b])
-        t_all = self._gather(self.model.encode(x_local))
-        return t_all, self.model.decode(t_all[rank * b:(rank + 1) * b])
+            t = self.model.encode_codes(x_local)
+            return self._gather(t, sizes), self.model.decode_codes(t)
+        t = self.model.encode(x_local)
+        return self._gather(t, sizes), self.model.decode(t)

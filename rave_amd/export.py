@@ -88,10 +88,32 @@ class NNTildeRAVE:
         return self._attrs[name][0]
 
     def set_attribute(self, name: str, value) -> int:
+        """Store ``value`` as a 1-tuple.  Bool attributes take a bool, an int 0/1
+        or a 0-d tensor; int attributes an int or 0-d integer tensor.  Anything
+        else (e.g. the string 'False', which bool() would turn True) raises."""
         if name not in self._attrs:
             raise KeyError(name)
-        kind = type(self._attrs[name][0])
-        self._attrs[name] = (kind(value),)
+        if isinstance(value, tuple) and len(value) == 1:
+            value = value[0]
+        if isinstance(value, torch.Tensor):
+            if value.numel() != 1:
+                raise TypeError(f"{name}: expected a scalar, got a tensor of shape {tuple(value.shape)}")
+            value = value.item()
+        default = self._attrs[name][0]
+        if isinstance(default, bool):
+            if isinstance(value, bool):
+                pass
+            elif isinstance(value, int) and value in (0, 1):
+                value = bool(value)
+            else:
+                raise TypeError(f"{name}: expected a bool, got {value!r}")
+        elif isinstance(default, int):
+            if isinstance(value, bool) or not isinstance(value, int):
+                if isinstance(value, float) and value.is_integer():
+                    value = int(value)
+                else:
+                    raise TypeError(f"{name}: expected an int, got {value!r}")
+        self._attrs[name] = (value,)
         return 0
 
     def __getattr__(self, item: str):
@@ -103,15 +125,46 @@ class NNTildeRAVE:
             return lambda v: self.set_attribute(item[4:], v)
         raise AttributeError(item)
 
+    # ------------------------------------------------------------ AdaIN controls
+    def update_adain(self) -> None:
+        """ScriptedRAVE.update_adain (scripts/export.py:248-265): the learn
+        flags of every AdaIN module follow learn_target / learn_source, a set
+        reset_* flag resets that side's statistics once and is cleared."""
+        ad = getattr(self.model, "adain", None)
+        if ad is None:
+            return
+        ad.set_learn(learn_x=self.get_attribute("learn_source"), learn_y=self.get_attribute("learn_target"))
+        if self.get_attribute("reset_target"):
+            ad.reset_y()
+        if self.get_attribute("reset_source"):
+            ad.reset_x()
+        self._attrs["reset_source"] = (False,)
+        self._attrs["reset_target"] = (False,)
+
     # ------------------------------------------------------------ methods
-    def _streams(self, batch: int):
+    def _enc_streamer(self, batch: int):
+        """The encode stream; created (zeroed) on first use or a batch change,
+        without touching the decode stream's caches."""
         from rave_amd.streaming import StreamingRAVE
         if self._enc_stream is None or self._enc_stream.B != batch:
             self._enc_stream = StreamingRAVE(self.model, batch=batch, block=self.block)
-        nd = 2 * batch if self.stereo else batch
-        if self._dec_stream is None or self._dec_stream.B != nd:
-            self._dec_stream = StreamingRAVE(self.model, batch=nd, block=self.block)
-        return self._enc_stream, self._dec_stream
+        return self._enc_stream
+
+    def _dec_streamer(self, batch: int):
+        from rave_amd.streaming import StreamingRAVE
+        if self._dec_stream is None or self._dec_stream.B != batch:
+            self._dec_stream = StreamingRAVE(self.model, batch=batch, block=self.block)
+        return self._dec_stream
+
+    def _blocks(self, t: torch.Tensor, per_block: int) -> List[torch.Tensor]:
+        """Split a host buffer into the stream's blocks (any multiple of the
+        block length is accepted, as cached_conv accepts any multiple of hop
+        once the plan's block is fixed)."""
+        T = t.shape[-1]
+        if T % per_block:
+            raise ValueError(f"streaming buffers must be a multiple of the block: {T} columns, "
+                             f"block {per_block} (configure NNTildeRAVE(block=...))")
+        return [t[..., i:i + per_block].contiguous() for i in range(0, T, per_block)]
 
     def _check(self, name: str, t: torch.Tensor) -> None:
         c = self._methods[name][0]
@@ -119,26 +172,35 @@ class NNTildeRAVE:
             raise ValueError(f"{name}: expected (B, {c}, T), got {tuple(t.shape)}")
 
     def encode(self, x: torch.Tensor) -> torch.Tensor:
-        """scripts/export.py:298-314 (PQMF -> encoder on 6 bands -> cat speaker)."""
+        """scripts/export.py:298-314 (update_adain -> PQMF -> encoder on 6 bands
+        -> cat speaker)."""
         self._check("encode", x)
+        self.update_adain()
         if self.streaming:
-            return self._streams(x.shape[0])[0].encode(x)
+            st = self._enc_streamer(x.shape[0])
+            return torch.cat([st.encode(b) for b in self._blocks(x, self.block)], -1)
         return self.model.encode(x)
 
-    def decode(self, z: torch.Tensor) -> torch.Tensor:
-        """scripts/export.py:317-336: stereo decodes the batch twice and puts the
-        copies side by side as channels (L, R)."""
+    def decode(self, z: torch.Tensor, from_forward: bool = False) -> torch.Tensor:
+        """scripts/export.py:317-336: update_adain unless called from forward;
+        stereo decodes the batch twice and puts the copies side by side as
+        channels (L, R)."""
         self._check("decode", z)
-        B = z.shape[0]
+        if not from_forward:
+            self.update_adain()
         if self.stereo:
             z = torch.cat([z, z], 0)
-        y = self._streams(B)[1].decode(z.contiguous()) if self.streaming else self.model.decode(z)
+        if self.streaming:
+            st = self._dec_streamer(z.shape[0])
+            y = torch.cat([st.decode(b) for b in self._blocks(z, self.block // self.cfg.hop)], -1)
+        else:
+            y = self.model.decode(z)
         if self.stereo:
             y = torch.cat(y.chunk(2, 0), 1)
         return y
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.decode(self.encode(x))
+        return self.decode(self.encode(x), from_forward=True)
 
     __call__ = forward
 

@@ -37,13 +37,18 @@ def design_bank(attenuation: float = 100.0, n_band: int = 16) -> np.ndarray:
     """hk (n_band, next_pow2(N)) float32, as CachedPQMF registers it."""
     from scipy.optimize import fmin
     wc = fmin(lambda w: _objective(w, attenuation, n_band, None), 1 / n_band, disp=0)[0]
-    h = _kaiser(wc, attenuation).astype(np.float32)
+    # get_qmf_bank (rave/pqmf.py:32-52) runs on torch int64 / float32 CPU
+    # tensors: the modulation argument, the cosine and 2*h*mod are float32
+    # operations, so they are evaluated with the same torch ops (bit-exact with
+    # the reference's hk, tests/test_host.py); float64 differs by ~1.7e-7.
+    import torch
+    h = torch.from_numpy(_kaiser(wc, attenuation)).float()
     N = h.shape[-1]
-    k = np.arange(n_band).reshape(-1, 1)
-    t = np.arange(-(N // 2), N // 2 + 1)
-    phase = ((-1.0) ** k) * math.pi / 4
-    mod = np.cos((2 * k + 1) * math.pi / (2 * n_band) * t + phase).astype(np.float32)
-    hk = (2 * h * mod).astype(np.float32)
+    k = torch.arange(n_band).reshape(-1, 1)
+    t = torch.arange(-(N // 2), N // 2 + 1)
+    phase = (-1) ** k * math.pi / 4
+    mod = torch.cos((2 * k + 1) * math.pi / (2 * n_band) * t + phase)
+    hk = (2 * h * mod).numpy()
     pad = 2 ** math.ceil(math.log2(N)) - N
     return np.pad(hk, ((0, 0), (pad // 2, pad // 2 + pad % 2)))
 

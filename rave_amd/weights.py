@@ -13,13 +13,14 @@
   ``w = g * v / ||v||`` with the norm over every dim but 0.  For a
   ConvTranspose1d dim 0 is ``in_channels`` (weight ``(C_in, C_out, k)``).
 * ``load_checkpoint_state`` accepts a Lightning checkpoint dict (``state_dict``
-  or ``callbacks.EMA``; scripts/export.py:558-569) or a bare state_dict.
+  or ``callbacks.EMA``; scripts/export.py:558-569) or a bare state_dict, with
+  the reference's strict=False semantics and weight-norm-folded weights.
 """
 from __future__ import annotations
 
 import zlib
 from collections import OrderedDict
-from typing import Dict, Mapping
+from typing import Dict, Mapping, Optional
 
 import numpy as np
 
@@ -99,15 +100,53 @@ def to_numpy_state(state: Mapping) -> Dict[str, np.ndarray]:
     return out
 
 
-def load_checkpoint_state(ckpt: Mapping, use_ema: bool = False) -> Dict[str, np.ndarray]:
-    """Parameter dict from a Lightning checkpoint (scripts/export.py:558-569)."""
-    if use_ema:
-        state = ckpt["callbacks"]["EMA"]
+def load_checkpoint_state(ckpt: Mapping, use_ema: bool = False, cfg: Optional[RaveConfig] = None,
+                          base: Optional[Mapping[str, np.ndarray]] = None) -> Dict[str, np.ndarray]:
+    """Parameter dict from a Lightning checkpoint (scripts/export.py:558-569).
+
+    * ``use_ema`` and an ``EMA`` entry under ``checkpoint["callbacks"]`` -> the
+      EMA callback's weights, else ``checkpoint["state_dict"]`` (a bare
+      state_dict is accepted too), as export.py chooses.
+    * Without ``cfg`` every entry is returned (numpy).  With ``cfg`` the result
+      holds exactly the hot path's parameters (graph.param_shapes), shapes
+      checked.  Like the reference's ``load_state_dict(..., strict=False)``,
+      keys of other modules (speaker encoder, discriminators) are ignored and
+      a parameter the checkpoint lacks keeps its value in ``base`` (the EMA
+      callback stores parameters only, not buffers such as RVQ codebooks);
+      without ``base`` a missing parameter raises KeyError.
+    * A weight already folded by ``remove_weight_norm`` (``<name>.weight``
+      where the graph holds ``weight_g`` / ``weight_v``, scripts/export.py:
+      598-600) is taken as ``weight_v = weight``, ``weight_g = ||weight||``
+      (norm over every dim but 0), which folds back to the same weight."""
+    callbacks = ckpt.get("callbacks") if isinstance(ckpt, Mapping) else None
+    if use_ema and isinstance(callbacks, Mapping) and "EMA" in callbacks:
+        state = callbacks["EMA"]
     elif "state_dict" in ckpt:
         state = ckpt["state_dict"]
     else:
         state = ckpt
-    return to_numpy_state(state)
+    state = to_numpy_state(state)
+    if cfg is None:
+        return state
+    out: Dict[str, np.ndarray] = {}
+    for name, shape in param_shapes(cfg).items():
+        if name in state:
+            val = np.asarray(state[name], np.float32)
+        elif name.endswith((".weight_g", ".weight_v")) and name.rsplit(".", 1)[0] + ".weight" in state:
+            w = np.asarray(state[name.rsplit(".", 1)[0] + ".weight"], np.float32)
+            if name.endswith("_v"):
+                val = w
+            else:
+                w64 = w.astype(np.float64)
+                val = np.sqrt((w64.reshape(w64.shape[0], -1) ** 2).sum(1)).reshape(shape).astype(np.float32)
+        elif base is not None and name in base:
+            val = np.asarray(base[name], np.float32)
+        else:
+            raise KeyError(f"checkpoint has no parameter {name} (and no base value was given)")
+        if tuple(val.shape) != tuple(shape):
+            raise ValueError(f"{name}: expected shape {shape}, got {val.shape}")
+        out[name] = val
+    return out
 
 
 def check_params(cfg: RaveConfig, params: Mapping[str, np.ndarray]) -> None:

@@ -60,25 +60,27 @@ class _OracleCodesModel:
         return torch.from_numpy(self.o.decode(z.numpy()).astype(np.float32))
 
 
-def _worker(rank, size, port, x_all, q, mode="latent"):
+def _worker(rank, size, port, x_all, q, mode="latent", fixed_sizes=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=size)
     try:
         from rave_amd.distributed import ShardedRunner, shard_bounds
-        lo, hi = shard_bounds(x_all.shape[0], rank, size)
+        spans = [shard_bounds(x_all.shape[0], r, size) for r in range(size)]
+        lo, hi = spans[rank]
         model = _OracleModel() if mode == "latent" else _OracleCodesModel()
-        runner = ShardedRunner(model, mode=mode)
+        sizes = [h - l for l, h in spans] if fixed_sizes else None
+        runner = ShardedRunner(model, mode=mode, shard_sizes=sizes)
         z_all, y = runner.step(x_all[lo:hi])
         q.put((rank, z_all.numpy(), y.numpy()))
     finally:
         dist.destroy_process_group()
 
 
-def _run_world2(x_all, mode):
+def _run_world2(x_all, mode, fixed_sizes=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, x_all, q, mode)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, x_all, q, mode, fixed_sizes)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in procs]
@@ -114,26 +116,26 @@ def test_sharded_decode_mode_has_no_exchange():
         ShardedRunner(m, mode="tokens")
 
 
-def test_sharded_encode_gather_decode_matches_single_process():
+@pytest.mark.parametrize("n,fixed", [(4, True), (3, False)])
+def test_sharded_encode_gather_decode_matches_single_process(n, fixed):
+    """Equal shards with the sizes given up front, and an odd batch (2 + 1
+    clips) whose sizes are exchanged and whose shards travel padded."""
+    from rave_amd.distributed import shard_bounds
     rng = np.random.default_rng(0)
-    x_all = torch.from_numpy((0.2 * rng.standard_normal((4, 1, 2048))).astype(np.float32))
+    x_all = torch.from_numpy((0.2 * rng.standard_normal((n, 1, 2048))).astype(np.float32))
     ref_model = _OracleModel()
     z_ref = ref_model.encode(x_all)
     y_ref = ref_model.decode(z_ref)
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, x_all, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=120) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    res.sort(key=lambda t: t[0])
-    for rank, z_all, y in res:
+    for rank, z_all, y in _run_world2(x_all, "latent", fixed_sizes=fixed):
+        lo, hi = shard_bounds(n, rank, 2)
         np.testing.assert_allclose(z_all, z_ref.numpy(), atol=1e-6)     # every rank holds all latents
-        np.testing.assert_allclose(y, y_ref.numpy()[rank * 2:(rank + 1) * 2], atol=1e-6)
+        np.testing.assert_allclose(y, y_ref.numpy()[lo:hi], atol=1e-6)
+
+
+def test_shard_sizes_must_match():
+    from rave_amd.distributed import ShardedRunner
+    r = ShardedRunner(_OracleModel(), shard_sizes=[2, 2])
+    assert r.sizes(5, torch.device("cpu")) == [5]          # single process: no exchange
 
 
 def test_shard_bounds_cover_batch():

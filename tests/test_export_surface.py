@@ -49,3 +49,49 @@ def test_attributes_store_one_tuples():
         w.get_volume()
     with pytest.raises(ValueError):
         w.register_method("bad", 2, 1, 1, 1, ["one"], ["out"])
+
+
+def test_bool_attributes_reject_strings():
+    w = NNTildeRAVE(_Cfg(rcfg.v2()))
+    with pytest.raises(TypeError):
+        w.set_learn_target("False")           # bool('False') would be True
+    with pytest.raises(TypeError):
+        w.set_record(2)
+    with pytest.raises(TypeError):
+        w.set_speaker("3")
+    assert w.set_learn_target(1) == 0 and w.get_learn_target() is True
+    assert w.set_learn_target((False,)) == 0 and w.get_learn_target() is False
+    import torch
+    assert w.set_speaker(torch.tensor(2)) == 0 and w.get_speaker() == 2
+
+
+class _Adain:
+    """Records the controls ScriptedRAVE.update_adain drives (export.py:248-265)."""
+
+    def __init__(self):
+        self.calls = []
+
+    def set_learn(self, learn_x=None, learn_y=None):
+        self.calls.append(("learn", learn_x, learn_y))
+
+    def reset_x(self):
+        self.calls.append(("reset_x",))
+
+    def reset_y(self):
+        self.calls.append(("reset_y",))
+
+
+def test_update_adain_applies_flags_once():
+    m = _Cfg(rcfg.v2())
+    m.adain = _Adain()
+    w = NNTildeRAVE.__new__(NNTildeRAVE)
+    w.__init__(_Cfg(rcfg.v2()))            # build without AdaIN (stereo check), then attach
+    w.model = m
+    w.set_learn_target(True)
+    w.set_reset_source(True)
+    w.update_adain()
+    assert m.adain.calls == [("learn", False, True), ("reset_x",)]
+    assert w.get_reset_source() is False and w.get_learn_target() is True
+    m.adain.calls.clear()
+    w.update_adain()                       # the reset fired once
+    assert m.adain.calls == [("learn", False, True)]

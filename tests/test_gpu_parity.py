@@ -323,6 +323,42 @@ def test_v2_full_clip_vs_oracle(dev, precision):
 
 
 @pytest.mark.parametrize("precision", ["f32", "auto"])
+def test_discrete_codes_c4_shard_vs_oracle(dev, precision):
+    """BASELINE config 4's per-GPU shard (8 x 65536 of the B=64 batch): the
+    whole encode_codes -> decode_codes path, two clips checked against the
+    float64 oracle.  Indices equal the oracle's wherever its top-2 distance
+    gap exceeds the fp32 tie margin; decode_codes of the GPU's own indices
+    matches the oracle's decode of those indices within 1e-4."""
+    from oracle.rave_oracle import Oracle
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.discrete()
+    params, spk = init_params(cfg, 3), init_speaker(cfg, 3)
+    B, T = 8, 65536
+    n = np.arange(T)
+    rng = np.random.default_rng(4)
+    x = np.stack([0.3 * np.sin(2 * np.pi * (220 + 55 * b) * n / 48000) + 0.1 * rng.standard_normal(T)
+                  for b in range(B)])[:, None, :].astype(np.float32)
+    m = RAVE(cfg, params, spk, device=dev, precision=precision)
+    idx = m.encode_codes(torch.from_numpy(x).to(dev))
+    y = m.decode_codes(idx)
+    torch.cuda.synchronize()
+    idx, y = idx.cpu().numpy(), y.cpu().numpy()
+    o = Oracle(cfg, params, spk, hk=m.hk)
+    for b in (0, 5):
+        ref, gap = o.rvq_encode(o.encode(x[b:b + 1]), return_gaps=True)
+        gap = gap.reshape(cfg.rvq.num_quantizers, 1, -1).transpose(1, 0, 2)
+        mism = idx[b:b + 1] != ref
+        assert (gap[mism] < 1e-3).all(), (b, int(mism.sum()))
+        yr = o.decode(o.cat_speaker(o.rvq_decode(idx[b:b + 1])))
+        ey = maxabs(y[b:b + 1], yr)
+        print(f"\n[parity] discrete C4 shard clip {b} {precision}: index mismatches {int(mism.sum())} "
+              f"(all within the tie margin), y max-abs {ey:.3e}")
+        assert ey < TOL
+
+
+@pytest.mark.parametrize("precision", ["f32", "auto"])
 def test_batch_independence_and_determinism(dev, precision):
     """At BASELINE config 2 size (16 x 65536), in the bench's precision mode too:
     each clip of the batch equals the same clip run alone (no cross-sample
@@ -823,7 +859,9 @@ def test_nn_tilde_surface_streaming_and_stereo(dev):
         y = w.forward(x)
         y_ref = ref.forward(x)
         assert tuple(y.shape) == (1, 2, 2048)
-        assert torch.equal(y[:, :1], y_ref) and torch.equal(y[:, 1:], y_ref)
+        assert torch.equal(y[:, :1], y[:, 1:])                 # L == R bitwise
+        # batch 2 vs batch 1 may pick other tiles / K-splits: equal up to summation order
+        assert float((y[:, :1] - y_ref).abs().max()) < 1e-6
     cfg2 = rcfg.v2()
     m2 = RAVE(cfg2, init_params(cfg2, 6), init_speaker(cfg2, 6), device=dev)
     w2 = NNTildeRAVE(m2)
