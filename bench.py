@@ -62,9 +62,9 @@ FAMILIES = {
 }
 
 
-def op_family(kind: int, scalars: dict) -> str:
+def op_family(kind: int, precision: int) -> str:
     from rave_amd import _native as N
-    prec = "split16" if scalars.get("precision", 0) == N.PREC_SPLIT16 else "f32"
+    prec = "split16" if precision == N.PREC_SPLIT16 else "f32"
     if kind == N.OP_CONV:
         return "conv_" + prec
     if kind == N.OP_UNIT:
@@ -162,8 +162,9 @@ def run_mode(a, cfg, params, spk, precision, x, dev, world, rank, log_ops):
     def step():
         return runner.step(x)[1]
 
-    pe = model._encode_plan(B, T)
-    pd = model._decode_plan(B, Fz)
+    from rave_amd.model import DECODE, ENCODE
+    plans = ((ENCODE, T), (DECODE, Fz))
+    ops = {w: model.ops(w, B, t) for w, t in plans}          # builds (and autotunes) both plans
     if a.tuning_out and rank == 0 and precision == a.precision:
         with open(a.tuning_out, "w") as fh:
             json.dump(model.tuning(), fh)
@@ -188,13 +189,13 @@ def run_mode(a, cfg, params, spk, precision, x, dev, world, rank, log_ops):
     value = world * B * T * a.steps / el
     res = {"value": round(value, 1), "ms_per_step": round(1e3 * el / a.steps, 4),
            "x_realtime": round(value / SR, 1), "dtype": DTYPE[precision]}
-    ops = {}
-    for plan in (pe, pd):
-        for sym in plan.sym:
-            fam = op_family(sym[0], sym[2])
+    launches = {}
+    for w, _ in plans:
+        for o in ops[w]:
+            fam = op_family(o["kind"], o["precision"])
             if fam in FAMILIES:
-                ops[fam] = ops.get(fam, 0) + 1
-    res["gemm_launches_by_family"] = ops
+                launches[fam] = launches.get(fam, 0) + 1
+    res["gemm_launches_by_family"] = launches
     if a.no_profile:
         return res, y
 
@@ -203,24 +204,25 @@ def run_mode(a, cfg, params, spk, precision, x, dev, world, rank, log_ops):
     # inside the kernels' own dispatch packets (hipExtLaunchKernelGGL on the
     # plan's stream, no marker packets, no host syncs).  Kept out of the timed
     # pass above, whose wall time the event bookkeeping would stretch (~15 %).
-    pe.profile(a.steps)
-    pd.profile(a.steps)
+    for w, t in plans:
+        model.profile(w, B, t, a.steps)
     for _ in range(a.steps):
         step()
     torch.cuda.synchronize()
-    te, ne = pe.op_times()
-    td, nd = pd.op_times()
-    pe.profile(0)
-    pd.profile(0)
-    if ne != a.steps or nd != a.steps:
-        raise RuntimeError(f"profiled {ne}/{nd} runs, expected {a.steps}")
-    te /= a.steps
-    td /= a.steps
+    times = {}
+    for w, t in plans:
+        tm, nr = model.op_times(w, B, t)
+        model.profile(w, B, t, 0)
+        if nr != a.steps:
+            raise RuntimeError(f"profiled {nr} runs of plan {w}, expected {a.steps}")
+        times[w] = tm / a.steps
+    te, td = times[ENCODE], times[DECODE]
     rows = []
     fams: dict = {}
-    for plan, tm in ((pe, te), (pd, td)):
-        for sym, lab, fl, nb, ms in zip(plan.sym, plan.labels, plan.flops, plan.nbytes, tm):
-            fam = op_family(sym[0], sym[2])
+    for w, _ in plans:
+        for o, ms in zip(ops[w], times[w]):
+            lab, fl, nb = o["label"], o["flops"], o["bytes"]
+            fam = op_family(o["kind"], o["precision"])
             rows.append((lab, fam, fl, nb, ms))
             if fam in FAMILIES:
                 f = fams.setdefault(fam, [0, 0.0, 0.0, 0.0])

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 7
+#define RAVE_ABI_VERSION 8
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 
@@ -398,6 +398,153 @@ int rave_plan_size(const rave_plan* plan);
  * of runs summed (>= 0) or an error status. */
 int rave_plan_profile(rave_plan* plan, int enable);
 int rave_plan_op_times(rave_plan* plan, float* ms, int n);
+
+/* y[i] = lo + (hi - lo) * u_i, u_i in [0, 1) from a counter-based hash of
+ * (seed, i): the device draw behind torch.rand_like of NoiseGeneratorV2
+ * (rave/blocks.py:287) when the caller supplies no noise, and the scratch
+ * inputs of the engine's launch-configuration timing. */
+int rave_fill_uniform(float* y, int64_t n, uint64_t seed, float lo, float hi, void* stream);
+
+/* ================================================================ model engine
+ * The whole RAVE.encode / decode / forward (rave/model.py:594-634) behind one
+ * handle, for hosts with no Python (nn~ is C++): the model graph of
+ * EncoderV2 / GeneratorV2 / NoiseGeneratorV2 (rave/blocks.py:244-291, 508-710)
+ * is built from the hyper-parameters below (the reference's gin bindings,
+ * rave/configs/v1.gin + v2.gin + causal / discrete / snake / adain / noise),
+ * weights are uploaded once (weight norm folded, packed per arithmetic), and
+ * each (call kind, batch, length) gets a launch plan built on first use
+ * (optionally autotuned, see RAVE_PREC_AUTO) and replayed afterwards.
+ *
+ * Threading: a model (and each of its streams) is driven by one host thread
+ * at a time; calls are asynchronous on the given stream.  The engine owns its
+ * device memory (weight arena, per-plan workspaces, AdaIN buffers); callers
+ * own the tensors they pass.  Plans of one model share nothing mutable, but a
+ * plan's workspace is reused by every call of that plan: two calls of the same
+ * kind and shape must not run concurrently on different streams.
+ */
+#define RAVE_MAX_RATIOS 8
+#define RAVE_MAX_DILATIONS 8
+enum { RAVE_PREC_AUTO = 2 };   /* per op the faster of F32 / SPLIT16, timed at plan build */
+
+typedef struct rave_model_config {
+    int32_t n_band;               /* PQMF bands (v1.gin: 16)                                */
+    int32_t enc_bands;            /* bands the encoder reads (v2.gin data_size: 6)           */
+    int32_t capacity;             /* 64 (v2), 96 (discrete)                                  */
+    int32_t latent_size;          /* 64 (v2), 128 (discrete)                                 */
+    int32_t kernel_size;          /* 3                                                       */
+    int32_t speaker_size;         /* 256: width of the constant speaker embedding            */
+    int32_t n_ratios;
+    int32_t ratios[RAVE_MAX_RATIOS];                        /* 4, 4, 2, 2                    */
+    int32_t n_dilations[RAVE_MAX_RATIOS];                   /* 3, 3, 3, 2                    */
+    int32_t dilations[RAVE_MAX_RATIOS][RAVE_MAX_DILATIONS]; /* 1 3 9 / 1 3 9 / 1 3 9 / 1 3   */
+    int32_t amplitude_modulation; /* 1 (v2.gin)                                              */
+    int32_t causal;               /* 0 centered, 1 causal (causal.gin)                       */
+    int32_t activation;           /* RAVE_ACT_LEAKY or RAVE_ACT_SNAKE (snake.gin)            */
+    int32_t adain;                /* AdaIN before every residual unit (adain.gin)            */
+    float leaky_slope;            /* 0.2                                                     */
+    int32_t conv_bias;            /* 1 (v1.gin cc.Conv1d.bias)                               */
+    int32_t convt_bias;           /* 0 (v1.gin cc.ConvTranspose1d.bias)                      */
+    int32_t noise;                /* NoiseGeneratorV2 present (noise.gin)                    */
+    int32_t noise_hidden;         /* 128                                                     */
+    int32_t noise_bands;          /* 5                                                       */
+    int32_t n_noise_ratios;
+    int32_t noise_ratios[RAVE_MAX_RATIOS];                  /* 2, 2, 2                       */
+    int32_t rvq_quantizers;       /* 0 = no RVQ; 16 (discrete.gin)                           */
+    int32_t rvq_codebook_size;    /* 1024                                                    */
+    int32_t fuse_units;           /* 1: fused Residual(DilatedUnit) / residual-stack kernels */
+} rave_model_config;
+
+/* One named parameter in the reference's state_dict naming
+ * (encoder.encoder.net.*, decoder.net.*, decoder.noise_module.net.*,
+ * encoder.rvq.layers.*._codebook.embed, pqmf.hk), fp32, host memory, torch
+ * layout; weight-normed convs take <name>.weight_g and <name>.weight_v. */
+typedef struct rave_param {
+    const char* name;
+    const float* data;
+    int64_t numel;
+} rave_param;
+
+typedef struct rave_model rave_model;
+typedef struct rave_stream rave_stream;
+
+/* Parameter table of a config: the count, and the i-th name / element count
+ * (pqmf.hk included).  Returns a negative status on a bad config. */
+int rave_model_param_count(const rave_model_config* cfg);
+int rave_model_param_info(const rave_model_config* cfg, int i, char* name, int name_cap, int64_t* numel);
+
+/* Create on the calling thread's current HIP device.  `speaker`: speaker_size
+ * floats (the constant embedding RAVE.encode concatenates, rave/model.py:
+ * 618-620).  precision: RAVE_PREC_F32 / RAVE_PREC_SPLIT16 / RAVE_PREC_AUTO. */
+int rave_model_create(const rave_model_config* cfg, const rave_param* params, int n_params,
+                      const float* speaker, int precision, rave_model** out);
+int rave_model_destroy(rave_model* m);
+
+/* RAVE.encode: x (B, 1, T) -> z (B, latent + speaker, T / hop); T % hop == 0. */
+int rave_model_encode(rave_model* m, const float* x, int batch, int t, float* z, void* stream);
+/* RAVE.decode: z (B, latent + speaker, F) -> y (B, 1, F * hop).  noise_u: the
+ * U[0,1) draw of NoiseGeneratorV2, shape rave_model_noise_shape, or NULL (the
+ * engine draws it); ignored by configs without a noise synthesizer. */
+int rave_model_decode(rave_model* m, const float* z, int batch, int frames, float* y,
+                      const float* noise_u, void* stream);
+/* decode(encode(x)) through an engine-owned latent buffer. */
+int rave_model_forward(rave_model* m, const float* x, int batch, int t, float* y,
+                       const float* noise_u, void* stream);
+/* Discrete configs (DiscreteScriptedRAVE, scripts/export.py:503-517):
+ * encoder -> rvq.encode: idx (B, n_q, T / hop) int64; rvq.decode -> cat
+ * speaker -> decoder -> PQMF inverse. */
+int rave_model_encode_codes(rave_model* m, const float* x, int batch, int t, int64_t* idx, void* stream);
+int rave_model_decode_codes(rave_model* m, const int64_t* idx, int batch, int frames, float* y,
+                            const float* noise_u, void* stream);
+/* dims of NoiseGeneratorV2's noise for a decode of `frames` latent frames:
+ * (B, noise frames, n_band, target) written to out[0..3]. */
+int rave_model_noise_shape(const rave_model* m, int batch, int frames, int64_t* out4);
+
+/* AdaIN (rave/blocks.py:856-919; nn~ learn/reset attributes, scripts/export.py:
+ * 248-265).  learn_x / learn_y: -1 keeps, 0/1 sets; reset_*: nonzero resets.
+ * row0: first buffer row this process's batch uses (data-parallel shards). */
+int rave_model_adain_control(rave_model* m, int learn_x, int learn_y, int reset_x, int reset_y);
+int rave_model_set_row0(rave_model* m, int row0);
+int rave_model_adain_count(const rave_model* m);
+/* module i: name, channels, and its buffers copied out / in (host, synchronous):
+ * stats (4, max_batch, C) = mean_x, std_x, mean_y, std_y; counters[2] =
+ * num_update_x, num_update_y.  set marks the statistics as loaded. */
+int rave_model_adain_info(const rave_model* m, int i, char* name, int name_cap, int* channels, int* max_batch);
+int rave_model_adain_get(rave_model* m, int i, float* stats, float* counters);
+int rave_model_adain_set(rave_model* m, int i, const float* stats, const float* counters);
+
+/* Launch-configuration choices of the autotuner as text ("key value ms" per
+ * line), to replay them into another model without timing runs. */
+int rave_model_tuning_get(const rave_model* m, char* buf, int cap);   /* bytes needed (with NUL) */
+int rave_model_tuning_set(rave_model* m, const char* text);
+
+/* Measurement (bench.py): the op list of one plan and per-op HIP-event times.
+ * which: 0 encode, 1 decode, 2 encode_codes, 3 decode_codes (built if needed). */
+typedef struct rave_op_info {
+    int32_t kind;        /* RAVE_OP_* */
+    int32_t precision;   /* RAVE_PREC_* of conv / unit ops, else -1 */
+    double flops;        /* algorithmic: 2 * MACs of the fp32 op */
+    double bytes;        /* algorithmic: tensors and weights read or written once */
+    char label[96];      /* reference module path */
+} rave_op_info;
+int rave_model_plan_ops(rave_model* m, int which, int batch, int t, rave_op_info* out, int cap);
+int rave_model_profile(rave_model* m, int which, int batch, int t, int runs);
+int rave_model_op_times(rave_model* m, int which, int batch, int t, float* ms, int n);
+
+/* ---------------------------------------------------------------- streaming
+ * cached_conv's streaming mode (cc.use_cached_conv(True), scripts/export.py:
+ * 543) for a causal model: per-call blocks of `block` samples (a multiple of
+ * hop) with persistent per-layer caches (zeroed at creation and by reset).
+ * Decoded audio lags one-shot causal decoding by rave_stream_delay samples;
+ * the encoder is exact.  AdaIN statistics are per block, as the reference
+ * computes them per call.  RAVE_STREAM_GRAPH: each block replays a captured
+ * hipGraph (inputs and outputs pass through stream-owned staging buffers). */
+enum { RAVE_STREAM_GRAPH = 1 };
+int rave_stream_create(rave_model* m, int batch, int block, int flags, rave_stream** out);
+int rave_stream_destroy(rave_stream* s);
+int rave_stream_reset(rave_stream* s, void* stream);
+int rave_stream_encode(rave_stream* s, const float* x, float* z, void* stream);
+int rave_stream_decode(rave_stream* s, const float* z, float* y, const float* noise_u, void* stream);
+int rave_stream_delay(const rave_stream* s);
 
 #ifdef __cplusplus
 }

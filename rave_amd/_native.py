@@ -36,13 +36,15 @@ OP_NOISE = 9
 OP_ADAIN = 10
 OP_UNIT = 11
 OP_STACK = 12
-ABI_VERSION = 7
+ABI_VERSION = 8
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 
 # GEMM arithmetic of conv / unit ops (include/rave_amd.h RAVE_PREC_*)
 PREC_F32 = 0
 PREC_SPLIT16 = 1
+PREC_AUTO = 2
 PRECISION = {"f32": PREC_F32, "split16": PREC_SPLIT16}
+STREAM_GRAPH = 1
 
 i32, i64, f32, vp = C.c_int32, C.c_int64, C.c_float, C.c_void_p
 
@@ -139,6 +141,31 @@ class StackArgs(C.Structure):
                    for u in range(STACK_UNITS)])
 
 
+MAX_RATIOS = 8
+MAX_DILATIONS = 8
+
+
+class ModelConfig(C.Structure):
+    _fields_ = [("n_band", i32), ("enc_bands", i32), ("capacity", i32), ("latent_size", i32),
+                ("kernel_size", i32), ("speaker_size", i32), ("n_ratios", i32),
+                ("ratios", i32 * MAX_RATIOS), ("n_dilations", i32 * MAX_RATIOS),
+                ("dilations", (i32 * MAX_DILATIONS) * MAX_RATIOS),
+                ("amplitude_modulation", i32), ("causal", i32), ("activation", i32), ("adain", i32),
+                ("leaky_slope", f32), ("conv_bias", i32), ("convt_bias", i32),
+                ("noise", i32), ("noise_hidden", i32), ("noise_bands", i32), ("n_noise_ratios", i32),
+                ("noise_ratios", i32 * MAX_RATIOS), ("rvq_quantizers", i32), ("rvq_codebook_size", i32),
+                ("fuse_units", i32)]
+
+
+class Param(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("data", vp), ("numel", i64)]
+
+
+class OpInfo(C.Structure):
+    _fields_ = [("kind", i32), ("precision", i32), ("flops", C.c_double), ("bytes", C.c_double),
+                ("label", C.c_char * 96)]
+
+
 PAYLOAD = 240
 
 
@@ -152,7 +179,7 @@ class Reloc(C.Structure):
 
 
 STRUCTS = [ConvArgs, AnalysisArgs, SynthesisArgs, FillArgs, RvqArgs, ShiftArgs, PlanOp, Reloc,
-           CopyArgs, NoiseArgs, AdainArgs, UnitArgs, StackArgs]
+           CopyArgs, NoiseArgs, AdainArgs, UnitArgs, StackArgs, ModelConfig, Param, OpInfo]
 
 # every exported symbol of include/rave_amd.h
 EXPORTS = [
@@ -165,7 +192,14 @@ EXPORTS = [
     "rave_unit_split_packed_size", "rave_unit_split_pack_weight",
     "rave_stack_supported", "rave_residual_stack",
     "rave_plan_create", "rave_plan_run", "rave_plan_destroy", "rave_plan_size",
-    "rave_plan_profile", "rave_plan_op_times",
+    "rave_plan_profile", "rave_plan_op_times", "rave_fill_uniform",
+    "rave_model_param_count", "rave_model_param_info", "rave_model_create", "rave_model_destroy",
+    "rave_model_encode", "rave_model_decode", "rave_model_forward", "rave_model_encode_codes",
+    "rave_model_decode_codes", "rave_model_noise_shape", "rave_model_adain_control", "rave_model_set_row0",
+    "rave_model_adain_count", "rave_model_adain_info", "rave_model_adain_get", "rave_model_adain_set",
+    "rave_model_tuning_get", "rave_model_tuning_set", "rave_model_plan_ops", "rave_model_profile",
+    "rave_model_op_times", "rave_stream_create", "rave_stream_destroy", "rave_stream_reset",
+    "rave_stream_encode", "rave_stream_decode", "rave_stream_delay",
 ]
 
 
@@ -215,6 +249,37 @@ def _load():
     lib.rave_plan_size.argtypes = [vp]
     lib.rave_plan_profile.argtypes = [vp, C.c_int]
     lib.rave_plan_op_times.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
+    lib.rave_fill_uniform.argtypes = [vp, i64, C.c_uint64, f32, f32, vp]
+    # model engine
+    cfgp = C.POINTER(ModelConfig)
+    lib.rave_model_param_count.argtypes = [cfgp]
+    lib.rave_model_param_info.argtypes = [cfgp, C.c_int, C.c_char_p, C.c_int, C.POINTER(i64)]
+    lib.rave_model_create.argtypes = [cfgp, C.POINTER(Param), C.c_int, vp, C.c_int, C.POINTER(vp)]
+    lib.rave_model_destroy.argtypes = [vp]
+    lib.rave_model_encode.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp]
+    lib.rave_model_decode.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp]
+    lib.rave_model_forward.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp]
+    lib.rave_model_encode_codes.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp]
+    lib.rave_model_decode_codes.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp]
+    lib.rave_model_noise_shape.argtypes = [vp, C.c_int, C.c_int, C.POINTER(i64)]
+    lib.rave_model_adain_control.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int]
+    lib.rave_model_set_row0.argtypes = [vp, C.c_int]
+    lib.rave_model_adain_count.argtypes = [vp]
+    lib.rave_model_adain_info.argtypes = [vp, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_int),
+                                          C.POINTER(C.c_int)]
+    lib.rave_model_adain_get.argtypes = [vp, C.c_int, vp, vp]
+    lib.rave_model_adain_set.argtypes = [vp, C.c_int, vp, vp]
+    lib.rave_model_tuning_get.argtypes = [vp, C.c_char_p, C.c_int]
+    lib.rave_model_tuning_set.argtypes = [vp, C.c_char_p]
+    lib.rave_model_plan_ops.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.POINTER(OpInfo), C.c_int]
+    lib.rave_model_profile.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int]
+    lib.rave_model_op_times.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float), C.c_int]
+    lib.rave_stream_create.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
+    lib.rave_stream_destroy.argtypes = [vp]
+    lib.rave_stream_reset.argtypes = [vp, vp]
+    lib.rave_stream_encode.argtypes = [vp, vp, vp, vp]
+    lib.rave_stream_decode.argtypes = [vp, vp, vp, vp, vp]
+    lib.rave_stream_delay.argtypes = [vp]
     # ABI self-check
     n = lib.rave_struct_sizes(None, 0)
     buf = (i64 * n)()
@@ -229,6 +294,39 @@ def _load():
 
 
 lib = _load()
+
+
+def model_config(cfg) -> ModelConfig:
+    """rave_amd.config.RaveConfig -> the engine's rave_model_config."""
+    c = ModelConfig()
+    c.n_band, c.enc_bands, c.capacity = cfg.n_band, cfg.enc_bands, cfg.capacity
+    c.latent_size, c.kernel_size, c.speaker_size = cfg.latent_size, cfg.kernel_size, cfg.speaker_size
+    if len(cfg.ratios) > MAX_RATIOS or len(cfg.dilations) != len(cfg.ratios):
+        raise ValueError("ratios / dilations do not fit the engine's limits")
+    c.n_ratios = len(cfg.ratios)
+    for i, (r, ds) in enumerate(zip(cfg.ratios, cfg.dilations)):
+        if len(ds) > MAX_DILATIONS:
+            raise ValueError("too many dilations per stage")
+        c.ratios[i] = r
+        c.n_dilations[i] = len(ds)
+        for j, d in enumerate(ds):
+            c.dilations[i][j] = d
+    c.amplitude_modulation = int(cfg.amplitude_modulation)
+    c.causal = int(cfg.causal)
+    c.activation = ACT[cfg.activation]
+    c.adain = int(cfg.adain)
+    c.leaky_slope = cfg.leaky_slope
+    c.conv_bias, c.convt_bias = int(cfg.conv_bias), int(cfg.convt_bias)
+    if cfg.noise is not None:
+        c.noise = 1
+        c.noise_hidden, c.noise_bands = cfg.noise.hidden_size, cfg.noise.noise_bands
+        c.n_noise_ratios = len(cfg.noise.ratios)
+        for i, r in enumerate(cfg.noise.ratios):
+            c.noise_ratios[i] = r
+    if cfg.rvq is not None:
+        c.rvq_quantizers, c.rvq_codebook_size = cfg.rvq.num_quantizers, cfg.rvq.codebook_size
+    c.fuse_units = 1
+    return c
 
 
 def check(rc: int, what: str = "") -> None:

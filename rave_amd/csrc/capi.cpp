@@ -37,7 +37,8 @@ extern "C" int rave_struct_sizes(int64_t* out, int n) {
         (int64_t)sizeof(rave_plan_op),           (int64_t)sizeof(rave_reloc),
         (int64_t)sizeof(rave_copy_args),         (int64_t)sizeof(rave_noise_args),
         (int64_t)sizeof(rave_adain_args),        (int64_t)sizeof(rave_unit_args),
-        (int64_t)sizeof(rave_stack_args),
+        (int64_t)sizeof(rave_stack_args),        (int64_t)sizeof(rave_model_config),
+        (int64_t)sizeof(rave_param),             (int64_t)sizeof(rave_op_info),
     };
     const int cnt = (int)(sizeof(sizes) / sizeof(sizes[0]));
     if (!out) return cnt;
@@ -123,6 +124,20 @@ extern "C" int rave_plan_destroy(rave_plan* plan) {
 }
 
 extern "C" int rave_plan_size(const rave_plan* plan) { return plan ? (int)plan->ops.size() : -1; }
+
+namespace rave {
+// Engine-internal: overwrite `n` bytes of op `op`'s argument payload (e.g. an
+// AdaIN op's mode when the learn flags change between streaming blocks).
+int plan_patch(rave_plan* plan, int op, int offset, const void* data, int n) {
+    if (!plan || op < 0 || op >= (int)plan->ops.size() || offset < 0 || n < 0 || offset + n > RAVE_OP_PAYLOAD) {
+        set_error("plan_patch: bad arguments");
+        return RAVE_ERR_ARG;
+    }
+    std::memcpy(plan->ops[op].u.raw + offset, data, (size_t)n);
+    std::memcpy(plan->scratch[op].u.raw + offset, data, (size_t)n);
+    return RAVE_OK;
+}
+}  // namespace rave
 
 extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, void* stream) {
     if (!plan) {

@@ -301,9 +301,30 @@ __global__ void rvq_decode_kernel(rave_rvq_args a) {
     }
 }
 
+// Counter-based uniform draw: a splitmix64 finaliser of (seed, index), top 24
+// bits -> [0, 1).  Stateless, so any launch geometry gives the same values.
+__global__ __launch_bounds__(256) void fill_uniform_kernel(float* y, int64_t n, uint64_t seed, float lo,
+                                                           float scale) {
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        uint64_t z = seed + 0x9E3779B97F4A7C15ull * (uint64_t)(i + 1);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        y[i] = lo + scale * ((float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f));
+    }
+}
+
 }  // namespace rave
 
 using namespace rave;
+
+extern "C" int rave_fill_uniform(float* y, int64_t n, uint64_t seed, float lo, float hi, void* stream) {
+    RAVE_CHECK_ARG(y && n >= 0, "fill_uniform: bad arguments");
+    if (n == 0) return RAVE_OK;
+    const int blocks = (int)std::min<int64_t>(ceil_div64(n, 256), 2048);
+    launch(fill_uniform_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), y, n, seed, lo, hi - lo);
+    return launch_status("fill_uniform_kernel");
+}
 
 extern "C" int rave_fill_channels(const rave_fill_args* p, void* stream) {
     RAVE_CHECK_ARG(p && p->y && p->values, "fill_channels: null pointer");

@@ -339,6 +339,55 @@ def gen_streaming(mods, cfg, out, seed=0, n_blocks=12, block=2048):
     return res
 
 
+def gen_stream_v3(mods, cfg, out, fname="v3_noise_causal_stream.npz", seed=0, n_blocks=6, block=2048):
+    """Cached-conv streaming (cc.use_cached_conv(True)) of a causal v3 model with
+    the noise synthesizer and AdaIN, block by block: blocks 0-1 learn the target
+    statistics (learn_y), 2-3 learn the source (learn_x; the transfer turns on),
+    4-5 transfer with frozen statistics -- the nn~ learn_target / learn_source
+    sequence (scripts/export.py:248-265).  Encoder and decoder are streamed in
+    separate passes over fresh caches; the decoder's uniform noise is injected
+    per block (torch.rand_like, rave/blocks.py:287)."""
+    m = build_reference(mods, cfg, cached=True)
+    params = init_params(cfg, seed=seed)
+    load_params(m, cfg, params)
+    speaker = torch.from_numpy(init_speaker(cfg, seed=seed))
+    x = torch.from_numpy(synth_audio(1, n_blocks * block, seed0=9))
+    frames = block // cfg.hop
+    rng = np.random.Generator(np.random.PCG64(13))
+    zlat = rng.standard_normal((1, cfg.latent_size, n_blocks * frames)).astype(np.float32)
+    z = torch.cat([torch.from_numpy(zlat), speaker.reshape(1, -1, 1).repeat(1, 1, zlat.shape[-1])], 1)
+    F = block // cfg.n_band
+    n_fr = F // int(np.prod(cfg.noise.ratios))
+    u = rng.uniform(0, 1, size=(n_blocks, 1, n_fr, cfg.n_band, 2 * (cfg.noise.noise_bands - 1))).astype(np.float32)
+    ada = [mod for mod in m.modules() if isinstance(mod, mods["blocks"].AdaptiveInstanceNormalization)]
+    flags = [(0, 1), (0, 1), (1, 0), (1, 0), (0, 0), (0, 0)]
+
+    def set_learn(lx, ly):
+        for mod in ada:
+            mod.learn_x.fill_(float(lx))
+            mod.learn_y.fill_(float(ly))
+
+    res = {"x": x.numpy(), "z": z.numpy(), "noise_u": u, "speaker": speaker.numpy(), "block": np.int64(block),
+           "seed": np.int64(seed), "flags": np.array(flags, np.int64)}
+    with torch.no_grad():
+        zs = []
+        for i in range(n_blocks):
+            set_learn(*flags[i])
+            zs.append(ref_encode(m, cfg, x[..., i * block:(i + 1) * block], speaker))
+        for mod in ada:          # the decoder pass starts from fresh statistics too
+            mod.reset_x()
+            mod.reset_y()
+        ys = []
+        for i in range(n_blocks):
+            set_learn(*flags[i])
+            with NoiseInjector(torch.from_numpy(u[i])):
+                ys.append(ref_decode(m, z[..., i * frames:(i + 1) * frames]))
+    res["z_stream"] = torch.cat(zs, -1).numpy()
+    res["y_stream"] = torch.cat(ys, -1).numpy()
+    np.savez_compressed(os.path.join(out, fname), **res)
+    return res
+
+
 def gen_adain(mods, cfg, out, fname="v3_adain.npz", batch=2, t=8192, seed=0):
     """AdaIN style transfer in eval mode (rave/blocks.py:856-919), driven the
     way nn~'s learn_source / learn_target attributes drive it: learn the target
@@ -428,6 +477,9 @@ def main():
     a = ap.parse_args()
     torch.set_num_threads(8)
     mods = install_shims()
+    if a.only == "stream_v3":
+        gen_stream_v3(mods, rcfg.v3_noise(causal=True, capacity=16), a.out)
+        return
     if a.only == "adain":
         gen_adain(mods, rcfg.v3(), a.out)
         gen_adain(mods, rcfg.v3(capacity=8), a.out, fname="v3_adain_small.npz", t=4096)
@@ -451,6 +503,7 @@ def main():
               per_layer=True)
     gen_adain(mods, rcfg.v3(), a.out)
     gen_adain(mods, rcfg.v3(capacity=8), a.out, fname="v3_adain_small.npz", t=4096)
+    gen_stream_v3(mods, rcfg.v3_noise(causal=True, capacity=16), a.out)
 
     files = sorted(f for f in os.listdir(a.out) if f.endswith(".npz"))
     manifest["files"] = {f: hashlib.sha256(open(os.path.join(a.out, f), "rb").read()).hexdigest()[:16]

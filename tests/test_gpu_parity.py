@@ -186,26 +186,31 @@ def test_conv_every_config(N, dev, case, precision):
 # ------------------------------------------------------------------ PQMF
 @pytest.mark.parametrize("causal", [False, True])
 def test_pqmf_golden(N, dev, golden, causal):
-    from rave_amd import config as rcfg
-    from rave_amd.model import RAVE, View, Plan
+    """rave_pqmf_analysis / rave_pqmf_synthesis (CachedPQMF.forward / inverse)
+    through the C-ABI against the reference's PQMF fixtures, both paddings."""
+    from oracle.rave_oracle import get_padding
+    from rave_amd.pqmf import kernels
     g = golden("pqmf")
     mode = "causal" if causal else "centered"
-    cfg = rcfg.v2(causal=causal, capacity=8)
-    from rave_amd.weights import init_params
-    m = RAVE(cfg, init_params(cfg), np.zeros(256, np.float32), device=dev, hk=g["hk"])
+    hkf, hki = kernels(g["hk"])
+    hkf_d, hki_d = torch.from_numpy(hkf).to(dev), torch.from_numpy(hki).to(dev)
     x = torch.from_numpy(g["x"]).to(dev)
     B, _, T = x.shape
     F = T // 16
     y = torch.empty(B, 16, F, device=dev)
-    p = Plan(m.arena)
-    m._analysis(p, B, T, View(0, 0, T, T), View(1, 0, 16 * F, F), 16)
-    p.finalize(dev).run([x.data_ptr(), y.data_ptr()])
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    a = N.AnalysisArgs(n_band=16, taps=hkf.shape[-1], n_out_bands=16, batch=B, t_in=T,
+                       pad_left=get_padding(hkf.shape[-1], causal=causal)[0], t_out=F, x=x.data_ptr(), x_sb=T,
+                       y=y.data_ptr(), y_sb=16 * F, y_sc=F, hkf=hkf_d.data_ptr())
+    N.check(N.lib.rave_pqmf_analysis(C.byref(a), st))
     bands = torch.from_numpy(g["bands"]).to(dev)
-    out = torch.empty(B, 1, bands.shape[-1] * 16, device=dev)
-    p2 = Plan(m.arena)
-    m._synthesis(p2, B, bands.shape[-1], View(0, 0, 16 * bands.shape[-1], bands.shape[-1]),
-                 View(1, 0, out.shape[-1], out.shape[-1]), 0)
-    p2.finalize(dev).run([bands.data_ptr(), out.data_ptr()])
+    Fb = bands.shape[-1]
+    out = torch.empty(B, 1, Fb * 16, device=dev)
+    s_ = N.SynthesisArgs(n_band=16, taps=hki.shape[-1], batch=B, t_in=Fb,
+                         pad_left=get_padding(hki.shape[-1], causal=causal)[0], mode=0, frame0=0, x_len=0,
+                         x=bands.data_ptr(), x_sb=16 * Fb, x_sc=Fb, y=out.data_ptr(), y_sb=16 * Fb,
+                         hki=hki_d.data_ptr())
+    N.check(N.lib.rave_pqmf_synthesis(C.byref(s_), st))
     torch.cuda.synchronize()
     ref_a = g[f"analysis_{mode}"]
     ref_s = g[f"synthesis_{mode}"]
@@ -429,6 +434,93 @@ def test_streaming_matches_oneshot_long(dev):
     assert torch.equal(ys2, ys[..., :blk])
 
 
+def test_streaming_graph_equals_eager(dev):
+    """RAVE_STREAM_GRAPH (captured hipGraph per block, staging buffers) gives
+    bitwise the blocks of the eager plan replay, across a reset too."""
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE
+    from rave_amd.streaming import StreamingRAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.causal()
+    m = RAVE(cfg, init_params(cfg, 4), init_speaker(cfg, 4), device=dev, precision="auto")
+    sg = StreamingRAVE(m, batch=2, block=4096, graph=True)
+    se = StreamingRAVE(m, batch=2, block=4096, graph=False)
+    gen = torch.Generator().manual_seed(2)
+    for i in range(6):
+        if i == 3:
+            sg.reset()
+            se.reset()
+        x = (0.2 * torch.randn(2, 1, 4096, generator=gen)).to(dev)
+        zg, ze = sg.encode(x), se.encode(x)
+        yg, ye = sg.decode(zg), se.decode(ze)
+        torch.cuda.synchronize()
+        assert torch.equal(zg, ze) and torch.equal(yg, ye), i
+
+
+@pytest.mark.parametrize("precision", ["f32", "auto"])
+@pytest.mark.parametrize("graph", [True, False])
+def test_stream_v3_noise_adain_golden(dev, golden, precision, graph):
+    """Streaming a causal v3 model with the noise synthesizer and AdaIN against
+    the reference run in cached_conv streaming mode (make_golden.py
+    gen_stream_v3): blocks learn the target statistics, then the source, then
+    transfer (nn~'s learn_target / learn_source flags switched between
+    blocks); the decoder's per-block uniform noise is the reference's."""
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE
+    from rave_amd.streaming import StreamingRAVE
+    from rave_amd.weights import init_params
+    g = golden("v3_noise_causal_stream")
+    cfg = rcfg.v3_noise(causal=True, capacity=16)
+    m = RAVE(cfg, init_params(cfg, int(g["seed"])), g["speaker"], device=dev, hk=_golden_hk(golden),
+             precision=precision)
+    blk = int(g["block"])
+    s = StreamingRAVE(m, batch=1, block=blk, graph=graph)
+    x = torch.from_numpy(g["x"]).to(dev)
+    z = torch.from_numpy(g["z"]).to(dev)
+    u = torch.from_numpy(g["noise_u"]).to(dev)
+    Fz = blk // cfg.hop
+    zs, ys = [], []
+    for i, (lx, ly) in enumerate(g["flags"]):
+        m.adain.set_learn(learn_x=bool(lx), learn_y=bool(ly))
+        zs.append(s.encode(x[..., i * blk:(i + 1) * blk].contiguous()))
+    m.adain.reset_x()
+    m.adain.reset_y()
+    for i, (lx, ly) in enumerate(g["flags"]):
+        m.adain.set_learn(learn_x=bool(lx), learn_y=bool(ly))
+        ys.append(s.decode(z[..., i * Fz:(i + 1) * Fz].contiguous(), noise_u=u[i]))
+    torch.cuda.synchronize()
+    ez = maxabs(torch.cat(zs, -1).cpu().numpy(), g["z_stream"])
+    ey = maxabs(torch.cat(ys, -1).cpu().numpy(), g["y_stream"])
+    print(f"\n[parity] v3+noise+AdaIN causal streaming {precision} graph={graph}: z {ez:.3e}, y {ey:.3e}")
+    assert ez < TOL and ey < TOL
+
+
+def test_engine_forward_and_device_noise(dev):
+    """rave_model_forward == decode(encode(x)) bitwise; a noise config with no
+    noise tensor draws it on the device (a fresh draw per call, finite output,
+    same statistics as the injected-noise path)."""
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE
+    from rave_amd.weights import init_params, init_speaker
+    N = pytest.importorskip("rave_amd._native")
+    cfg = rcfg.v2(capacity=8)
+    m = RAVE(cfg, init_params(cfg, 1), init_speaker(cfg, 1), device=dev)
+    x = (0.2 * torch.randn(2, 1, 8192, generator=torch.Generator().manual_seed(5))).to(dev)
+    y = torch.empty_like(x)
+    N.check(N.lib.rave_model_forward(m.handle, x.data_ptr(), 2, 8192, y.data_ptr(), None,
+                                     C.c_void_p(torch.cuda.current_stream().cuda_stream)), "forward")
+    assert torch.equal(y, m.decode(m.encode(x)))
+    cfgn = rcfg.v3_noise(capacity=8)
+    mn = RAVE(cfgn, init_params(cfgn, 1), init_speaker(cfgn, 1), device=dev)
+    z = torch.randn(2, cfgn.dec_in, 8, generator=torch.Generator().manual_seed(6)).to(dev)
+    y1, y2 = mn.decode(z), mn.decode(z)
+    u = torch.rand(mn.noise_shape(2, 8), device=dev)
+    y3 = mn.decode(z, noise_u=u)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y1).all() and not torch.equal(y1, y2)
+    assert float((y1 - y3).abs().max()) < 0.5 and float((y1 - y3).abs().max()) > 0
+
+
 # ------------------------------------------------------------------ v3 noise / AdaIN (BASELINE config 5)
 @pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name,capacity", [("v3_noise", None), ("v3_noise_small_layers", 8)])
@@ -525,6 +617,35 @@ def test_adain_style_transfer_golden(dev, golden, precision):
                 assert maxabs(sd[f"{n}.{b}"], ref) < 1e-4 * max(1.0, float(np.abs(ref).max())), (n, b)
             for b in ("num_update_x", "num_update_y"):
                 assert float(sd[f"{n}.{b}"][0]) == float(g[f"final/{n}.{b}"][0])
+
+
+def test_adain_state_roundtrip(dev):
+    """AdaIN buffers held by the engine: reference init, load/state_dict under
+    the reference's names, learn flags -> kernel mode (learn_y wins, as
+    forward checks it first), reset_y."""
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.v3(capacity=4)
+    m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev)
+    st = m.adain
+    assert not st.active and st.mode == 0 and len(st.modules) == 22
+    (a, ca), (b, cb) = st.modules[0], st.modules[-1]
+    sd = st.state_dict()
+    assert sd[f"{a}.mean_x"].shape == (64, ca, 1) and (sd[f"{b}.std_y"] == 1).all()
+    rng = np.random.default_rng(0)
+    new = {f"{b}.mean_y": rng.standard_normal((64, cb, 1)), f"{b}.num_update_y": np.array([3.0])}
+    st.load(new)
+    assert st.active
+    sd = st.state_dict()
+    assert np.allclose(sd[f"{b}.mean_y"], new[f"{b}.mean_y"]) and sd[f"{b}.num_update_y"][0] == 3.0
+    assert (sd[f"{a}.mean_y"] == 0).all()
+    st.set_learn(learn_x=True, learn_y=True)
+    assert st.mode == 2
+    st.set_learn(learn_y=False)
+    assert st.mode == 1
+    st.reset_y()
+    assert (st.state_dict()[f"{b}.mean_y"] == 0).all() and st.state_dict()[f"{b}.num_update_y"][0] == 0
 
 
 def test_adain_loaded_stats_and_batch_limit(dev):
@@ -629,16 +750,25 @@ def test_residual_unit_kernel(N, dev, case, precision):
 
 
 @pytest.mark.parametrize("precision,n_fused", [("f32", 22), ("split16", 22), ("auto", 22)])
-def test_fused_units_match_unfused_model(dev, precision, n_fused):
+def test_fused_units_match_unfused_model(N, dev, precision, n_fused):
     """The v2 plan with fused residual units equals the conv-by-conv plan."""
     from rave_amd import config as rcfg
     from rave_amd.model import RAVE
     from rave_amd.weights import init_params, init_speaker
     cfg = rcfg.v2()
     params, spk = init_params(cfg, 0), init_speaker(cfg, 0)
+    from rave_amd.model import DECODE, ENCODE
     mf = RAVE(cfg, params, spk, device=dev, precision=precision)
     mu = RAVE(cfg, params, spk, device=dev, fuse_units=False, precision=precision)
-    assert len(mf.unit_off) == n_fused and not mu.unit_off
+
+    def units(m):
+        ops = m.ops(ENCODE, 4, 65536) + m.ops(DECODE, 4, 64)
+        return sum(1 for o in ops if o["kind"] == N.OP_UNIT) + 3 * sum(1 for o in ops if o["kind"] == N.OP_STACK)
+    assert units(mu) == 0
+    if precision == "auto":
+        assert 0 < units(mf) <= n_fused          # fused where it measured faster
+    else:
+        assert units(mf) == n_fused
     g = torch.Generator(device="cpu").manual_seed(1)
     x = (0.1 * torch.randn(4, 1, 65536, generator=g)).to(dev)
     zf, zu = mf.encode(x), mu.encode(x)
@@ -662,9 +792,9 @@ def test_auto_tuning_roundtrip(dev):
     x = (0.1 * torch.randn(2, 1, 32768, generator=g)).to(dev)
     y1 = m1.forward(x)
     tun = json.loads(json.dumps(m1.tuning()))
-    assert any(k[0] == "fuse" for k, _, _ in tun) and any(k[0] == "conv" for k, _, _ in tun)
+    kinds = {k.split("|")[0] for k, _, _ in tun}
+    assert {"fuse", "conv", "unit"} <= kinds
     m2 = RAVE(cfg, params, spk, device=dev, precision="auto", tuning=tun)
-    m2._time_native = None          # a timing run would now raise
     y2 = m2.forward(x)
     torch.cuda.synchronize()
     assert m2.tuning() == m1.tuning()
@@ -751,7 +881,6 @@ def test_shift_history_batched(dev, N):
     batched launch of up to 24 buffers, more split over launches): hist below,
     equal to and above t_new (in-place overlap), one-channel rows with long
     histories, padded channel strides, hist 0."""
-    from rave_amd.model import Arena, Plan, View
     rng = np.random.default_rng(7)
     shapes = [(1, 1, 512, 2048), (2, 64, 6, 128), (1, 512, 130, 64), (3, 16, 200, 200),
               (1, 8, 0, 32), (2, 33, 70, 5)]
@@ -772,14 +901,17 @@ def test_shift_history_batched(dev, N):
     exp[:, :Cc] = _shift_ref(refs[2][:, :Cc], h, t)
     assert np.array_equal(b0.cpu().numpy(), exp)
     # all of them as consecutive plan ops
-    plan = Plan(Arena())
-    for (B, Cc, h, t), buf in zip(shapes, bufs):
-        plan.add(N.OP_SHIFT_HISTORY, N.ShiftArgs,
-                 dict(batch=B, channels=Cc, hist=h, t_new=t, sb=buf.stride(0), sc=buf.stride(1)),
-                 dict(buf=View("abs", buf.data_ptr(), 0, 0, 1)))
-    plan.finalize(dev)
-    plan.run([])
+    ops = (N.PlanOp * len(shapes))()
+    for i, ((B, Cc, h, t), buf) in enumerate(zip(shapes, bufs)):
+        sa = N.ShiftArgs(batch=B, channels=Cc, hist=h, t_new=t, buf=buf.data_ptr(), sb=buf.stride(0),
+                         sc=buf.stride(1))
+        ops[i].kind = N.OP_SHIFT_HISTORY
+        C.memmove(ops[i].raw, C.addressof(sa), C.sizeof(sa))
+    hp = C.c_void_p()
+    N.check(N.lib.rave_plan_create(ops, len(shapes), None, 0, C.byref(hp)), "plan_create")
+    N.check(N.lib.rave_plan_run(hp, None, 0, C.c_void_p(torch.cuda.current_stream().cuda_stream)), "plan_run")
     torch.cuda.synchronize()
+    N.lib.rave_plan_destroy(hp)
     for (B, Cc, h, t), buf, r in zip(shapes, bufs, refs):
         exp = r.copy()
         exp[:, :Cc] = _shift_ref(r[:, :Cc], h, t)
@@ -868,3 +1000,29 @@ def test_nn_tilde_surface_streaming_and_stereo(dev):
     x = (0.2 * torch.randn(2, 1, 8192, generator=gen)).to(dev)
     assert torch.equal(w2.encode(x), m2.encode(x))
     assert w2.get_method_params("encode") == [1, 1, 320, 1024]
+
+
+def test_nn_tilde_learn_target_drives_adain(dev):
+    """nn~'s learn_target / reset_target attributes reach the model's AdaIN
+    modules on encode (ScriptedRAVE.update_adain, scripts/export.py:248-265):
+    statistics are learned, then a reset clears them once."""
+    from rave_amd import config as rcfg
+    from rave_amd.export import NNTildeRAVE
+    from rave_amd.model import RAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.v3(capacity=8)
+    m = RAVE(cfg, init_params(cfg, 2), init_speaker(cfg, 2), device=dev)
+    w = NNTildeRAVE(m)
+    x = (0.3 * torch.randn(1, 1, 4096, generator=torch.Generator().manual_seed(1))).to(dev)
+    name = m.adain.modules[0][0]
+    w.encode(x)
+    assert m.adain.state_dict()[f"{name}.num_update_y"][0] == 0
+    w.set_learn_target(True)
+    w.encode(x)
+    w.encode(x)
+    sd = m.adain.state_dict()
+    assert sd[f"{name}.num_update_y"][0] == 2 and not np.allclose(sd[f"{name}.mean_y"][0], 0)
+    w.set_learn_target(False)
+    w.set_reset_target(True)
+    w.encode(x)
+    assert m.adain.state_dict()[f"{name}.num_update_y"][0] == 0 and w.get_reset_target() is False

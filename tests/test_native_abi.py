@@ -154,25 +154,6 @@ def test_plan_create_and_relocation_bounds():
         N.check(N.lib.rave_plan_create(ops, 1, bad, 1, C.byref(h)), "plan_create")
 
 
-def test_workspace_splitk_slab_disjoint():
-    """The split-K slab never aliases a planned tensor (regression: it was
-    taken from the end-of-plan free list, which overlaps mid-plan tensors)."""
-    from rave_amd.model import Plan
-
-    class _Arena:
-        def ptr(self, off):
-            return 4096 + 4 * off
-    p = Plan(_Arena())
-    a = p.ws.alloc(1000)
-    b = p.ws.alloc(3000)
-    p.ws.release(a, 1000)          # free at the end of planning, live mid-plan
-    p.ws.release(b, 3000)
-    p.splitk_view(500)
-    p.add(N.OP_FILL, N.FillArgs, dict(batch=1, channels=1, t_len=1), dict(y=None, values=None))
-    p.finalize("cpu")
-    assert p.splitk_off >= b + 3000
-
-
 @pytest.mark.parametrize("c_in,c_out,r", [(64, 32, 2), (32, 16, 4)])
 def test_pack_layout_transposed_cached_form(c_in, c_out, r):
     """out_shift = 0 (cached_conv's overlap-add form): output = the uncropped
@@ -187,25 +168,37 @@ def test_pack_layout_transposed_cached_form(c_in, c_out, r):
     assert np.abs(got - ref).max() < 1e-9 * max(1, np.abs(ref).max()) * 1e4
 
 
-def test_adain_state_roundtrip():
-    """AdaIN buffers: reference init, load/state_dict under the reference's
-    names, learn flags -> kernel mode (learn_y wins, as forward checks it first)."""
-    import torch
-    from rave_amd.adain import AdainState
-    st = AdainState([("a", 4), ("b", 8)], torch.device("cpu"))
-    assert not st.active and st.mode == 0
-    sd = st.state_dict()
-    assert sd["a.mean_x"].shape == (64, 4, 1) and (sd["b.std_y"] == 1).all()
-    rng = np.random.default_rng(0)
-    new = {"b.mean_y": rng.standard_normal((64, 8, 1)), "b.num_update_y": np.array([3.0])}
-    st.load(new)
-    assert st.active
-    sd = st.state_dict()
-    assert np.allclose(sd["b.mean_y"], new["b.mean_y"]) and sd["b.num_update_y"][0] == 3.0
-    assert (sd["a.mean_y"] == 0).all()
-    st.set_learn(learn_x=True, learn_y=True)
-    assert st.mode == 2
-    st.set_learn(learn_y=False)
-    assert st.mode == 1
-    st.reset_y()
-    assert (st.state_dict()["b.mean_y"] == 0).all() and st.state_dict()["b.num_update_y"][0] == 0
+@pytest.mark.parametrize("name", ["v2", "causal", "discrete", "v3", "v3_noise"])
+def test_engine_parameter_table_matches_graph(name):
+    """The native engine's module graph (rave_amd/csrc/engine.cpp) asks for
+    exactly the reference state_dict names and shapes that rave_amd.graph
+    restates -- the table the golden fixtures load into the reference modules."""
+    from rave_amd import config as rcfg
+    from rave_amd.graph import param_shapes
+    cfg = rcfg.get_config(name)
+    ccfg = N.model_config(cfg)
+    n = N.lib.rave_model_param_count(C.byref(ccfg))
+    assert n > 0
+    buf = C.create_string_buffer(256)
+    numel = C.c_int64()
+    got = {}
+    for i in range(n):
+        N.check(N.lib.rave_model_param_info(C.byref(ccfg), i, buf, 256, C.byref(numel)), "param_info")
+        got[buf.value.decode()] = numel.value
+    assert got.pop("pqmf.hk") == -1                   # any (n_band, L): the checkpoint's buffer
+    exp = {k: int(np.prod(v)) for k, v in param_shapes(cfg).items()}
+    assert got == exp
+
+
+def test_engine_config_validation():
+    from rave_amd import config as rcfg
+    ccfg = N.model_config(rcfg.v2())
+    ccfg.activation = 7
+    assert N.lib.rave_model_param_count(C.byref(ccfg)) == N.RAVE_ERR_ARG
+    ccfg = N.model_config(rcfg.v2())
+    ccfg.n_ratios = 0
+    with pytest.raises(ValueError):
+        N.check(N.lib.rave_model_param_count(C.byref(ccfg)), "param_count")
+    h = C.c_void_p()
+    with pytest.raises(ValueError):   # rejected before any device work
+        N.check(N.lib.rave_model_create(C.byref(ccfg), None, 0, None, 0, C.byref(h)), "model_create")
