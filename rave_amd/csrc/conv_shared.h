@@ -58,13 +58,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, int 
 // [0, q0) of every channel (rows up to the 64-aligned group-1 start are
 // padding: co >= c_out), rows [split_row, M) phases [q0, R).
 __device__ __forceinline__ void convt_row(const ConvKArgs& a, int m, int& co, int& q) {
+    const int p = a.R - a.q0;            // phases in row group 1 (0: no group 1)
     if (m < a.split_row) {
         co = m / a.q0;
         q = m - co * a.q0;
-    } else {
-        const int mm = m - a.split_row, p = a.R - a.q0;
+    } else if (p > 0) {
+        const int mm = m - a.split_row;
         co = mm / p;
         q = a.q0 + (mm - co * p);
+    } else {                             // padding row past a single group: never stored
+        co = a.bias_rows;
+        q = 0;
     }
 }
 

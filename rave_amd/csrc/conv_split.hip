@@ -264,7 +264,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         const int m = mw + j * 32 + l32;
-        e_rs[j] = a.rscale[m];                   // m < Mpad
+        e_rs[j] = m < a.Mpad ? a.rscale[m] : 0.f;   // tiles taller than the padded rows
         int co = m, q = 0;
         if (a.transposed) convt_row(a, m, co, q);
         e_co[j] = co;

@@ -1026,3 +1026,65 @@ def test_nn_tilde_learn_target_drives_adain(dev):
     w.set_reset_target(True)
     w.encode(x)
     assert m.adain.state_dict()[f"{name}.num_update_y"][0] == 0 and w.get_reset_target() is False
+
+
+def _stream_conv_cases(cfg):
+    """(node, t_src, extra history) of every conv of a causal graph at a 2048-sample
+    block, with the operand views the streaming engine gives it: x starts
+    `need` columns before the block inside a [history | block] row, row widths
+    not a multiple of 4 (the unaligned window-DMA path)."""
+    from rave_amd.graph import build_graph
+    g = build_graph(cfg)
+    t = {"enc_in": 2048 // cfg.n_band, "dec_in": 2048 // cfg.hop}
+    out = []
+    for n in g.encoder + g.decoder + g.noise:
+        ts = t[n.src]
+        t[n.dst] = ts * n.stride if n.transposed else ts // n.stride
+        out.append((n, ts))
+    return out
+
+
+@pytest.mark.parametrize("capacity", [8, 16, 64])
+def test_stream_conv_shapes_split16_vs_f32(N, dev, capacity):
+    """Every streaming conv shape of a causal v3+noise graph: split-f16 ==
+    exact fp32 (layer tolerance), with the cached views (history offset, odd
+    row widths, the cached ConvTranspose form with one history column)."""
+    from rave_amd import config as rcfg
+    cfg = rcfg.v3_noise(causal=True, capacity=capacity)
+    rng = np.random.default_rng(capacity)
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for n, ts in _stream_conv_cases(cfg):
+        need = 1 if n.transposed else n.pad[0]
+        h = need + 3                                   # history columns in the row
+        width = h + ts
+        t_in = need + ts
+        t_out = ts * n.stride if n.transposed else ts // n.stride
+        B = 2
+        xbuf = torch.from_numpy(rng.standard_normal((B, n.c_in, width)).astype(np.float32)).to(dev)
+        wshape = (n.c_in, n.c_out, n.kernel) if n.transposed else (n.c_out, n.c_in, n.kernel)
+        w = (rng.uniform(-1, 1, wshape) / np.sqrt(n.c_in * n.kernel)).astype(np.float32)
+        bias = torch.from_numpy(rng.uniform(-0.1, 0.1, n.c_out).astype(np.float32)).to(dev)
+        alpha = torch.from_numpy((1 + 0.1 * rng.standard_normal(n.c_in)).astype(np.float32)).to(dev)
+        outs = []
+        for prec in (N.PREC_F32, N.PREC_SPLIT16):
+            packed = torch.from_numpy(N.pack_conv_weight(w, n.c_in, n.c_out, n.kernel, n.stride, n.dilation,
+                                                         n.transposed, out_shift=0, precision=prec)).to(dev)
+            y = torch.full((B, n.c_out, t_out + 5), float("nan"), device=dev)
+            a = N.ConvArgs(c_in=n.c_in, c_out=n.c_out, kernel=n.kernel, stride=n.stride, dilation=n.dilation,
+                           pad_left=1 if n.transposed else 0, pad_right=0, transposed=int(n.transposed),
+                           out_shift=0, act=N.ACT[n.act], leaky_slope=0.2, batch=B, t_in=t_in, t_out=t_out,
+                           precision=prec, x=xbuf.data_ptr() + 4 * (h - need), x_sb=n.c_in * width, x_sc=width,
+                           y=y.data_ptr(), y_sb=n.c_out * (t_out + 5), y_sc=t_out + 5,
+                           weight=packed.data_ptr(), bias=bias.data_ptr() if n.bias else None,
+                           alpha=alpha.data_ptr() if n.act == "snake" else None)
+            nws = int(N.lib.rave_conv1d_workspace(C.byref(a)))
+            ws = torch.zeros(max(nws, 1), device=dev)
+            a.partial = ws.data_ptr() if nws > 0 else None
+            N.check(N.lib.rave_conv1d(C.byref(a), st), n.name)
+            torch.cuda.synchronize()
+            outs.append(y[..., :t_out].cpu().numpy())
+            assert torch.isnan(y[..., t_out:]).all(), n.name           # nothing written past t_out
+        ref = outs[0]
+        assert np.isfinite(ref).all(), n.name
+        err = maxabs(outs[1], ref)
+        assert err <= 2e-5 * max(1.0, np.abs(ref).max()), (n.name, n.c_in, n.c_out, n.kernel, ts, err)
