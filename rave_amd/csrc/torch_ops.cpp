@@ -1,0 +1,238 @@
+// TorchScript binding of the model engine (TORCH_LIBRARY): the operator seam
+// nn~ needs.  nn~ (a C++ Max/PD external) loads a TorchScript module and calls
+// its registered methods (scripts/export.py:58-480, export_to_ts :618); ctypes
+// cannot be scripted, so the engine is exposed as the custom class
+// torch.classes.rave_amd.Engine whose methods take and return tensors on
+// torch's current HIP stream, and which pickles (def_pickle) so a scripted
+// module holding one can be saved and loaded like any .ts file.
+//
+// Only tensors, ints and strings cross this file; every launch goes through
+// the C-ABI (include/rave_amd.h rave_model_* / rave_stream_*).
+#include <torch/custom_class.h>
+#include <torch/script.h>
+
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/rave_amd.h"
+
+namespace {
+
+void check(int rc, const char* what) {
+    if (rc == RAVE_OK) return;
+    const std::string msg = std::string(what) + ": " + rave_last_error();
+    if (rc == RAVE_ERR_ARG) TORCH_CHECK_VALUE(false, msg);
+    if (rc == RAVE_ERR_UNSUPPORTED) TORCH_CHECK_NOT_IMPLEMENTED(false, msg);
+    TORCH_CHECK(false, msg, " (status ", rc, ")");
+}
+
+// rave_model_config <-> a flat int list (the TorchScript-visible form) + leaky slope
+// n_band .. n_ratios (7), ratios, n_dilations, dilations, am / causal / act / adain (4),
+// biases (2), noise / hidden / bands / n_noise_ratios (4), noise_ratios, rvq x2 + fuse (3)
+constexpr int kCfgInts = 7 + 2 * RAVE_MAX_RATIOS + RAVE_MAX_RATIOS * RAVE_MAX_DILATIONS + 4 + 2 + 4 +
+                         RAVE_MAX_RATIOS + 3;
+
+rave_model_config config_from(const std::vector<int64_t>& v, double slope) {
+    TORCH_CHECK_VALUE((int)v.size() == kCfgInts, "engine config: expected ", kCfgInts, " ints, got ", v.size());
+    rave_model_config c{};
+    size_t i = 0;
+    auto nx = [&]() { return (int32_t)v[i++]; };
+    c.n_band = nx(); c.enc_bands = nx(); c.capacity = nx(); c.latent_size = nx();
+    c.kernel_size = nx(); c.speaker_size = nx(); c.n_ratios = nx();
+    for (int k = 0; k < RAVE_MAX_RATIOS; ++k) c.ratios[k] = nx();
+    for (int k = 0; k < RAVE_MAX_RATIOS; ++k) c.n_dilations[k] = nx();
+    for (int k = 0; k < RAVE_MAX_RATIOS; ++k)
+        for (int j = 0; j < RAVE_MAX_DILATIONS; ++j) c.dilations[k][j] = nx();
+    c.amplitude_modulation = nx(); c.causal = nx(); c.activation = nx(); c.adain = nx();
+    c.conv_bias = nx(); c.convt_bias = nx();
+    c.noise = nx(); c.noise_hidden = nx(); c.noise_bands = nx(); c.n_noise_ratios = nx();
+    for (int k = 0; k < RAVE_MAX_RATIOS; ++k) c.noise_ratios[k] = nx();
+    c.rvq_quantizers = nx(); c.rvq_codebook_size = nx(); c.fuse_units = nx();
+    c.leaky_slope = (float)slope;
+    return c;
+}
+
+struct Engine : torch::CustomClassHolder {
+    // constructor arguments, kept for pickling
+    std::vector<int64_t> cfg_ints;
+    double slope;
+    std::vector<std::string> names;
+    std::vector<at::Tensor> params;
+    at::Tensor speaker;
+    int64_t precision;
+    int64_t stream_block;
+    // engine state
+    rave_model_config cfg{};
+    rave_model* m = nullptr;
+    rave_stream* s_enc = nullptr;   // streaming: one state per direction (nn~'s encode / decode
+    rave_stream* s_dec = nullptr;   // methods run independently), created on first use
+    int64_t s_enc_b = 0, s_dec_b = 0;
+    int device = 0;
+    int hop = 1;
+
+    Engine(std::vector<int64_t> ci, double sl, std::vector<std::string> nm, std::vector<at::Tensor> ps, at::Tensor spk,
+           int64_t prec, int64_t block)
+        : cfg_ints(std::move(ci)), slope(sl), names(std::move(nm)), params(std::move(ps)), speaker(std::move(spk)),
+          precision(prec), stream_block(block) {
+        TORCH_CHECK_VALUE(names.size() == params.size(), "one tensor per parameter name");
+        cfg = config_from(cfg_ints, slope);
+        hop = cfg.n_band;
+        for (int i = 0; i < cfg.n_ratios; ++i) hop *= cfg.ratios[i];
+        std::vector<at::Tensor> host;
+        std::vector<rave_param> p(names.size());
+        for (size_t i = 0; i < names.size(); ++i) {
+            host.push_back(params[i].detach().to(at::kCPU, at::kFloat).contiguous());
+            p[i] = rave_param{names[i].c_str(), host.back().data_ptr<float>(), host.back().numel()};
+        }
+        at::Tensor spk_h = speaker.detach().to(at::kCPU, at::kFloat).contiguous();
+        device = c10::hip::current_device();
+        check(rave_model_create(&cfg, p.data(), (int)p.size(), spk_h.data_ptr<float>(), (int)precision, &m),
+              "rave_model_create");
+    }
+    ~Engine() override {
+        if (s_enc) rave_stream_destroy(s_enc);
+        if (s_dec) rave_stream_destroy(s_dec);
+        if (m) rave_model_destroy(m);
+    }
+
+    void* cur() const { return c10::hip::getCurrentHIPStream(device).stream(); }
+    void on_device(const at::Tensor& t, const char* what) const {
+        TORCH_CHECK_VALUE(t.is_cuda() && t.get_device() == device, what, " must be on cuda:", device);
+    }
+    int64_t zc() const { return cfg.latent_size + cfg.speaker_size; }
+
+    at::Tensor encode(at::Tensor x) {
+        on_device(x, "x");
+        TORCH_CHECK_VALUE(x.dim() == 3 && x.size(1) == 1 && x.scalar_type() == at::kFloat, "x must be (B, 1, T) float32");
+        c10::hip::HIPGuard g((c10::DeviceIndex)device);
+        x = x.contiguous();
+        auto z = at::empty({x.size(0), zc(), x.size(2) / hop}, x.options());
+        check(rave_model_encode(m, x.data_ptr<float>(), (int)x.size(0), (int)x.size(2), z.data_ptr<float>(), cur()),
+              "encode");
+        return z;
+    }
+    at::Tensor decode(at::Tensor z) {
+        on_device(z, "z");
+        TORCH_CHECK_VALUE(z.dim() == 3 && z.size(1) == zc() && z.scalar_type() == at::kFloat,
+                          "z must be (B, latent + speaker, F) float32");
+        c10::hip::HIPGuard g((c10::DeviceIndex)device);
+        z = z.contiguous();
+        auto y = at::empty({z.size(0), 1, z.size(2) * hop}, z.options());
+        check(rave_model_decode(m, z.data_ptr<float>(), (int)z.size(0), (int)z.size(2), y.data_ptr<float>(), nullptr,
+                                cur()),
+              "decode");
+        return y;
+    }
+    at::Tensor forward(at::Tensor x) {
+        on_device(x, "x");
+        TORCH_CHECK_VALUE(x.dim() == 3 && x.size(1) == 1 && x.scalar_type() == at::kFloat, "x must be (B, 1, T) float32");
+        c10::hip::HIPGuard g((c10::DeviceIndex)device);
+        x = x.contiguous();
+        auto y = at::empty_like(x);
+        check(rave_model_forward(m, x.data_ptr<float>(), (int)x.size(0), (int)x.size(2), y.data_ptr<float>(), nullptr,
+                                 cur()),
+              "forward");
+        return y;
+    }
+    at::Tensor encode_codes(at::Tensor x) {
+        on_device(x, "x");
+        c10::hip::HIPGuard g((c10::DeviceIndex)device);
+        x = x.contiguous();
+        auto idx = at::empty({x.size(0), (int64_t)cfg.rvq_quantizers, x.size(2) / hop}, x.options().dtype(at::kLong));
+        check(rave_model_encode_codes(m, x.data_ptr<float>(), (int)x.size(0), (int)x.size(2), idx.data_ptr<int64_t>(),
+                                      cur()),
+              "encode_codes");
+        return idx;
+    }
+    at::Tensor decode_codes(at::Tensor idx) {
+        on_device(idx, "idx");
+        TORCH_CHECK_VALUE(idx.scalar_type() == at::kLong, "idx must be int64");
+        c10::hip::HIPGuard g((c10::DeviceIndex)device);
+        idx = idx.contiguous();
+        auto y = at::empty({idx.size(0), 1, idx.size(2) * hop}, idx.options().dtype(at::kFloat));
+        check(rave_model_decode_codes(m, idx.data_ptr<int64_t>(), (int)idx.size(0), (int)idx.size(2),
+                                      y.data_ptr<float>(), nullptr, cur()),
+              "decode_codes");
+        return y;
+    }
+    // cached_conv streaming (one block of stream_block samples per call)
+    rave_stream* stream_for(rave_stream*& s, int64_t& sb, int64_t batch) {
+        if (!s || sb != batch) {
+            if (s) rave_stream_destroy(s);
+            s = nullptr;
+            check(rave_stream_create(m, (int)batch, (int)stream_block, RAVE_STREAM_GRAPH, &s), "rave_stream_create");
+            sb = batch;
+        }
+        return s;
+    }
+    at::Tensor stream_encode(at::Tensor x) {
+        on_device(x, "x");
+        TORCH_CHECK_VALUE(x.dim() == 3 && x.size(1) == 1 && x.size(2) == stream_block, "x must be (B, 1, block)");
+        c10::hip::HIPGuard g((c10::DeviceIndex)device);
+        x = x.contiguous();
+        rave_stream* s = stream_for(s_enc, s_enc_b, x.size(0));
+        auto z = at::empty({x.size(0), zc(), stream_block / hop}, x.options());
+        check(rave_stream_encode(s, x.data_ptr<float>(), z.data_ptr<float>(), cur()), "stream_encode");
+        return z;
+    }
+    at::Tensor stream_decode(at::Tensor z) {
+        on_device(z, "z");
+        TORCH_CHECK_VALUE(z.dim() == 3 && z.size(1) == zc() && z.size(2) == stream_block / hop,
+                          "z must be (B, latent + speaker, block / hop)");
+        c10::hip::HIPGuard g((c10::DeviceIndex)device);
+        z = z.contiguous();
+        rave_stream* s = stream_for(s_dec, s_dec_b, z.size(0));
+        auto y = at::empty({z.size(0), 1, stream_block}, z.options());
+        check(rave_stream_decode(s, z.data_ptr<float>(), y.data_ptr<float>(), nullptr, cur()), "stream_decode");
+        return y;
+    }
+    void stream_reset() {
+        if (s_enc) check(rave_stream_reset(s_enc, cur()), "stream_reset");
+        if (s_dec) check(rave_stream_reset(s_dec, cur()), "stream_reset");
+    }
+    // AdaIN controls (ScriptedRAVE.update_adain): -1 keeps a flag
+    void adain_control(int64_t learn_x, int64_t learn_y, bool reset_x, bool reset_y) {
+        check(rave_model_adain_control(m, (int)learn_x, (int)learn_y, reset_x, reset_y), "adain_control");
+    }
+    int64_t get_hop() const { return hop; }
+    int64_t latent_channels() const { return zc(); }
+    int64_t block() const { return stream_block; }
+};
+
+using State = std::tuple<std::vector<int64_t>, double, std::vector<std::string>, std::vector<at::Tensor>, at::Tensor,
+                         int64_t, int64_t>;
+
+}  // namespace
+
+TORCH_LIBRARY(rave_amd, lib) {
+    lib.class_<Engine>("Engine")
+        .def(torch::init<std::vector<int64_t>, double, std::vector<std::string>, std::vector<at::Tensor>, at::Tensor,
+                         int64_t, int64_t>())
+        .def("encode", &Engine::encode)
+        .def("decode", &Engine::decode)
+        .def("forward", &Engine::forward)
+        .def("encode_codes", &Engine::encode_codes)
+        .def("decode_codes", &Engine::decode_codes)
+        .def("stream_encode", &Engine::stream_encode)
+        .def("stream_decode", &Engine::stream_decode)
+        .def("stream_reset", &Engine::stream_reset)
+        .def("adain_control", &Engine::adain_control)
+        .def("hop", &Engine::get_hop)
+        .def("latent_channels", &Engine::latent_channels)
+        .def("block", &Engine::block)
+        .def_pickle(
+            [](const c10::intrusive_ptr<Engine>& e) -> State {
+                std::vector<at::Tensor> ps;
+                for (auto& p : e->params) ps.push_back(p.detach().cpu());
+                return State(e->cfg_ints, e->slope, e->names, ps, e->speaker.detach().cpu(), e->precision,
+                             e->stream_block);
+            },
+            [](State st) -> c10::intrusive_ptr<Engine> {
+                return c10::make_intrusive<Engine>(std::get<0>(st), std::get<1>(st), std::get<2>(st), std::get<3>(st),
+                                                   std::get<4>(st), std::get<5>(st), std::get<6>(st));
+            });
+}

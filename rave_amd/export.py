@@ -209,3 +209,7 @@ class NNTildeRAVE:
         for s in (self._enc_stream, self._dec_stream):
             if s is not None:
                 s.reset()
+
+
+# The TorchScript (nn~ .ts) export lives in rave_amd/scripted.py (no postponed
+# annotations there: TorchScript resolves attribute annotations at script time).

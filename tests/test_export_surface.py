@@ -95,3 +95,17 @@ def test_update_adain_applies_flags_once():
     m.adain.calls.clear()
     w.update_adain()                       # the reset fired once
     assert m.adain.calls == [("learn", False, True)]
+
+
+def test_torch_library_registers_engine():
+    """The TORCH_LIBRARY binding loads on a CPU host and registers the custom
+    class; a malformed config is rejected before any device work."""
+    import torch
+    from rave_amd.scripted import config_ints, load_torch_ops
+    load_torch_ops()
+    load_torch_ops()                      # idempotent
+    eng = torch.classes.rave_amd.Engine
+    assert eng is not None
+    assert len(config_ints(rcfg.v2())) == 108
+    with pytest.raises((ValueError, RuntimeError)):
+        torch.classes.rave_amd.Engine([1, 2, 3], 0.2, [], [], torch.zeros(256), 0, 2048)

@@ -1088,3 +1088,80 @@ def test_stream_conv_shapes_split16_vs_f32(N, dev, capacity):
         assert np.isfinite(ref).all(), n.name
         err = maxabs(outs[1], ref)
         assert err <= 2e-5 * max(1.0, np.abs(ref).max()), (n.name, n.c_in, n.c_out, n.kernel, ts, err)
+
+
+# ------------------------------------------------------------------ TorchScript (nn~) export
+def test_scripted_export_roundtrip_golden(dev, golden, tmp_path):
+    """ScriptedRAVE -> torch.jit.script -> save -> torch.jit.load (what nn~
+    does with the .ts, scripts/export.py:618): the loaded module's encode /
+    decode match the reference fixtures and its nn~ metadata is intact."""
+    from rave_amd import config as rcfg
+    from rave_amd.scripted import ScriptedRAVE
+    from rave_amd.weights import init_params
+    g = golden("v2")
+    cfg = rcfg.v2()
+    m = ScriptedRAVE(cfg, init_params(cfg, seed=int(g["seed"])), g["speaker"], hk=_golden_hk(golden))
+    path = str(tmp_path / "rave_v2.ts")
+    m.export_to_ts(path)
+    ts = torch.jit.load(path)
+    assert ts.get_methods() == ["encode", "decode", "forward"]
+    assert ts.get_method_params("encode") == [1, 1, 320, 1024]
+    assert ts.set_speaker(3) == 0 and ts.get_speaker() == 3
+    z = ts.encode(torch.from_numpy(g["x"]).to(dev))
+    y = ts.decode(torch.from_numpy(g["z"]).to(dev))
+    torch.cuda.synchronize()
+    assert maxabs(z.cpu().numpy()[:, :64], g["z"][:, :64]) < TOL
+    assert maxabs(y.cpu().numpy(), g["y"]) < TOL
+
+
+def test_scripted_streaming_matches_streaming_rave(dev):
+    """A scripted causal model streams block by block through the engine's
+    hipGraph streams: equal to rave_amd.StreamingRAVE; a 2-block buffer is
+    split into blocks."""
+    from rave_amd import config as rcfg
+    from rave_amd.scripted import ScriptedRAVE
+    from rave_amd.model import RAVE
+    from rave_amd.streaming import StreamingRAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.causal()
+    p, spk = init_params(cfg, 7), init_speaker(cfg, 7)
+    ts = torch.jit.script(ScriptedRAVE(cfg, p, spk, block=2048))
+    ref = StreamingRAVE(RAVE(cfg, p, spk, device=dev), batch=1, block=2048)
+    gen = torch.Generator().manual_seed(4)
+    x = (0.2 * torch.randn(1, 1, 3 * 4096, generator=gen)).to(dev)
+    for i in range(3):
+        xi = x[..., i * 4096:(i + 1) * 4096]
+        y = ts.forward(xi)
+        y_ref = torch.cat([ref.forward(xi[..., :2048].contiguous()), ref.forward(xi[..., 2048:].contiguous())], -1)
+        torch.cuda.synchronize()
+        assert float((y - y_ref).abs().max()) < 1e-6
+
+
+def test_scripted_adain_attributes(dev):
+    """set_learn_target on the scripted module drives the engine's AdaIN (the
+    output changes once target statistics exist and transfer is on)."""
+    from rave_amd import config as rcfg
+    from rave_amd.scripted import ScriptedRAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.v3(capacity=8)
+    ts = torch.jit.script(ScriptedRAVE(cfg, init_params(cfg, 1), init_speaker(cfg, 1)))
+    gen = torch.Generator().manual_seed(8)
+    x_tgt = (0.5 * torch.randn(1, 1, 4096, generator=gen)).to(dev)
+    x = (0.2 * torch.randn(1, 1, 4096, generator=gen)).to(dev)
+    y0 = ts.forward(x)
+    ts.set_learn_target(True)
+    ts.encode(x_tgt)
+    ts.set_learn_target(False)
+    ts.set_learn_source(True)
+    ts.encode(x)
+    ts.set_learn_source(False)
+    y1 = ts.forward(x)
+    torch.cuda.synchronize()
+    assert float((y1 - y0).abs().max()) > 1e-3
+    ts.set_reset_target(True)
+    ts.set_reset_source(True)
+    ts.encode(x)
+    assert ts.get_reset_target() is False
+    y2 = ts.forward(x)
+    torch.cuda.synchronize()
+    assert float((y2 - y0).abs().max()) < 1e-6
