@@ -402,6 +402,7 @@ struct Model {
     Plan& encode_plan(int B, int T, bool codes);
     Plan& decode_plan(int B, int Fz, bool codes);
     Plan& plan_of(int which, int B, int T);
+    void run_kind(int which, int batch, int t, const void* in, void* out, const float* noise, hipStream_t st);
     const float* noise_ptr(const float* u, int B, int Fz, hipStream_t st);
     template <typename F>
     double time_native(F&& fn, int reps = 5);
@@ -1147,6 +1148,14 @@ Plan& Model::plan_of(int which, int B, int T) {
     }
 }
 
+// One call of a plan kind over `batch` items: I/O slot 0 = in, 1 = out, 2 = noise.
+void Model::run_kind(int which, int batch, int t, const void* in, void* out, const float* noise, hipStream_t st) {
+    cur_stream = st;
+    Plan& p = plan_of(which, batch, t);
+    void* slots[3] = {(void*)in, out, (void*)noise};
+    p.run(slots, (which == 1 || which == 3) && cfg.noise ? 3 : 2, st);
+}
+
 const float* Model::noise_ptr(const float* u, int B, int Fz, hipStream_t st) {
     if (!cfg.noise) return nullptr;
     if (u) return u;
@@ -1405,9 +1414,7 @@ extern "C" int rave_model_encode(rave_model* h, const float* x, int batch, int t
         Model* m = model_of(h);
         if (!x || !z) fail(RAVE_ERR_ARG, "encode: null tensor");
         check_len(m, batch, t);
-        m->cur_stream = as_stream(stream);
-        void* slots[2] = {(void*)x, (void*)z};
-        m->encode_plan(batch, t, false).run(slots, 2, as_stream(stream));
+        m->run_kind(0, batch, t, x, z, nullptr, as_stream(stream));
     });
 }
 
@@ -1417,10 +1424,8 @@ extern "C" int rave_model_decode(rave_model* h, const float* z, int batch, int f
         Model* m = model_of(h);
         if (!z || !y) fail(RAVE_ERR_ARG, "decode: null tensor");
         if (batch <= 0 || frames <= 0) fail(RAVE_ERR_ARG, "batch and frames must be positive");
-        m->cur_stream = as_stream(stream);
-        Plan& p = m->decode_plan(batch, frames, false);
-        void* slots[3] = {(void*)z, (void*)y, (void*)m->noise_ptr(noise_u, batch, frames, as_stream(stream))};
-        p.run(slots, m->cfg.noise ? 3 : 2, as_stream(stream));
+        m->run_kind(1, batch, frames, z, y, m->noise_ptr(noise_u, batch, frames, as_stream(stream)),
+                    as_stream(stream));
     });
 }
 
@@ -1438,13 +1443,9 @@ extern "C" int rave_model_forward(rave_model* h, const float* x, int batch, int 
             RAVE_HIP_OR_THROW(hipMalloc(&m->fwd_z, (size_t)nz * 4));
             m->fwd_z_n = nz;
         }
-        m->cur_stream = as_stream(stream);
         if (m->cfg.rvq_quantizers > 0) fail(RAVE_ERR_ARG, "forward of a discrete config: use encode_codes / decode_codes");
-        void* s1[2] = {(void*)x, (void*)m->fwd_z};
-        m->encode_plan(batch, t, false).run(s1, 2, as_stream(stream));
-        Plan& d = m->decode_plan(batch, Fz, false);
-        void* s2[3] = {(void*)m->fwd_z, (void*)y, (void*)m->noise_ptr(noise_u, batch, Fz, as_stream(stream))};
-        d.run(s2, m->cfg.noise ? 3 : 2, as_stream(stream));
+        m->run_kind(0, batch, t, x, m->fwd_z, nullptr, as_stream(stream));
+        m->run_kind(1, batch, Fz, m->fwd_z, y, m->noise_ptr(noise_u, batch, Fz, as_stream(stream)), as_stream(stream));
     });
 }
 
@@ -1454,9 +1455,7 @@ extern "C" int rave_model_encode_codes(rave_model* h, const float* x, int batch,
         if (m->cfg.rvq_quantizers <= 0) fail(RAVE_ERR_ARG, "encode_codes needs a discrete (RVQ) config");
         if (!x || !idx) fail(RAVE_ERR_ARG, "encode_codes: null tensor");
         check_len(m, batch, t);
-        m->cur_stream = as_stream(stream);
-        void* slots[2] = {(void*)x, (void*)idx};
-        m->encode_plan(batch, t, true).run(slots, 2, as_stream(stream));
+        m->run_kind(2, batch, t, x, idx, nullptr, as_stream(stream));
     });
 }
 
@@ -1467,10 +1466,8 @@ extern "C" int rave_model_decode_codes(rave_model* h, const int64_t* idx, int ba
         if (m->cfg.rvq_quantizers <= 0) fail(RAVE_ERR_ARG, "decode_codes needs a discrete (RVQ) config");
         if (!idx || !y) fail(RAVE_ERR_ARG, "decode_codes: null tensor");
         if (batch <= 0 || frames <= 0) fail(RAVE_ERR_ARG, "batch and frames must be positive");
-        m->cur_stream = as_stream(stream);
-        Plan& p = m->decode_plan(batch, frames, true);
-        void* slots[3] = {(void*)idx, (void*)y, (void*)m->noise_ptr(noise_u, batch, frames, as_stream(stream))};
-        p.run(slots, m->cfg.noise ? 3 : 2, as_stream(stream));
+        m->run_kind(3, batch, frames, idx, y, m->noise_ptr(noise_u, batch, frames, as_stream(stream)),
+                    as_stream(stream));
     });
 }
 

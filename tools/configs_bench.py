@@ -61,15 +61,22 @@ def c3(precision, blocks, warmup, dev):
     cfg = rcfg.causal()
     m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=precision)
     blk = 2048
-    s = StreamingRAVE(m, batch=1, block=blk)
     Fz = blk // cfg.hop
     n = warmup + blocks
     gen = torch.Generator().manual_seed(0)
     z = torch.randn(n, 1, cfg.dec_in, Fz, generator=gen).to(dev)
     x = (0.2 * torch.randn(n, 1, 1, blk, generator=gen)).to(dev)
     out = {"workload": "v2 --config causal streaming, 2048-sample blocks, B=1 (BASELINE configs[2])",
-           "block_samples": blk, "blocks_timed": blocks, "decode_delay_samples": s.decode_delay}
-    for name, fn in (("decode", lambda i: s.decode(z[i])), ("encode_decode", lambda i: s.forward(x[i]))):
+           "block_samples": blk, "blocks_timed": blocks}
+    runs = []
+    for graph in (True, False):
+        s = StreamingRAVE(m, batch=1, block=blk, graph=graph)
+        out["decode_delay_samples"] = s.decode_delay
+        tag = "" if graph else "_eager"
+        runs += [("decode" + tag, s, (lambda s: lambda i: s.decode(z[i]))(s)),
+                 ("encode_decode" + tag, s, (lambda s: lambda i: s.forward(x[i]))(s))]
+    out["note"] = "default: each block replays a captured hipGraph (RAVE_STREAM_GRAPH); *_eager: plan replay"
+    for name, s, fn in runs:
         s.reset()
         lat = []
         for i in range(n):
