@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 8
+#define RAVE_ABI_VERSION 9
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 
@@ -405,6 +405,72 @@ int rave_plan_op_times(rave_plan* plan, float* ms, int n);
  * inputs of the engine's launch-configuration timing. */
 int rave_fill_uniform(float* y, int64_t n, uint64_t seed, float lo, float hi, void* stream);
 
+/* ================================================================ edges of the path
+ * Resampler (rave/resampler.py:9-66) and the SpeakerRAVE pooling head
+ * (rave/CombinedRave.py:301-328); their convolutions run on rave_conv1d /
+ * rave_residual_unit.  All HBM-bound VALU kernels (csrc/speaker.hip).
+ *
+ * rave_fir: polyphase FIR, the two cached_conv Conv1d of the Resampler
+ *   y[b, t*phases + p] = sum_k h[p*taps + k] * x[b, t*stride + k - pad_left]
+ * for t in [0, t_out); x columns outside [0, t_in) read as zero.  Decimation
+ * (to_model_sampling_rate :60-61): phases 1, stride = ratio.  Interpolation
+ * (from_model_sampling_rate :63-66, the (B, ratio, T) -> (B, 1, ratio T)
+ * interleave fused): phases = ratio, stride 1.  Streaming: x = [history | block],
+ * pad_left 0.  Limits: taps * phases <= 4096, taps <= 1024. */
+typedef struct rave_fir_args {
+    int32_t batch, t_in, t_out, phases, taps, stride, pad_left, _pad0;
+    const float* x; int64_t x_sb;
+    float* y;       int64_t y_sb;
+    const float* h;
+} rave_fir_args;
+int rave_fir(const rave_fir_args* a, void* stream);
+
+/* rave_row_stats: per (b, c) row of act(x) over t in [0, t_len):
+ *   y[b*y_sb + c] = mean,  y[b*y_sb + channels + c] = sqrt(clamp(var, var_min, var_max))
+ * with the unbiased variance (torch.var, rave/CombinedRave.py:316-318).
+ * act: RAVE_ACT_NONE or RAVE_ACT_LEAKY (slope leaky_slope) applied on read. */
+typedef struct rave_row_stats_args {
+    int32_t batch, channels, t_len, act;
+    float leaky_slope, var_min, var_max, _pad0;
+    const float* x; int64_t x_sb, x_sc;
+    float* y;       int64_t y_sb;
+} rave_row_stats_args;
+int rave_row_stats(const rave_row_stats_args* a, void* stream);
+
+/* rave_attn_pool: attentive statistics pooling (rave/CombinedRave.py:320-323):
+ * w = softmax_t(logits[b, c, :]),  mu = sum_t act(x) w,
+ * sg = sqrt(clamp(sum_t act(x)^2 w - mu^2, var_min, var_max));
+ * y[b*y_sb + c] = mu, y[b*y_sb + channels + c] = sg. */
+typedef struct rave_attn_pool_args {
+    int32_t batch, channels, t_len, act;
+    float leaky_slope, var_min, var_max, _pad0;
+    const float* x;      int64_t x_sb, x_sc;
+    const float* logits; int64_t l_sb, l_sc;
+    float* y;            int64_t y_sb;
+} rave_attn_pool_args;
+int rave_attn_pool(const rave_attn_pool_args* a, void* stream);
+
+/* rave_linear: y[b*y_sb + o] = bias[o] + sum_i w[o*n_in + i] * x[b*x_sb + i]
+ * (nn.Linear; also the per-clip bias of a conv whose input has time-constant
+ * channels).  bias may be NULL. */
+typedef struct rave_linear_args {
+    int32_t batch, n_in, n_out, _pad0;
+    const float* x; int64_t x_sb;
+    const float* w;
+    const float* bias;
+    float* y;       int64_t y_sb;
+} rave_linear_args;
+int rave_linear(const rave_linear_args* a, void* stream);
+
+/* rave_maxpool: nn.MaxPool1d(kernel) (stride = kernel, no padding):
+ * y[b, c, t] = max_j x[b, c, t*kernel + j], t in [0, t_out). */
+typedef struct rave_maxpool_args {
+    int32_t batch, channels, t_out, kernel;
+    const float* x; int64_t x_sb, x_sc;
+    float* y;       int64_t y_sb, y_sc;
+} rave_maxpool_args;
+int rave_maxpool(const rave_maxpool_args* a, void* stream);
+
 /* ================================================================ model engine
  * The whole RAVE.encode / decode / forward (rave/model.py:594-634) behind one
  * handle, for hosts with no Python (nn~ is C++): the model graph of
@@ -504,6 +570,11 @@ int rave_model_noise_shape(const rave_model* m, int batch, int frames, int64_t* 
  * row0: first buffer row this process's batch uses (data-parallel shards). */
 int rave_model_adain_control(rave_model* m, int learn_x, int learn_y, int reset_x, int reset_y);
 int rave_model_set_row0(rave_model* m, int row0);
+/* Replace the constant speaker embedding the encode / decode_codes paths
+ * concatenate (speaker_size floats, host or device memory) -- the nn~
+ * `speaker` attribute's choice among embeddings (scripts/export.py:384-396).
+ * Asynchronous on `stream`; later calls on that stream see the new value. */
+int rave_model_set_speaker(rave_model* m, const float* speaker, void* stream);
 int rave_model_adain_count(const rave_model* m);
 /* module i: name, channels, and its buffers copied out / in (host, synchronous):
  * stats (4, max_batch, C) = mean_x, std_x, mean_y, std_y; counters[2] =

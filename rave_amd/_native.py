@@ -36,7 +36,7 @@ OP_NOISE = 9
 OP_ADAIN = 10
 OP_UNIT = 11
 OP_STACK = 12
-ABI_VERSION = 8
+ABI_VERSION = 9
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 
 # GEMM arithmetic of conv / unit ops (include/rave_amd.h RAVE_PREC_*)
@@ -141,6 +141,35 @@ class StackArgs(C.Structure):
                    for u in range(STACK_UNITS)])
 
 
+class FirArgs(C.Structure):
+    _fields_ = [("batch", i32), ("t_in", i32), ("t_out", i32), ("phases", i32), ("taps", i32),
+                ("stride", i32), ("pad_left", i32), ("_pad0", i32),
+                ("x", vp), ("x_sb", i64), ("y", vp), ("y_sb", i64), ("h", vp)]
+
+
+class RowStatsArgs(C.Structure):
+    _fields_ = [("batch", i32), ("channels", i32), ("t_len", i32), ("act", i32),
+                ("leaky_slope", f32), ("var_min", f32), ("var_max", f32), ("_pad0", i32),
+                ("x", vp), ("x_sb", i64), ("x_sc", i64), ("y", vp), ("y_sb", i64)]
+
+
+class AttnPoolArgs(C.Structure):
+    _fields_ = [("batch", i32), ("channels", i32), ("t_len", i32), ("act", i32),
+                ("leaky_slope", f32), ("var_min", f32), ("var_max", f32), ("_pad0", i32),
+                ("x", vp), ("x_sb", i64), ("x_sc", i64), ("logits", vp), ("l_sb", i64), ("l_sc", i64),
+                ("y", vp), ("y_sb", i64)]
+
+
+class LinearArgs(C.Structure):
+    _fields_ = [("batch", i32), ("n_in", i32), ("n_out", i32), ("_pad0", i32),
+                ("x", vp), ("x_sb", i64), ("w", vp), ("bias", vp), ("y", vp), ("y_sb", i64)]
+
+
+class MaxPoolArgs(C.Structure):
+    _fields_ = [("batch", i32), ("channels", i32), ("t_out", i32), ("kernel", i32),
+                ("x", vp), ("x_sb", i64), ("x_sc", i64), ("y", vp), ("y_sb", i64), ("y_sc", i64)]
+
+
 MAX_RATIOS = 8
 MAX_DILATIONS = 8
 
@@ -179,7 +208,8 @@ class Reloc(C.Structure):
 
 
 STRUCTS = [ConvArgs, AnalysisArgs, SynthesisArgs, FillArgs, RvqArgs, ShiftArgs, PlanOp, Reloc,
-           CopyArgs, NoiseArgs, AdainArgs, UnitArgs, StackArgs, ModelConfig, Param, OpInfo]
+           CopyArgs, NoiseArgs, AdainArgs, UnitArgs, StackArgs, ModelConfig, Param, OpInfo,
+           FirArgs, RowStatsArgs, AttnPoolArgs, LinearArgs, MaxPoolArgs]
 
 # every exported symbol of include/rave_amd.h
 EXPORTS = [
@@ -196,10 +226,12 @@ EXPORTS = [
     "rave_model_param_count", "rave_model_param_info", "rave_model_create", "rave_model_destroy",
     "rave_model_encode", "rave_model_decode", "rave_model_forward", "rave_model_encode_codes",
     "rave_model_decode_codes", "rave_model_noise_shape", "rave_model_adain_control", "rave_model_set_row0",
+    "rave_model_set_speaker",
     "rave_model_adain_count", "rave_model_adain_info", "rave_model_adain_get", "rave_model_adain_set",
     "rave_model_tuning_get", "rave_model_tuning_set", "rave_model_plan_ops", "rave_model_profile",
     "rave_model_op_times", "rave_stream_create", "rave_stream_destroy", "rave_stream_reset",
     "rave_stream_encode", "rave_stream_decode", "rave_stream_delay",
+    "rave_fir", "rave_row_stats", "rave_attn_pool", "rave_linear", "rave_maxpool",
 ]
 
 
@@ -240,7 +272,9 @@ def _load():
                      ("rave_rvq_encode", RvqArgs), ("rave_rvq_decode", RvqArgs),
                      ("rave_shift_history", ShiftArgs), ("rave_copy", CopyArgs),
                      ("rave_noise_synth", NoiseArgs), ("rave_adain", AdainArgs),
-                     ("rave_residual_unit", UnitArgs), ("rave_residual_stack", StackArgs)]:
+                     ("rave_residual_unit", UnitArgs), ("rave_residual_stack", StackArgs),
+                     ("rave_fir", FirArgs), ("rave_row_stats", RowStatsArgs), ("rave_attn_pool", AttnPoolArgs),
+                     ("rave_linear", LinearArgs), ("rave_maxpool", MaxPoolArgs)]:
         getattr(lib, name).argtypes = [C.POINTER(st), vp]
     lib.rave_plan_create.argtypes = [C.POINTER(PlanOp), C.c_int, C.POINTER(Reloc), C.c_int,
                                      C.POINTER(vp)]
@@ -264,6 +298,7 @@ def _load():
     lib.rave_model_noise_shape.argtypes = [vp, C.c_int, C.c_int, C.POINTER(i64)]
     lib.rave_model_adain_control.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int]
     lib.rave_model_set_row0.argtypes = [vp, C.c_int]
+    lib.rave_model_set_speaker.argtypes = [vp, vp, vp]
     lib.rave_model_adain_count.argtypes = [vp]
     lib.rave_model_adain_info.argtypes = [vp, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_int),
                                           C.POINTER(C.c_int)]

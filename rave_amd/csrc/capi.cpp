@@ -39,6 +39,9 @@ extern "C" int rave_struct_sizes(int64_t* out, int n) {
         (int64_t)sizeof(rave_adain_args),        (int64_t)sizeof(rave_unit_args),
         (int64_t)sizeof(rave_stack_args),        (int64_t)sizeof(rave_model_config),
         (int64_t)sizeof(rave_param),             (int64_t)sizeof(rave_op_info),
+        (int64_t)sizeof(rave_fir_args),          (int64_t)sizeof(rave_row_stats_args),
+        (int64_t)sizeof(rave_attn_pool_args),    (int64_t)sizeof(rave_linear_args),
+        (int64_t)sizeof(rave_maxpool_args),
     };
     const int cnt = (int)(sizeof(sizes) / sizeof(sizes[0]));
     if (!out) return cnt;

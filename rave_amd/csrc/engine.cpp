@@ -1518,6 +1518,18 @@ extern "C" int rave_model_set_row0(rave_model* h, int row0) {
     });
 }
 
+extern "C" int rave_model_set_speaker(rave_model* h, const float* speaker, void* stream) {
+    return guarded([&] {
+        Model* m = model_of(h);
+        if (!speaker) fail(RAVE_ERR_ARG, "set_speaker: null embedding");
+        if (m->cfg.speaker_size == 0) fail(RAVE_ERR_ARG, "set_speaker: the model has no speaker channels");
+        // host or device source (unified addressing); ordered on the caller's stream
+        // before every later encode/decode (and streaming graph replay) on it
+        RAVE_HIP_OR_THROW(hipMemcpyAsync(m->arena + m->spk_off, speaker, sizeof(float) * m->cfg.speaker_size,
+                                         hipMemcpyDefault, as_stream(stream)));
+    });
+}
+
 extern "C" int rave_model_adain_count(const rave_model* h) {
     int n = 0;
     int rc = guarded([&] { n = (int)model_of(const_cast<rave_model*>(h))->g.adain_modules.size(); });

@@ -198,10 +198,66 @@ struct Engine : torch::CustomClassHolder {
     void adain_control(int64_t learn_x, int64_t learn_y, bool reset_x, bool reset_y) {
         check(rave_model_adain_control(m, (int)learn_x, (int)learn_y, reset_x, reset_y), "adain_control");
     }
+    // the constant speaker embedding encode concatenates (nn~ `speaker` choice)
+    void set_speaker(at::Tensor emb) {
+        TORCH_CHECK_VALUE(emb.numel() == cfg.speaker_size, "speaker embedding must have ", cfg.speaker_size, " values");
+        c10::hip::HIPGuard g((c10::DeviceIndex)device);
+        at::Tensor src = emb.detach().to(at::Device(at::kCUDA, device), at::kFloat).contiguous();
+        check(rave_model_set_speaker(m, src.data_ptr<float>(), cur()), "set_speaker");
+        // src came from torch's caching allocator on this stream, so freeing it on
+        // return is stream-ordered after the copy
+        speaker = emb.detach().cpu().to(at::kFloat).reshape({-1}).clone();    // travels with the pickle
+    }
     int64_t get_hop() const { return hop; }
     int64_t latent_channels() const { return zc(); }
     int64_t block() const { return stream_block; }
 };
+
+// rave_amd::fir -- the Resampler's cached_conv Conv1d (rave/resampler.py:29-58) on
+// rave_fir: x (B, T) at any stride; h (P, K); y (B, P * T_out) interleaved.
+// Offline: zero padding (pad_left, pad_right).  Streaming: `hist` (B, H) with
+// H = pad_left + pad_right + stride_delay is the cached input (CachedConv1d),
+// updated in place; T must be a multiple of the stride.
+at::Tensor fir_op(at::Tensor x, at::Tensor h, int64_t stride, int64_t pad_left, int64_t pad_right,
+                  c10::optional<at::Tensor> hist) {
+    TORCH_CHECK_VALUE(x.is_cuda() && x.dim() == 2 && x.scalar_type() == at::kFloat, "x must be (B, T) float32 on GPU");
+    TORCH_CHECK_VALUE(h.dim() == 2 && h.scalar_type() == at::kFloat, "h must be (phases, taps) float32");
+    TORCH_CHECK_VALUE(stride > 0 && pad_left >= 0 && pad_right >= 0, "bad stride / padding");
+    c10::hip::HIPGuard g((c10::DeviceIndex)x.get_device());
+    const int64_t B = x.size(0), T = x.size(1), P = h.size(0), K = h.size(1);
+    at::Tensor hd = h.to(x.device()).contiguous();
+    at::Tensor src;
+    int64_t t_in, t_out, pl;
+    if (hist.has_value()) {
+        at::Tensor hs = *hist;
+        TORCH_CHECK_VALUE(hs.is_cuda() && hs.dim() == 2 && hs.size(0) == B && hs.scalar_type() == at::kFloat,
+                          "hist must be (B, H) float32 on the GPU");
+        TORCH_CHECK_VALUE(T % stride == 0, "streaming block must be a multiple of the stride");
+        src = at::cat({hs, x}, 1).contiguous();
+        t_in = src.size(1);
+        t_out = T / stride;
+        pl = 0;
+    } else {
+        src = x.contiguous();
+        t_in = T;
+        t_out = (T + pad_left + pad_right - K) / stride + 1;
+        pl = pad_left;
+    }
+    TORCH_CHECK_VALUE(t_out > 0, "input too short");
+    auto y = at::empty({B, P * t_out}, x.options());
+    rave_fir_args a{};
+    a.batch = (int)B; a.t_in = (int)t_in; a.t_out = (int)t_out; a.phases = (int)P; a.taps = (int)K;
+    a.stride = (int)stride; a.pad_left = (int)pl;
+    a.x = src.data_ptr<float>(); a.x_sb = src.stride(0);
+    a.y = y.data_ptr<float>(); a.y_sb = y.stride(0);
+    a.h = hd.data_ptr<float>();
+    check(rave_fir(&a, c10::hip::getCurrentHIPStream(x.get_device()).stream()), "fir");
+    if (hist.has_value()) {
+        at::Tensor hs = *hist;
+        hs.copy_(src.narrow(1, T, hs.size(1)));      // newest H samples become the cache
+    }
+    return y;
+}
 
 using State = std::tuple<std::vector<int64_t>, double, std::vector<std::string>, std::vector<at::Tensor>, at::Tensor,
                          int64_t, int64_t>;
@@ -209,6 +265,7 @@ using State = std::tuple<std::vector<int64_t>, double, std::vector<std::string>,
 }  // namespace
 
 TORCH_LIBRARY(rave_amd, lib) {
+    lib.def("fir(Tensor x, Tensor h, int stride, int pad_left, int pad_right, Tensor? hist) -> Tensor", &fir_op);
     lib.class_<Engine>("Engine")
         .def(torch::init<std::vector<int64_t>, double, std::vector<std::string>, std::vector<at::Tensor>, at::Tensor,
                          int64_t, int64_t>())
@@ -221,6 +278,7 @@ TORCH_LIBRARY(rave_amd, lib) {
         .def("stream_decode", &Engine::stream_decode)
         .def("stream_reset", &Engine::stream_reset)
         .def("adain_control", &Engine::adain_control)
+        .def("set_speaker", &Engine::set_speaker)
         .def("hop", &Engine::get_hop)
         .def("latent_channels", &Engine::latent_channels)
         .def("block", &Engine::block)

@@ -31,7 +31,11 @@ _ATTRIBUTES = (("learn_target", False), ("reset_target", False), ("learn_source"
 
 class NNTildeRAVE:
     def __init__(self, model, stereo: bool = False, streaming: Optional[bool] = None,
-                 block: int = 2048, batch: int = 1):
+                 block: int = 2048, batch: int = 1, speakers=None, target_sr: Optional[int] = None):
+        """``speakers``: embeddings the ``speaker`` attribute selects (speaker1..4,
+        scripts/export.py:84-93; any other index -> speaker5, ones, :96); None
+        keeps the model's own.  ``target_sr``: host rate, wrapping the model in
+        the Resampler (:101-106)."""
         cfg = model.cfg
         self.model, self.cfg, self.stereo = model, cfg, bool(stereo)
         self.streaming = cfg.causal if streaming is None else bool(streaming)
@@ -44,13 +48,23 @@ class NNTildeRAVE:
                              "(DiscreteScriptedRAVE), not this method table")
         self.block, self.batch = block, batch
         self.sr = getattr(cfg, "sampling_rate", 48000)                       # v2.gin SAMPLING_RATE
+        self.speakers = None if speakers is None else [torch.as_tensor(e, dtype=torch.float32).reshape(-1)
+                                                       for e in speakers]
+        self.speaker5 = torch.ones(cfg.speaker_size)
+        self._active_speaker = 0 if speakers is None else -1
+        self.resampler = None
+        if target_sr is not None and int(target_sr) != self.sr:
+            from rave_amd.resampler import Resampler
+            self.resampler = Resampler(int(target_sr), self.sr, device=getattr(model, "device", None), causal=cfg.causal,
+                                       streaming=self.streaming)
+            self.sr = int(target_sr)
         self.latent_size = cfg.latent_size + cfg.speaker_size                # encode's channels
         self._methods: Dict[str, Tuple[int, int, int, int, List[str], List[str]]] = {}
         self._attrs: Dict[str, tuple] = {}
         self._enc_stream = self._dec_stream = None
         for name, default in _ATTRIBUTES:
             self.register_attribute(name, default)
-        ratio = cfg.hop                                                      # x_len // z.shape[-1]
+        ratio = cfg.hop * (self.resampler.ratio if self.resampler else 1)   # x_len // z.shape[-1]
         channels = ["(L)", "(R)"] if self.stereo else ["(mono)"]
         audio_in = ["(signal) Input audio signal"]
         audio_out = [f"(signal) Reconstructed audio signal {c}" for c in channels]
@@ -141,6 +155,17 @@ class NNTildeRAVE:
         self._attrs["reset_source"] = (False,)
         self._attrs["reset_target"] = (False,)
 
+    def _select_speaker(self) -> None:
+        """scripts/export.py:384-396: the ``speaker`` attribute picks the
+        embedding encode concatenates (set on the model when it changes)."""
+        if self.speakers is None:
+            return
+        idx = self.get_attribute("speaker")
+        if idx != self._active_speaker:
+            emb = self.speakers[idx] if 0 <= idx < len(self.speakers) else self.speaker5
+            self.model.set_speaker(emb)
+            self._active_speaker = idx
+
     # ------------------------------------------------------------ methods
     def _enc_streamer(self, batch: int):
         """The encode stream; created (zeroed) on first use or a batch change,
@@ -176,6 +201,9 @@ class NNTildeRAVE:
         -> cat speaker)."""
         self._check("encode", x)
         self.update_adain()
+        self._select_speaker()
+        if self.resampler is not None:
+            x = self.resampler.to_model_sampling_rate(x)
         if self.streaming:
             st = self._enc_streamer(x.shape[0])
             return torch.cat([st.encode(b) for b in self._blocks(x, self.block)], -1)
@@ -195,6 +223,8 @@ class NNTildeRAVE:
             y = torch.cat([st.decode(b) for b in self._blocks(z, self.block // self.cfg.hop)], -1)
         else:
             y = self.model.decode(z)
+        if self.resampler is not None:
+            y = self.resampler.from_model_sampling_rate(y)
         if self.stereo:
             y = torch.cat(y.chunk(2, 0), 1)
         return y
@@ -209,6 +239,8 @@ class NNTildeRAVE:
         for s in (self._enc_stream, self._dec_stream):
             if s is not None:
                 s.reset()
+        if self.resampler is not None:
+            self.resampler.reset()
 
 
 # The TorchScript (nn~ .ts) export lives in rave_amd/scripted.py (no postponed

@@ -118,6 +118,27 @@ class RAVE:
                        for k, c, ms in tuning)
         N.check(N.lib.rave_model_tuning_set(self.handle, text.encode()), "tuning_set")
 
+    # ------------------------------------------------------------ speaker
+    def set_speaker(self, embedding) -> None:
+        """Replace the constant speaker embedding that encode / decode_codes
+        concatenate (rave/model.py:617-618; the nn~ `speaker` choice among
+        embeddings, scripts/export.py:384-396).  ``embedding``: speaker_size
+        values, numpy or a torch tensor (e.g. ``SpeakerRAVE.embed`` output on
+        this device).  Ordered on the current stream before later calls."""
+        if isinstance(embedding, torch.Tensor):
+            src = embedding.detach().to(self.device, torch.float32).contiguous().reshape(-1)
+            if src.numel() != self.cfg.speaker_size:
+                raise ValueError(f"speaker embedding must have {self.cfg.speaker_size} values")
+            N.check(N.lib.rave_model_set_speaker(self.handle, src.data_ptr(), _stream(self.device)), "set_speaker")
+            self._spk_keep = src          # the copy is asynchronous
+            return
+        spk = np.ascontiguousarray(np.asarray(embedding, np.float32).reshape(-1))
+        if spk.size != self.cfg.speaker_size:
+            raise ValueError(f"speaker embedding must have {self.cfg.speaker_size} values")
+        src = torch.from_numpy(spk).to(self.device)
+        N.check(N.lib.rave_model_set_speaker(self.handle, src.data_ptr(), _stream(self.device)), "set_speaker")
+        self._spk_keep = src
+
     # ------------------------------------------------------------ AdaIN rows
     @property
     def adain_row0(self) -> int:

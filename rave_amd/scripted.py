@@ -61,9 +61,21 @@ class ScriptedRAVE(torch.nn.Module):
     streaming: bool
     hop: int
     latent_size: int
+    active_speaker: int
+    use_resampler: bool
+    rs_ratio: int
+    rs_down_pad: List[int]
+    rs_up_pad: List[int]
 
     def __init__(self, cfg, params, speaker, hk=None, precision: str = "f32", stereo: bool = False,
-                 streaming: Optional[bool] = None, block: int = 2048):
+                 streaming: Optional[bool] = None, block: int = 2048, speakers=None,
+                 target_sr: Optional[int] = None, sampling_rate: int = 48000):
+        """``speakers``: the embeddings the nn~ ``speaker`` attribute selects
+        (speaker1..4 of scripts/export.py:84-93, e.g. SpeakerRAVE.embed outputs);
+        index ``i`` picks ``speakers[i]``, any other index ``speaker5`` (the
+        recorded target, ones until set, :96).  Default: ``[speaker]``.
+        ``target_sr``: host rate; != sampling_rate adds the Resampler around
+        the model (:101-106, 159-160, 331-332)."""
         super().__init__()
         import numpy as np
         from . import _native as N
@@ -88,6 +100,32 @@ class ScriptedRAVE(torch.nn.Module):
                                                     prec, int(block))
         self.hop = int(cfg.hop)
         self.latent_size = int(cfg.latent_size + cfg.speaker_size)
+        spks = [speaker] if speakers is None else list(speakers)
+        self.register_buffer("speakers", torch.from_numpy(
+            np.stack([np.asarray(e, np.float32).reshape(-1) for e in spks])) if spks else
+            torch.zeros(0, int(cfg.speaker_size)))
+        self.register_buffer("speaker5", torch.ones(int(cfg.speaker_size)))
+        self.active_speaker = -1 if speakers is not None else 0
+        # Resampler (rave/resampler.py) on torch.ops.rave_amd.fir
+        self.use_resampler = target_sr is not None and int(target_sr) != int(sampling_rate)
+        self.rs_ratio = 1
+        self.rs_down_pad, self.rs_up_pad = [0, 0, 0], [0, 0, 0]
+        self.register_buffer("rs_down_h", torch.zeros(1, 1))
+        self.register_buffer("rs_up_h", torch.zeros(1, 1))
+        self.register_buffer("rs_down_hist", torch.zeros(0, 0))
+        self.register_buffer("rs_up_hist", torch.zeros(0, 0))
+        if self.use_resampler:
+            from . import resampler as R
+            from .config import get_padding
+            ratio, down, up = R.design(int(target_sr), int(sampling_rate))
+            if self.streaming and ratio % 2:
+                raise ValueError(f"When using streaming mode, resampling ratio must be a power of 2, got {ratio}")
+            self.rs_ratio = ratio
+            self.rs_down_h, self.rs_up_h = torch.from_numpy(down), torch.from_numpy(up)
+            for pads, k, st in ((self.rs_down_pad, down.shape[1], ratio), (self.rs_up_pad, up.shape[1], 1)):
+                l, r = get_padding(k, st, causal=cfg.causal)
+                pads[0], pads[1], pads[2] = l, r, (st - r % st) % st     # + CachedConv1d's stride_delay
+        io_ratio = self.hop * self.rs_ratio
         self.learn_target, self.reset_target = (False,), (False,)
         self.learn_source, self.reset_source = (False,), (False,)
         self.speaker, self.record = (0,), (False,)
@@ -97,8 +135,8 @@ class ScriptedRAVE(torch.nn.Module):
         latents = [f"(signal) Latent dimension {i}" for i in range(self.latent_size)]
         n_out = 2 if stereo else 1
         self._methods: List[str] = []
-        self.register_method("encode", 1, 1, self.latent_size, self.hop, audio_in, latents)
-        self.register_method("decode", self.latent_size, self.hop, n_out, 1, latents, audio_out)
+        self.register_method("encode", 1, 1, self.latent_size, io_ratio, audio_in, latents)
+        self.register_method("decode", self.latent_size, io_ratio, n_out, 1, latents, audio_out)
         self.register_method("forward", 1, 1, n_out, 1, audio_in, audio_out)
         self._attributes: List[str] = ["learn_target", "reset_target", "learn_source", "reset_source",
                                        "speaker", "record"]
@@ -201,10 +239,43 @@ class ScriptedRAVE(torch.nn.Module):
             raise ValueError("streaming buffers must be a multiple of the block")
         return [t[..., i:i + per_block] for i in range(0, T, per_block)]
 
+    def _select_speaker(self) -> None:
+        """scripts/export.py:384-396: the `speaker` attribute picks the embedding."""
+        idx = self.speaker[0]
+        if idx != self.active_speaker:
+            if idx >= 0 and idx < self.speakers.shape[0]:
+                self.engine.set_speaker(self.speakers[idx])
+            else:
+                self.engine.set_speaker(self.speaker5)
+            self.active_speaker = idx
+
+    def _fir(self, x: torch.Tensor, down: bool) -> torch.Tensor:
+        """One Resampler conv on (B, 1, T); cached (streaming) or zero-padded."""
+        h = self.rs_down_h if down else self.rs_up_h
+        pads = self.rs_down_pad if down else self.rs_up_pad
+        stride = self.rs_ratio if down else 1
+        xs = x[:, 0, :].contiguous()
+        if self.streaming:
+            H = pads[0] + pads[1] + pads[2]
+            hist = self.rs_down_hist if down else self.rs_up_hist
+            if hist.shape[0] != xs.shape[0] or hist.shape[1] != H or hist.device != xs.device:
+                hist = torch.zeros(xs.shape[0], H, device=xs.device)
+                if down:
+                    self.rs_down_hist = hist
+                else:
+                    self.rs_up_hist = hist
+            y = torch.ops.rave_amd.fir(xs, h, stride, pads[0], pads[1], hist)
+        else:
+            y = torch.ops.rave_amd.fir(xs, h, stride, pads[0], pads[1], None)
+        return y.unsqueeze(1)
+
     @torch.jit.export
     def encode(self, x: torch.Tensor) -> torch.Tensor:
         if self.is_using_adain:
             self.update_adain()
+        self._select_speaker()
+        if self.use_resampler:
+            x = self._fir(x, True)                         # to_model_sampling_rate
         if self.streaming:
             return torch.cat([self.engine.stream_encode(b) for b in self._blocks(x, self.engine.block())], -1)
         return self.engine.encode(x)
@@ -219,6 +290,8 @@ class ScriptedRAVE(torch.nn.Module):
             y = torch.cat([self.engine.stream_decode(b) for b in self._blocks(z, self.engine.block() // self.hop)], -1)
         else:
             y = self.engine.decode(z)
+        if self.use_resampler:
+            y = self._fir(y, False)                        # from_model_sampling_rate
         if self.stereo:
             y = torch.cat(y.chunk(2, 0), 1)
         return y

@@ -90,7 +90,7 @@ def install_shims():
     pkg.__path__ = [os.path.join(REF, "rave")]
     sys.modules["rave"] = pkg
     mods = {}
-    for name in ("pqmf", "core", "blocks", "quantization"):
+    for name in ("pqmf", "core", "blocks", "quantization", "CombinedRave", "resampler"):
         mods[name] = importlib.import_module(f"rave.{name}")
     return mods
 
@@ -432,6 +432,87 @@ def gen_adain(mods, cfg, out, fname="v3_adain.npz", batch=2, t=8192, seed=0):
     return res
 
 
+def gen_speaker(mods, out, seed=0):
+    """SpeakerRAVE (rave/CombinedRave.py:200-328) in eval mode on the 16 PQMF
+    bands of two synthetic clips (the reference's embedding call,
+    scripts/export.py:84-90), centred and causal padding; seeded parameters
+    (rave_amd.speaker.init_params) loaded under the module's own names."""
+    import cached_conv as cc
+    from rave_amd.speaker import init_params as speaker_params
+    params = speaker_params(seed)
+    res = {"seed": np.int64(seed)}
+    for mode in ("centered", "causal"):
+        cc.use_cached_conv(False)
+        cc.set_padding_mode(mode)
+        m = mods["CombinedRave"].SpeakerRAVE()
+        sd = {k: torch.from_numpy(v) for k, v in params.items()}
+        missing, unexpected = m.load_state_dict(sd, strict=False)
+        assert not unexpected, unexpected
+        assert all(k.startswith("bn6.") or k.endswith("num_batches_tracked") for k in missing), missing
+        m.eval()
+        pq = mods["pqmf"].CachedPQMF(attenuation=100, n_band=16)
+        x = torch.from_numpy(synth_audio(2, 16384, seed0=300))
+        acts = {}
+        hooks = [getattr(m, n).register_forward_hook(
+            lambda mod, i, o, n=n: acts.__setitem__(n, o.detach().numpy().copy()))
+            for n in ("layer2", "layer3", "layer4", "cat_layer", "out_layer")]
+        with torch.no_grad():
+            bands = pq(x)
+            emb = m(bands)
+        for h in hooks:
+            h.remove()
+        res[f"{mode}/x"] = x.numpy()
+        res[f"{mode}/bands"] = bands.numpy()
+        res[f"{mode}/emb"] = emb.numpy()
+        for n, v in acts.items():
+            res[f"{mode}/{n}"] = v
+    cc.set_padding_mode("centered")
+    np.savez_compressed(os.path.join(out, "speaker.npz"), **res)
+    return res
+
+
+def gen_resampler(mods, out):
+    """Resampler (rave/resampler.py:9-66): its two filters, offline
+    to/from_model_sampling_rate for ratios 2, 3 (centred) and 2 (causal), and
+    the cached (streaming) form for ratio 2 over 2048-sample blocks.  These are
+    the ratios the reference can build: for 4..8 the polyphase split of
+    rave/resampler.py:41-44 pads len(h) % ratio taps and the reshape fails
+    (rave_amd.resampler.design raises for them too), and streaming rejects odd
+    ratios (:21-25)."""
+    import cached_conv as cc
+    res = {}
+    rng = np.random.Generator(np.random.PCG64(400))
+    x = torch.from_numpy(rng.standard_normal((2, 1, 4096)).astype(np.float32))
+    for ratio, mode in ((2, "centered"), (3, "centered"), (2, "causal")):
+        cc.use_cached_conv(False)
+        cc.set_padding_mode(mode)
+        r = mods["resampler"].Resampler(48000 * ratio, 48000)
+        key = f"r{ratio}_{mode}"
+        with torch.no_grad():
+            res[f"{key}/down_w"] = r.downsample.weight.numpy().copy()
+            res[f"{key}/up_w"] = r.upsample.weight.numpy().copy()
+            res[f"{key}/down"] = r.to_model_sampling_rate(x).numpy()
+            res[f"{key}/up"] = r.from_model_sampling_rate(x).numpy()
+    res["x"] = x.numpy()
+    n_blocks, block = 6, 2048
+    xs = torch.from_numpy(rng.standard_normal((1, 1, n_blocks * block)).astype(np.float32))
+    res["stream/x"] = xs.numpy()
+    for ratio in (2,):
+        for mode in ("centered", "causal"):
+            cc.use_cached_conv(True)
+            cc.set_padding_mode(mode)
+            r = mods["resampler"].Resampler(48000 * ratio, 48000)
+            with torch.no_grad():
+                down = [r.to_model_sampling_rate(xs[..., i * block:(i + 1) * block]) for i in range(n_blocks)]
+                up = [r.from_model_sampling_rate(xs[..., i * block:(i + 1) * block]) for i in range(n_blocks)]
+            res[f"stream/r{ratio}_{mode}/down"] = torch.cat(down, -1).numpy()
+            res[f"stream/r{ratio}_{mode}/up"] = torch.cat(up, -1).numpy()
+    cc.use_cached_conv(False)
+    cc.set_padding_mode("centered")
+    np.savez_compressed(os.path.join(out, "resampler.npz"), **res)
+    return res
+
+
 def check_residual_semantics(mods):
     """The reference's tests/test_residual.py logic (streaming == one-shot,
     delay-shifted) run against the cached_conv restatement."""
@@ -480,6 +561,10 @@ def main():
     if a.only == "stream_v3":
         gen_stream_v3(mods, rcfg.v3_noise(causal=True, capacity=16), a.out)
         return
+    if a.only == "speaker":
+        gen_speaker(mods, a.out)
+        gen_resampler(mods, a.out)
+        return
     if a.only == "adain":
         gen_adain(mods, rcfg.v3(), a.out)
         gen_adain(mods, rcfg.v3(capacity=8), a.out, fname="v3_adain_small.npz", t=4096)
@@ -504,6 +589,8 @@ def main():
     gen_adain(mods, rcfg.v3(), a.out)
     gen_adain(mods, rcfg.v3(capacity=8), a.out, fname="v3_adain_small.npz", t=4096)
     gen_stream_v3(mods, rcfg.v3_noise(causal=True, capacity=16), a.out)
+    gen_speaker(mods, a.out)
+    gen_resampler(mods, a.out)
 
     files = sorted(f for f in os.listdir(a.out) if f.endswith(".npz"))
     manifest["files"] = {f: hashlib.sha256(open(os.path.join(a.out, f), "rb").read()).hexdigest()[:16]

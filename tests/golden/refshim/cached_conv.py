@@ -26,14 +26,16 @@ import torch.nn as nn
 
 MAX_BATCH_SIZE = 64
 _USE_CACHED = False
+USE_BUFFER_CONV = False       # the package's public flag (read by rave/resampler.py:21)
 _PAD_MODE = "centered"
 _CONVT_BIAS_DEFAULT = False   # v1.gin:34 cc.ConvTranspose1d.bias = False
 _CONV_BIAS_DEFAULT = True     # v1.gin:33 cc.Conv1d.bias = True
 
 
 def use_cached_conv(state: bool):
-    global _USE_CACHED
+    global _USE_CACHED, USE_BUFFER_CONV
     _USE_CACHED = bool(state)
+    USE_BUFFER_CONV = _USE_CACHED
 
 
 def set_padding_mode(mode: str):

@@ -109,3 +109,15 @@ def test_torch_library_registers_engine():
     assert len(config_ints(rcfg.v2())) == 108
     with pytest.raises((ValueError, RuntimeError)):
         torch.classes.rave_amd.Engine([1, 2, 3], 0.2, [], [], torch.zeros(256), 0, 2048)
+
+
+def test_resampler_changes_method_ratios():
+    """export.py:101-106: with a target rate the registered ratios include the
+    resampling factor (x_len // z.shape[-1] is measured at the host rate)."""
+    w = NNTildeRAVE(_Cfg(rcfg.v2()), target_sr=96000)
+    assert w.sr == 96000 and w.resampler.ratio == 2
+    assert w.get_method_params("encode") == [1, 1, 320, 2048]
+    assert w.get_method_params("decode") == [320, 2048, 1, 1]
+    assert NNTildeRAVE(_Cfg(rcfg.v2()), target_sr=48000).resampler is None
+    with pytest.raises(ValueError):
+        NNTildeRAVE(_Cfg(rcfg.causal()), target_sr=144000)   # odd ratio while streaming
