@@ -386,6 +386,12 @@ typedef struct rave_reloc {
 typedef struct rave_plan rave_plan;
 int rave_plan_create(const rave_plan_op* ops, int n_ops, const rave_reloc* relocs, int n_relocs,
                      rave_plan** out);
+/* Threading: rave_plan_run relocates into a per-call, per-host-thread copy and
+ * never writes the plan, so several threads may replay one plan at once on
+ * their own streams PROVIDED each call binds its own activation / workspace
+ * slots (the split-K ticket counters live in the workspace slot).  Profiling
+ * (rave_plan_profile / rave_plan_op_times) keeps per-plan event state and is
+ * single-threaded.  Errors are per thread (rave_last_error). */
 int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, void* stream);
 int rave_plan_destroy(rave_plan* plan);
 int rave_plan_size(const rave_plan* plan);

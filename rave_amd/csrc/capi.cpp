@@ -19,7 +19,6 @@ thread_local OpEvents g_op_events;
 struct rave_plan {
     std::vector<rave_plan_op> ops;
     std::vector<rave_reloc> relocs;
-    std::vector<rave_plan_op> scratch;   // relocated copy used by run()
     std::vector<hipEvent_t> ev;          // 2 per op per armed run when profiling
     int runs_cap = 0;                    // armed runs
     int runs = 0;                        // runs recorded since the last op_times
@@ -67,7 +66,6 @@ extern "C" int rave_plan_create(const rave_plan_op* ops, int n_ops, const rave_r
     rave_plan* p = new rave_plan;
     p->ops.assign(ops, ops + n_ops);
     p->relocs.assign(relocs, relocs + n_relocs);
-    p->scratch = p->ops;
     *out = p;
     return RAVE_OK;
 }
@@ -137,7 +135,6 @@ int plan_patch(rave_plan* plan, int op, int offset, const void* data, int n) {
         return RAVE_ERR_ARG;
     }
     std::memcpy(plan->ops[op].u.raw + offset, data, (size_t)n);
-    std::memcpy(plan->scratch[op].u.raw + offset, data, (size_t)n);
     return RAVE_OK;
 }
 }  // namespace rave
@@ -147,18 +144,23 @@ extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, v
         rave::set_error("plan_run: null plan");
         return RAVE_ERR_STATE;
     }
+    // The relocated op list is per call and per host thread (the plan itself is
+    // read-only here), so threads may run one plan concurrently on their own
+    // streams as long as the plan's workspace slots differ per call.
+    static thread_local std::vector<rave_plan_op> scratch;
+    scratch.assign(plan->ops.begin(), plan->ops.end());
     for (const rave_reloc& r : plan->relocs) {
         if (r.slot >= n_slots || !slots || !slots[r.slot]) {
             rave::set_error("plan_run: slot " + std::to_string(r.slot) + " not bound");
             return RAVE_ERR_ARG;
         }
         char* base = static_cast<char*>(slots[r.slot]) + r.byte_offset;
-        std::memcpy(plan->scratch[r.op].u.raw + r.field_offset, &base, sizeof(void*));
+        std::memcpy(scratch[r.op].u.raw + r.field_offset, &base, sizeof(void*));
     }
     const bool prof = plan->runs < plan->runs_cap;   // armed and not yet full
-    hipEvent_t* ev = prof ? plan->ev.data() + (size_t)2 * plan->scratch.size() * plan->runs : nullptr;
-    for (size_t i = 0; i < plan->scratch.size(); ++i) {
-        const rave_plan_op& op = plan->scratch[i];
+    hipEvent_t* ev = prof ? plan->ev.data() + (size_t)2 * scratch.size() * plan->runs : nullptr;
+    for (size_t i = 0; i < scratch.size(); ++i) {
+        const rave_plan_op& op = scratch[i];
         int rc;
         if (prof) rave::g_op_events = {ev[2 * i], ev[2 * i + 1]};
         switch (op.kind) {
@@ -173,9 +175,9 @@ extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, v
                 // one launch, timed on the first op; the rest record empty intervals
                 const rave_shift_args* batch[rave::kShiftBatch];
                 int n = 0;
-                while (n < rave::kShiftBatch && i + n < plan->scratch.size() &&
-                       plan->scratch[i + n].kind == RAVE_OP_SHIFT_HISTORY) {
-                    batch[n] = &plan->scratch[i + n].u.shift;
+                while (n < rave::kShiftBatch && i + n < scratch.size() &&
+                       scratch[i + n].kind == RAVE_OP_SHIFT_HISTORY) {
+                    batch[n] = &scratch[i + n].u.shift;
                     ++n;
                 }
                 rc = rave::shift_history_batch(batch, n, static_cast<hipStream_t>(stream));
