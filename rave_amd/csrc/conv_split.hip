@@ -133,15 +133,25 @@ __device__ __forceinline__ u32x4_t raw_rsrc(const void* p, int bytes) {
 
 // Workgroup tile: BN time columns x BM GEMM rows.  A wave owns WM rows x WN
 // columns (WM = 32: 128 columns; WM = 64: 64 columns), four 32x32 blocks.
-// KG = 2: two waves per output tile ("K-groups"), each taking part of every
-// chunk's K-steps (group 0 the first ceil(KSC/2)); summed through LDS at the end.
-template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 4096 / WM> struct SGeo {
+// KG = 2 or 4: KG waves per output tile ("K-groups"), each taking a contiguous
+// share of every chunk's K-steps (group g: ks_of(g) steps from st_of(g));
+// summed through LDS at the end in group order.
+// VCX: one staged chunk is VCX packed weight chunks ("sub-chunks") of the
+// family's VC virtual channels -- more K-steps per barrier and per window DMA
+// round, and enough of them for four K-groups on the short-N layers (C >= 512
+// at 64-128 frames), which would otherwise need split-K slabs in HBM.
+template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 4096 / WM, int VCX = 1>
+struct SGeo {
     using F = SFam<KT>;
-    static constexpr int Q = F::Q, S = F::S, VC = F::VC;
-    static constexpr int KSC = Q * VC / 16, CPC = VC / S;
+    static constexpr int Q = F::Q, S = F::S, VC0 = F::VC, VC = VC0 * VCX;
+    static constexpr int KSC0 = Q * VC0 / 16;                // K-steps per packed weight chunk
+    static constexpr int HPS0 = VC0 / 16;                    // K-steps per tap within a packed chunk
+    static constexpr int KSC = KSC0 * VCX, CPC = VC / S;     // per staged chunk
     static constexpr int WN = WN_, NJ = WM / 32, NI = WN / 32;
     static constexpr int WGM = BM / WM, WGN = BN / WN, NWT = WGM * WGN, NW = NWT * KG, NT = 64 * NW;
-    static constexpr int KS0 = (KSC + KG - 1) / KG, KS1 = KSC - KS0;   // K-steps of group 0 / 1
+    static constexpr int ks_of(int g) { return KSC / KG + (g < KSC % KG ? 1 : 0); }
+    static constexpr int st_of(int g) { return g * (KSC / KG) + (g < KSC % KG ? g : KSC % KG); }
+    static constexpr int KS0 = ks_of(0);                     // most K-steps of any group
     // window rows: columns + tap reach (+1: ConvT phase group 1 reads one row later)
     static constexpr int XW_MAX = BN + (Q - 1) * F::DMAX + (KT == 2 ? 1 : 0);
     static constexpr int PH = VC + 8;                        // halves per plane row (conflict-free b128)
@@ -169,23 +179,23 @@ template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;   // convert tasks per thread
     static_assert(XPLANE % 16 == 0 && STAGE % 16 == 0, "16-byte LDS alignment");
     static_assert((NI * NJ == 4 || NI * NJ == 2) && NW >= 1 && NW <= 16, "tile");
-    static_assert(KG == 1 || (KG == 2 && KS1 >= 1), "K-groups");
+    static_assert(KG == 1 || KG == 2 || KG == 4, "K-groups");
     // a configuration is built only if its hand-counted waits fit the vmcnt
-    // field and its LDS fits the CU
-    static constexpr bool VALID = 2 * WR + 2 * XI <= 63 && LDS_ALL <= 160 * 1024;
+    // field, its LDS fits the CU and every K-group has a K-step
+    static constexpr bool VALID = 2 * WR + 2 * XI <= 63 && LDS_ALL <= 160 * 1024 && ks_of(KG - 1) >= 1;
 };
 
 template <int V> struct IC {
     static constexpr int value = V;
 };
 
-template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_>
+template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split_kernel(ConvKArgs a) {
-    using G = SGeo<KT, BM, BN, WM, XV, KG, WN_>;
-    constexpr int S = G::S, VC = G::VC, KSC = G::KSC, CPC = G::CPC, PH = G::PH;
+    using G = SGeo<KT, BM, BN, WM, XV, KG, WN_, VCX>;
+    constexpr int S = G::S, CPC = G::CPC, PH = G::PH;
     constexpr int NT = G::NT, NW = G::NW, NWT = G::NWT, WGM = G::WGM, G8 = G::G8, XT = G::XT;
     constexpr int NI = G::NI, NJ = G::NJ, WN = G::WN;
-    constexpr int HPS = VC / 16;                 // K-steps per tap
+    constexpr int KSC0 = G::KSC0, HPS0 = G::HPS0, VC0 = G::VC0;
     constexpr unsigned kOOB = 0xFFFFFFF0u;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -241,8 +251,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
     const u32x4_t xrs = raw_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);
     const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
     const u32x4_t wrs = raw_rsrc(a.w, a.w_bytes);
-    const unsigned wcstride = (unsigned)(a.MB * KSC * 2) * 1024u;
-    const unsigned wbase = (unsigned)((mw / 32) * KSC * 2) * 1024u + (unsigned)lane * 16u;
+    // packed weights: [packed chunk][32-row block][KSC0 K-steps][hi|lo][64 lanes][8 halves]
+    const unsigned wcstride = (unsigned)(a.MB * KSC0 * 2) * 1024u;
+    const unsigned wbase = (unsigned)((mw / 32) * KSC0 * 2) * 1024u + (unsigned)lane * 16u;
     const uint32_t lds0 = lds_addr(smem);
     char* planes = smem + G::NS * G::STAGE;
     float* alpha_s = reinterpret_cast<float*>(smem + G::NS * G::STAGE + 4 * G::XPLANE);
@@ -295,13 +306,15 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
     // the packed image read zeros)
     // (slot = this group's local K-step; st = the chunk's K-step)
     u32x4_t wr[G::KS0][NJ][2];
+    // (staged chunk c, K-step st = sub-chunk u, packed K-step s0)
     auto load_w = [&](int c, int slot, int st) __attribute__((always_inline)) {
+        const int u = st / KSC0, s0 = st - u * KSC0;
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int pl = 0; pl < 2; ++pl)
-                wr[slot][j][pl] = bload16(wrs, wbase + (unsigned)c * wcstride +
-                                                   (unsigned)(((j * KSC + st) * 2 + pl) * 1024));
+                wr[slot][j][pl] = bload16(wrs, wbase + (unsigned)(c * VCX + u) * wcstride +
+                                                   (unsigned)(((j * KSC0 + s0) * 2 + pl) * 1024));
     };
     // raw window of a stage -> activation -> (hi, lo) f16 planes
     auto convert_task = [&](int c, int stage, int pb, int i) __attribute__((always_inline)) {
@@ -348,7 +361,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
         s_h8 h[NI], l[NI];
     };
     auto read_a = [&](int pb, int st, AFrag& f) __attribute__((always_inline)) {
-        const int q = st / HPS, hv = st - q * HPS;
+        const int u = st / KSC0, s0 = st - u * KSC0;
+        const int q = s0 / HPS0, hv = u * (VC0 / 16) + (s0 - q * HPS0);   // 16-channel column group
         const _Float16* xh = reinterpret_cast<const _Float16*>(planes + pb * 2 * G::XPLANE);
         const _Float16* xl = reinterpret_cast<const _Float16*>(planes + pb * 2 * G::XPLANE + G::XPLANE);
 #pragma unroll
@@ -365,8 +379,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
     // both groups pass the same barriers.
     auto body = [&](auto gtag) __attribute__((always_inline)) {
         constexpr int GG = decltype(gtag)::value;
-        constexpr int KS = GG == 0 ? G::KS0 : G::KS1;   // own K-steps per chunk
-        constexpr int ST0 = GG == 0 ? 0 : G::KS0;       // first own K-step
+        constexpr int KS = G::ks_of(GG);                // own K-steps per chunk
+        constexpr int ST0 = G::st_of(GG);               // first own K-step
         constexpr int WR = KS * NJ * 2, XI = G::XI;
         issue(c_begin, 0);
         issue(c_begin + 1, 1);
@@ -436,17 +450,24 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
             if (c == c_begin) stamp(2);
         }
     };
-    if (KG == 1 || kg == 0) body(IC<0>{});
-    else body(IC<1>{});
+    if (kg == 0) body(IC<0>{});
+    else if constexpr (KG >= 2) {
+        if (kg == 1) body(IC<1>{});
+        else if constexpr (KG == 4) {
+            if (kg == 2) body(IC<2>{});
+            else body(IC<3>{});
+        }
+    }
     stamp(3);
     wait_vm<0>();                           // drain the ring before the epilogue's own loads
-    if constexpr (KG == 2) {
-        // group 1 hands its partial tile to group 0 through LDS (ring and planes
-        // are dead); group 0 adds it in a fixed order.  Group 1 then runs the
-        // epilogue's barriers with its stores muted ("live" below).
+    if constexpr (KG >= 2) {
+        // groups 1.. hand their partial tiles to group 0 through LDS (ring and
+        // planes are dead); group 0 adds them in group order (fixed: bitwise
+        // reproducible).  The others then run the epilogue's barriers with their
+        // stores muted ("live" below).
         __syncthreads();
         float* red = reinterpret_cast<float*>(smem) + (size_t)wave * WM * G::EROW;
-        if (kg == 1) {
+        if (kg != 0) {
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -456,13 +477,16 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
         }
         __syncthreads();
         if (kg == 0) {
-            const float* o = reinterpret_cast<const float*>(smem) + (size_t)(wave + NWT) * WM * G::EROW;
 #pragma unroll
-            for (int i = 0; i < NI; ++i)
+            for (int g = 1; g < KG; ++g) {
+                const float* o = reinterpret_cast<const float*>(smem) + (size_t)(wave + g * NWT) * WM * G::EROW;
 #pragma unroll
-                for (int j = 0; j < NJ; ++j)
+                for (int i = 0; i < NI; ++i)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[i][j][r] += o[((i * NJ + j) * 16 + r) * 64 + lane];
+                    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) acc[i][j][r] += o[((i * NJ + j) * 16 + r) * 64 + lane];
+            }
         }
         __syncthreads();                    // partner areas read before the epilogue reuses LDS
     }
@@ -688,32 +712,42 @@ struct SplitCfg {
     int tile, S, sep;     // kSplitTiles index, K-splits, separate reduce launch
 };
 
-// Tiles (BM rows x BN columns, wave WM x WN, KG waves per output tile).  The
-// table index is part of the launch-configuration code, so retired shapes keep
-// their slot: only the rows marked built are instantiated (the 32 x 64 wave
-// tiles are what the autotuner picks on every RAVE layer, profiles/r01_final/
-// tuning.json; the retired 64-row / 128-column wave tiles never won).
+// Tiles (BM rows x BN columns, wave WM x WN, KG waves per output tile, VCX
+// packed chunks per staged chunk).  The table index is part of the
+// launch-configuration code.  Slots 10-15 are round 1's 32 x 64 wave tiles
+// (what the autotuner picks on every RAVE layer, profiles/r01_final/
+// tuning.json); slots 0-7 (round 1's retired 64-row / 128-column wave tiles,
+// which never won) now hold the wide-chunk tiles for the short-N layers:
+// two or four K-groups on 2- or 4-chunk windows (slots 4 and 6 measured no
+// better than these on any v2 layer and are not built).  Only the rows marked
+// built are instantiated.  Split-K counts of wide-chunk tiles are in staged chunks.
 constexpr int kNumSplitTiles = 16;
-[[maybe_unused]] constexpr int kSplitTiles[kNumSplitTiles][5] = {   // BM, BN, WM, KG, WN
-    {128, 128, 32, 1, 128}, {64, 256, 32, 1, 128}, {64, 128, 32, 1, 128}, {256, 64, 64, 1, 64},
-    {128, 64, 64, 1, 64},   {64, 64, 64, 1, 64},   {128, 64, 64, 2, 64},  {64, 128, 32, 2, 128},
-    {128, 128, 32, 2, 128}, {256, 64, 64, 2, 64},  {128, 64, 32, 1, 64},  {64, 128, 32, 1, 64},
-    {256, 64, 32, 1, 64},   {256, 64, 32, 2, 64},  {128, 64, 32, 2, 64},  {64, 128, 32, 2, 64}};
-[[maybe_unused]] constexpr bool kSplitTileBuilt[kNumSplitTiles] = {false, false, false, false, false, false, false, false,
+[[maybe_unused]] constexpr int kSplitTiles[kNumSplitTiles][6] = {   // BM, BN, WM, KG, WN, VCX
+    {64, 64, 32, 4, 64, 2},   {64, 64, 32, 4, 64, 4},   {128, 64, 32, 2, 64, 2},  {32, 64, 32, 4, 64, 2},
+    {128, 64, 32, 4, 64, 2},  {64, 128, 32, 2, 64, 2},  {32, 64, 32, 4, 64, 4},   {64, 64, 32, 2, 64, 2},
+    {128, 128, 32, 2, 128, 1}, {256, 64, 64, 2, 64, 1}, {128, 64, 32, 1, 64, 1},  {64, 128, 32, 1, 64, 1},
+    {256, 64, 32, 1, 64, 1},  {256, 64, 32, 2, 64, 1},  {128, 64, 32, 2, 64, 1},  {64, 128, 32, 2, 64, 1}};
+[[maybe_unused]] constexpr bool kSplitTileBuilt[kNumSplitTiles] = {true,  true,  true,  true,  false, true,  false, true,
                                                   false, false, true,  true,  true,  true,  true,  true};
 [[maybe_unused]] constexpr int kSplitDefaultTile = 10;
 
-// Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>, IC<WN>) for a built tile index ti
-// (compile-time dispatch; callers check kSplitTileBuilt first).
+// Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>, IC<WN>, IC<VCX>) for a built tile
+// index ti (compile-time dispatch; callers check kSplitTileBuilt first).
 template <typename Fn>
 static inline auto with_tile(int ti, Fn&& f) {
     switch (ti) {
-        case 11: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{});
-        case 12: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});
-        case 13: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{});
-        case 14: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{});
-        case 15: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{});
-        default: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{});   // 10
+        case 0: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<2>{});
+        case 1: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<4>{});
+        case 2: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{});
+        case 3: return f(IC<32>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<2>{});
+        case 5: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{});
+        case 7: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{});
+        case 11: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{});
+        case 12: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{});
+        case 13: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{});
+        case 14: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{});
+        case 15: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{});
+        default: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{});   // 10
     }
 }
 
@@ -725,9 +759,9 @@ template <int KT, bool SNAKE, bool XV>
 int split_launch_inst(ConvKArgs k, int tile, hipStream_t st);
 
 #ifdef RAVE_SPLIT_KT
-template <int KT, int BM, int BN, int WM, int KG, int WN, bool SNAKE, bool XV>
+template <int KT, int BM, int BN, int WM, int KG, int WN, int VCX, bool SNAKE, bool XV>
 static int split_launch_xv(ConvKArgs k, hipStream_t st) {
-    using G = SGeo<KT, BM, BN, WM, XV, KG, WN>;
+    using G = SGeo<KT, BM, BN, WM, XV, KG, WN, VCX>;
     if constexpr (!G::VALID) {
         set_error("conv1d(split16): tile exceeds LDS or the vmcnt range");
         return RAVE_ERR_UNSUPPORTED;
@@ -739,7 +773,7 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
         constexpr size_t lds = (size_t)G::LDS_ALL;
         static_assert(lds <= 160 * 1024, "LDS budget");
         dim3 grid(k.gx * k.gy * k.B * k.S);
-        auto kern = conv1d_split_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN>;
+        auto kern = conv1d_split_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN, VCX>;
         if (lds > 64 * 1024) {
             static bool done = false;
             if (!done) {
@@ -755,10 +789,10 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
 
 template <int KT, bool SNAKE, bool XV>
 int split_launch_inst(ConvKArgs k, int tile, hipStream_t st) {
-    return with_tile(tile, [&](auto bm, auto bn, auto wm, auto kg, auto wn) {
+    return with_tile(tile, [&](auto bm, auto bn, auto wm, auto kg, auto wn, auto vcx) {
         constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
-                      KG = decltype(kg)::value, WN = decltype(wn)::value;
-        return split_launch_xv<KT, BM, BN, WM, KG, WN, SNAKE, XV>(k, st);
+                      KG = decltype(kg)::value, WN = decltype(wn)::value, VCX = decltype(vcx)::value;
+        return split_launch_xv<KT, BM, BN, WM, KG, WN, VCX, SNAKE, XV>(k, st);
     });
 }
 template int split_launch_inst<RAVE_SPLIT_KT, (RAVE_SPLIT_SNAKE != 0), (RAVE_SPLIT_XV != 0)>(ConvKArgs, int,
@@ -816,10 +850,10 @@ static inline int tile_waves(int ti) {   // waves per workgroup
 
 template <int KT>
 static bool split_tile_fits(int idx) {   // both DMA variants must fit
-    return with_tile(idx, [](auto bm, auto bn, auto wm, auto kg, auto wn) {
+    return with_tile(idx, [](auto bm, auto bn, auto wm, auto kg, auto wn, auto vcx) {
         constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
-                      KG = decltype(kg)::value, WN = decltype(wn)::value;
-        return SGeo<KT, BM, BN, WM, true, KG, WN>::VALID && SGeo<KT, BM, BN, WM, false, KG, WN>::VALID;
+                      KG = decltype(kg)::value, WN = decltype(wn)::value, VCX = decltype(vcx)::value;
+        return SGeo<KT, BM, BN, WM, true, KG, WN, VCX>::VALID && SGeo<KT, BM, BN, WM, false, KG, WN, VCX>::VALID;
     });
 }
 static bool split_fits(int taps, int idx) {
@@ -910,7 +944,7 @@ static int split_resolve(const rave_conv1d_args& a, const ConvKArgs& k, int taps
     }
     ConfigCode cc;
     RAVE_CHECK_ARG(decode_config(a.config, cc) && split_tile_ok(taps, cc.tile, k.M, k.split_row) &&
-                       split_count_distinct(cc.S, k.nchunks),
+                       split_count_distinct(cc.S, ceil_div(k.nchunks, kSplitTiles[cc.tile][5])),
                    "conv1d(split16): config not valid for these args (see rave_conv1d_configs)");
     c = {cc.tile, cc.S, cc.sep};
     return RAVE_OK;
@@ -931,8 +965,9 @@ int conv1d_split_configs(const rave_conv1d_args& a, int32_t* cfgs, int max_cfgs)
         const int* t = kSplitTiles[ti];
         const int nw = tile_waves(ti);
         const int64_t ntiles = (int64_t)ceil_div(k.M, t[0]) * ceil_div(k.U, t[1]) * k.B;
+        const int nst = ceil_div(k.nchunks, t[5]);   // staged chunks
         for (int S : kSplitCands) {
-            if (!split_count_distinct(S, k.nchunks)) continue;
+            if (!split_count_distinct(S, nst)) continue;
             const int64_t waves = ntiles * nw * S;
             if (S > 1 && (waves > 16384 || ntiles * nw >= 4096)) continue;   // enough waves unsplit
             // in-launch combine: the last split reads S slabs serially -- only for few splits
@@ -963,6 +998,7 @@ int conv1d_split(const rave_conv1d_args& a, void* stream) {
     rc = split_resolve(a, k, taps, c);
     if (rc != RAVE_OK) return rc;
     if (c.S > 1 && a.partial == nullptr) c.S = 1;
+    k.nchunks = ceil_div(k.nchunks, kSplitTiles[c.tile][5]);   // staged chunks (the kernel's unit)
     k.cps = ceil_div(k.nchunks, c.S);
     k.S = ceil_div(k.nchunks, k.cps);
     k.tickets = reinterpret_cast<int*>(a.partial);

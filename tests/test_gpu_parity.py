@@ -68,6 +68,9 @@ CONV_CASES = [
     (8, 16, 4, 2, 1, 0, "snake", False, 2, 256),
     (64, 8, 3, 1, 1, 0, "leaky", False, 2, 8),
     (40, 64, 3, 1, 1, 0, "none", False, 2, 8),
+    # v2's short-N layers at bench size (wide-chunk K-group tiles)
+    (512, 512, 1, 1, 1, 0, "leaky", True, 16, 128),
+    (1024, 128, 3, 1, 1, 0, "leaky", False, 16, 64),
 ]
 
 
@@ -158,7 +161,7 @@ def test_conv_layer(N, dev, case, split, precision):
     assert maxabs(got, ref) <= 2e-5 * max(1.0, np.abs(ref).max())
 
 
-CONFIG_CASES = [CONV_CASES[i] for i in (1, 2, 4, 5, 8, 9, 11, 12, 14)]
+CONFIG_CASES = [CONV_CASES[i] for i in (1, 2, 4, 5, 8, 9, 11, 12, 14)] + CONV_CASES[-2:]
 
 
 @pytest.mark.parametrize("precision", ["f32", "split16"])
