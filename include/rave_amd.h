@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 9
+#define RAVE_ABI_VERSION 10
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 
@@ -159,7 +159,7 @@ int rave_conv1d(const rave_conv1d_args* a, void* stream);
 typedef struct rave_pqmf_analysis_args {
     int32_t n_band, taps, n_out_bands, batch;
     int32_t t_in, pad_left;     /* t_out = t_in / n_band                          */
-    int32_t t_out, _pad0;
+    int32_t t_out, precision;   /* RAVE_PREC_F32 (exact fp32 MFMA) or RAVE_PREC_SPLIT16 */
     const float* x; int64_t x_sb;
     float* y;       int64_t y_sb, y_sc;
     const float* hkf;
@@ -184,6 +184,8 @@ typedef struct rave_pqmf_synthesis_args {
     const float* noise; int64_t n_sb, n_sc;
     float* y;           int64_t y_sb;
     const float* hki;   /* (n_band, n_band, taps) */
+    int32_t precision;  /* RAVE_PREC_F32 (exact fp32 MFMA) or RAVE_PREC_SPLIT16 */
+    int32_t _pad0;
 } rave_pqmf_synthesis_args;
 int rave_pqmf_synthesis(const rave_pqmf_synthesis_args* a, void* stream);
 

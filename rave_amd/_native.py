@@ -36,7 +36,7 @@ OP_NOISE = 9
 OP_ADAIN = 10
 OP_UNIT = 11
 OP_STACK = 12
-ABI_VERSION = 9
+ABI_VERSION = 10
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 
 # GEMM arithmetic of conv / unit ops (include/rave_amd.h RAVE_PREC_*)
@@ -63,7 +63,7 @@ class ConvArgs(C.Structure):
 
 class AnalysisArgs(C.Structure):
     _fields_ = [("n_band", i32), ("taps", i32), ("n_out_bands", i32), ("batch", i32),
-                ("t_in", i32), ("pad_left", i32), ("t_out", i32), ("_pad0", i32),
+                ("t_in", i32), ("pad_left", i32), ("t_out", i32), ("precision", i32),
                 ("x", vp), ("x_sb", i64),
                 ("y", vp), ("y_sb", i64), ("y_sc", i64),
                 ("hkf", vp)]
@@ -75,7 +75,7 @@ class SynthesisArgs(C.Structure):
                 ("x", vp), ("x_sb", i64), ("x_sc", i64),
                 ("noise", vp), ("n_sb", i64), ("n_sc", i64),
                 ("y", vp), ("y_sb", i64),
-                ("hki", vp)]
+                ("hki", vp), ("precision", i32), ("_pad0", i32)]
 
 
 class FillArgs(C.Structure):

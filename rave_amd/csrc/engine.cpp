@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <sstream>
 
 namespace rave {
@@ -406,6 +407,7 @@ struct Model {
     const float* noise_ptr(const float* u, int B, int Fz, hipStream_t st);
     template <typename F>
     double time_native(F&& fn, int reps = 5);
+    int pqmf_prec(const std::string& key, const std::function<int(int, hipStream_t)>& run);
 };
 
 Model::~Model() {
@@ -949,6 +951,26 @@ std::map<std::string, std::pair<View, int>> Model::run_stack(Plan& p, const std:
 }
 
 // ------------------------------------------------------------------ PQMF / misc ops
+// Arithmetic of a PQMF op: exact fp32 in an fp32 model, split-f16 in a split16
+// model, and with RAVE_PREC_AUTO the faster of the two, timed on scratch
+// operands of the op's own shape (`run(precision, stream)` launches it).
+int Model::pqmf_prec(const std::string& key, const std::function<int(int, hipStream_t)>& run) {
+    if (precs.size() == 1) return precs[0];
+    if (!tuned.count(key)) {
+        double best = 1e30;
+        int bp = RAVE_PREC_F32;
+        for (int pr : precs) {
+            const double ms = time_native([&](hipStream_t st) { return run(pr, st); });
+            if (ms >= 0 && ms < best) {
+                best = ms;
+                bp = pr;
+            }
+        }
+        tuned[key] = {bp, best};
+    }
+    return (int)tuned.at(key).first;
+}
+
 void Model::analysis_op(Plan& p, int B, int T, const View& x, const View& y, int n_out, int pad, int t_in) {
     const int F = T / cfg.n_band;
     rave_pqmf_analysis_args a{};
@@ -962,6 +984,19 @@ void Model::analysis_op(Plan& p, int B, int T, const View& x, const View& y, int
     a.x_sb = x.sb;
     a.y_sb = y.sb;
     a.y_sc = y.sc;
+    {
+        rave_pqmf_analysis_args q = a;            // scratch operands, the op's strides
+        const int64_t nx = (int64_t)(B - 1) * x.sb + t_in, ny = (int64_t)(B - 1) * y.sb + (int64_t)n_out * y.sc;
+        float* sc = scratch_buf(nx + ny + 128);
+        q.x = sc;
+        q.y = sc + nx + 64;
+        q.hkf = arena + hkf_off;
+        a.precision = pqmf_prec(key_of({"pqa", std::to_string(B), std::to_string(T), std::to_string(t_in)}),
+                                [&](int pr, hipStream_t st) {
+                                    q.precision = pr;
+                                    return rave_pqmf_analysis(&q, st);
+                                });
+    }
     PlanOp& o = p.add(RAVE_OP_PQMF_ANALYSIS, a, "pqmf_analysis");
     rave_pqmf_analysis_args& A = *reinterpret_cast<rave_pqmf_analysis_args*>(o.op.u.raw);
     View h = arena_view(hkf_off);
@@ -988,6 +1023,23 @@ void Model::synthesis_op(Plan& p, int B, int F, const View& x, const View& y, co
     a.n_sb = noise ? noise->sb : 0;
     a.n_sc = noise ? noise->sc : 0;
     a.y_sb = y.sb;
+    {
+        rave_pqmf_synthesis_args q = a;           // scratch operands (no noise), the op's strides
+        const int xl = x_len > 0 ? x_len : F;
+        const int64_t nx = (int64_t)(B - 1) * x.sb + (int64_t)(2 * cfg.n_band - 1) * x.sc + xl;
+        const int64_t ny = (int64_t)(B - 1) * y.sb + (int64_t)F * cfg.n_band;
+        float* sc = scratch_buf(nx + ny + 128);
+        q.x = sc;
+        q.y = sc + ((nx + 63) / 64 + 1) * 64;     // 16-byte aligned
+        q.noise = nullptr;
+        q.hki = arena + hki_off;
+        a.precision = pqmf_prec(key_of({"pqs", std::to_string(B), std::to_string(F), std::to_string(x_len),
+                                        std::to_string(pad)}),
+                                [&](int pr, hipStream_t st) {
+                                    q.precision = pr;
+                                    return rave_pqmf_synthesis(&q, st);
+                                });
+    }
     PlanOp& o = p.add(RAVE_OP_PQMF_SYNTHESIS, a, "pqmf_synthesis");
     rave_pqmf_synthesis_args& A = *reinterpret_cast<rave_pqmf_synthesis_args*>(o.op.u.raw);
     View h = arena_view(hki_off);

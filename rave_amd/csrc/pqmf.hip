@@ -244,6 +244,250 @@ __global__ __launch_bounds__(64 * kPqWaves) void pqmf_synthesis_kernel(rave_pqmf
     PQ_STAMP(4);
 }
 
+// ------------------------------------------------- split-f16 variants (RAVE_PREC_SPLIT16)
+// The same two GEMMs on v_mfma_f32_16x16x32_f16 with conv_split.hip's
+// arithmetic: every fp32 operand v is an f16 pair hi = f16(v), lo =
+// f16((v - hi) 2^11); acc += (hi_h 2^11) hi_x + hi_h lo_x + lo_h hi_x (the lo*lo
+// term and two roundings ~2^-22 relative); the filter is scaled by one power of
+// two 2^e (max |h 2^e| in [8, 16), computed in-kernel) so its halves stay
+// normal, and the epilogue multiplies by 2^-(e + 11) exactly.
+// A wave owns kPsBlk blocks of 16 frames; a workgroup kPsWaves waves.
+typedef _Float16 ps_h8 __attribute__((ext_vector_type(8)));
+typedef float ps_f32x8 __attribute__((ext_vector_type(8)));
+constexpr int kPsWaves = 4;
+constexpr int kPsBlk = 4;
+constexpr int kPsFrames = kPsWaves * kPsBlk * 16;            // frames per workgroup (256)
+constexpr int kPsK = 17;                                     // 32-deep K-steps (<= 544 taps / K rows)
+constexpr int kPsKP = 552;                                   // halves per filter row: 1104 B = 20 banks mod 64
+
+// power-of-two scale 2^e with max |v 2^e| in [8, 16) over the workgroup's values
+// (wave max via LDS; `red` holds kPsWaves floats)
+__device__ __forceinline__ float ps_scale(float amax, float* red) {
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = amax;
+    __syncthreads();
+    float m = red[0];
+#pragma unroll
+    for (int w = 1; w < kPsWaves; ++w) m = fmaxf(m, red[w]);
+    if (!(m > 0.f)) return 1.f;
+    int e;
+    (void)frexpf(m, &e);                  // m in [2^(e-1), 2^e)
+    return ldexpf(1.f, 4 - e);            // m 2^(4-e) in [8, 16)
+}
+
+__device__ __forceinline__ void ps_split(float v, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)v;
+    lo = (_Float16)((v - (float)hi) * 2048.0f);
+}
+
+// analysis: A = filter rows (band), k = tap j; B = window samples, frame f's
+// K-run j..j+7 = samples 16 f + j .. +7 (flat f16 planes, 8 halves of pad every
+// 128 samples: the 16 frames of a read land on 16 distinct bank quads)
+__host__ __device__ constexpr int ps_xi(int i) { return i + 8 * (i >> 7); }
+template <int NBO>
+__global__ __launch_bounds__(64 * kPsWaves) void pqmf_analysis_split_kernel(rave_pqmf_analysis_args a, int wframes) {
+    extern __shared__ __attribute__((aligned(16))) char ps_smem[];
+    _Float16* fh = reinterpret_cast<_Float16*>(ps_smem);     // [16][kPsKP]
+    _Float16* fl = fh + 16 * kPsKP;
+    _Float16* xh = fl + 16 * kPsKP;                           // [ps_xi(wframes * 16)]
+    const int WS = ps_xi(wframes * 16) + 8;
+    _Float16* xl = xh + WS;
+    float* red = reinterpret_cast<float*>(xl + WS);
+    constexpr int NT = 64 * kPsWaves;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t0 = blockIdx.x * kPsFrames;
+    const int b = blockIdx.y;
+    const float* xb = a.x + (int64_t)b * a.x_sb;
+    // filter: rows < NBO, taps < a.taps (all loads before the first LDS store)
+    constexpr int KW = 32 * kPsK;                             // 544
+    constexpr int HT = (NBO * KW + NT - 1) / NT;
+    float hv[HT];
+    float amax = 0.f;
+#pragma unroll
+    for (int it = 0; it < HT; ++it) {
+        const int i = tid + it * NT;
+        const int k = i / KW, j = i - k * KW;
+        const float v = a.hkf[(int64_t)min(k, NBO - 1) * a.taps + min(j, a.taps - 1)];
+        hv[it] = (i < NBO * KW && j < a.taps) ? v : 0.f;
+        amax = fmaxf(amax, fabsf(hv[it]));
+    }
+    const int s0 = t0 * 16 - a.pad_left;
+    constexpr int XT = ((kPsFrames + 40) * 16 + NT - 1) / NT;
+    float xv[XT];
+#pragma unroll
+    for (int it = 0; it < XT; ++it) {
+        const int i = tid + it * NT;
+        const int t = s0 + i;
+        const float v = xb[min(max(t, 0), a.t_in - 1)];
+        xv[it] = (i < wframes * 16 && t >= 0 && t < a.t_in) ? v : 0.f;
+    }
+    const float sc = ps_scale(amax, red);
+    for (int i = tid; i < (16 - NBO) * kPsKP; i += NT) {
+        fh[NBO * kPsKP + i] = (_Float16)0.f;
+        fl[NBO * kPsKP + i] = (_Float16)0.f;
+    }
+#pragma unroll
+    for (int it = 0; it < HT; ++it) {
+        const int i = tid + it * NT;
+        if (i < NBO * KW) {
+            const int k = i / KW, j = i - k * KW;
+            ps_split(hv[it] * sc, fh[k * kPsKP + j], fl[k * kPsKP + j]);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < XT; ++it) {
+        const int i = tid + it * NT;
+        if (i < wframes * 16) ps_split(xv[it], xh[ps_xi(i)], xl[ps_xi(i)]);
+    }
+    __syncthreads();
+    const int g = lane >> 4, col = lane & 15;
+    const int fb = wave * kPsBlk * 16;
+    pq_f32x4 acc[kPsBlk];
+#pragma unroll
+    for (int q = 0; q < kPsBlk; ++q) acc[q] = pq_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kPsK; ++s) {
+        const int ka = col * kPsKP + 32 * s + 8 * g;
+        const ps_h8 ah = *reinterpret_cast<const ps_h8*>(fh + ka);
+        const ps_h8 al = *reinterpret_cast<const ps_h8*>(fl + ka);
+        const ps_h8 a2 = ah * (_Float16)2048.0f;
+#pragma unroll
+        for (int q = 0; q < kPsBlk; ++q) {
+            const int xi = ps_xi(16 * (fb + 16 * q + col) + 32 * s + 8 * g);
+            const ps_h8 bh = *reinterpret_cast<const ps_h8*>(xh + xi);
+            const ps_h8 bl = *reinterpret_cast<const ps_h8*>(xl + xi);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, bh, acc[q], 0, 0, 0);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc[q], 0, 0, 0);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[q], 0, 0, 0);
+        }
+    }
+    const float unscale = 1.0f / (sc * 2048.0f);              // exact: powers of two
+    float* yb = a.y + (int64_t)b * a.y_sb;
+#pragma unroll
+    for (int q = 0; q < kPsBlk; ++q) {
+        const int t = t0 + fb + q * 16 + col;
+        if (t >= a.t_out) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int k = 4 * g + r;
+            if (k < NBO) {
+                float v = acc[q][r] * unscale;
+                if ((k & 1) && !(t & 1)) v = -v;              // reverse_half
+                yb[(int64_t)k * a.y_sc + t] = v;
+            }
+        }
+    }
+}
+
+// synthesis: A = hki rows m, k = tap * 16 + c (K 528 -> 544); B = the staged
+// input channels-last, row w = frame + tap: a K-run (tap, 8 channels) is one
+// 16-byte read; row stride 24 halves = 12 banks, conflict-free over 16 frames.
+constexpr int kPsXW = kPsFrames + 34;                        // window rows (taps 0..33)
+constexpr int kPsXP = 24;                                    // halves per window row
+__global__ __launch_bounds__(64 * kPsWaves) void pqmf_synthesis_split_kernel(rave_pqmf_synthesis_args a,
+                                                                             unsigned a_xw_magic) {
+    extern __shared__ __attribute__((aligned(16))) char ps_smem[];
+    _Float16* fh = reinterpret_cast<_Float16*>(ps_smem);     // [16][kPsKP]
+    _Float16* fl = fh + 16 * kPsKP;
+    _Float16* xh = fl + 16 * kPsKP;                           // [kPsXW][kPsXP]
+    _Float16* xl = xh + kPsXW * kPsXP;
+    float* red = reinterpret_cast<float*>(xl + kPsXW * kPsXP);
+    constexpr int nb = 16, taps = kSynTaps, kdim = nb * taps;
+    constexpr int NT = 64 * kPsWaves;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n0 = blockIdx.x * kPsFrames;
+    const int b = blockIdx.y;
+    constexpr int KW = 32 * kPsK;                             // 544
+    constexpr int HT = (16 * KW + NT - 1) / NT;
+    float hv[HT];
+    float amax = 0.f;
+#pragma unroll
+    for (int it = 0; it < HT; ++it) {
+        const int i = tid + it * NT;
+        const int m = i / KW, k = i - m * KW;                 // K index = tap*16 + c
+        const int kc = min(k, kdim - 1);
+        const float v = a.hki[(int64_t)min(m, 15) * kdim + (kc & 15) * taps + (kc >> 4)];
+        hv[it] = (i < 16 * KW && k < kdim) ? v : 0.f;
+        amax = fmaxf(amax, fabsf(hv[it]));
+    }
+    const float* xb = a.x + (int64_t)b * a.x_sb;
+    const float* nzb = a.noise ? a.noise + (int64_t)b * a.n_sb : nullptr;
+    const int x_len = a.x_len > 0 ? a.x_len : a.t_in;
+    constexpr int xw = kPsXW;
+    constexpr int XT = (16 * xw + NT - 1) / NT;
+    float xv[XT], av[XT], nv[XT];
+#pragma unroll
+    for (int it = 0; it < XT; ++it) {
+        const int i = tid + it * NT;
+        const int c = (int)__umulhi((unsigned)i, a_xw_magic);
+        const int w = i - c * xw;
+        const int f = n0 - a.pad_left + w;
+        const int cc = min(c, 15), ff = min(max(f, 0), max(x_len - 1, 0));
+        xv[it] = xb[(int64_t)cc * a.x_sc + ff];
+        av[it] = xb[(int64_t)(a.mode == 1 ? cc + 16 : cc) * a.x_sc + ff];
+        nv[it] = nzb ? nzb[(int64_t)cc * a.n_sc + ff] : 0.f;
+    }
+    const float sc = ps_scale(amax, red);
+#pragma unroll
+    for (int it = 0; it < HT; ++it) {
+        const int i = tid + it * NT;
+        if (i < 16 * KW) {
+            const int m = i / KW, k = i - m * KW;
+            ps_split(hv[it] * sc, fh[m * kPsKP + k], fl[m * kPsKP + k]);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < XT; ++it) {
+        const int i = tid + it * NT;
+        const int c = (int)__umulhi((unsigned)i, a_xw_magic);
+        const int w = i - c * xw;
+        const int f = n0 - a.pad_left + w;
+        const bool ok = i < 16 * xw && f >= 0 && f < x_len;
+        float v = ok ? xv[it] : 0.f;
+        if (a.mode != 0) {
+            if (a.mode == 1) v = v * (1.0f / (1.0f + __expf(-av[it])));
+            v = v + (ok ? nv[it] : 0.f);
+            v = tanhf(v);
+        }
+        if ((c & 1) && !((a.frame0 + f) & 1)) v = -v;   // reverse_half
+        if (i < 16 * xw) ps_split(ok ? v : 0.f, xh[w * kPsXP + c], xl[w * kPsXP + c]);
+    }
+    __syncthreads();
+    const int g = lane >> 4, col = lane & 15;
+    const int fb = wave * kPsBlk * 16;
+    pq_f32x4 acc[kPsBlk];
+#pragma unroll
+    for (int q = 0; q < kPsBlk; ++q) acc[q] = pq_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kPsK; ++s) {
+        // k = 32 s + 8 g + e: tap 2 s + (g >> 1), channels 8 (g & 1) + e
+        const int ka = col * kPsKP + 32 * s + 8 * g;
+        const ps_h8 ah = *reinterpret_cast<const ps_h8*>(fh + ka);
+        const ps_h8 al = *reinterpret_cast<const ps_h8*>(fl + ka);
+        const ps_h8 a2 = ah * (_Float16)2048.0f;
+        const int tap = 2 * s + (g >> 1);
+#pragma unroll
+        for (int q = 0; q < kPsBlk; ++q) {
+            const int xi = (fb + 16 * q + col + tap) * kPsXP + 8 * (g & 1);
+            const ps_h8 bh = *reinterpret_cast<const ps_h8*>(xh + xi);
+            const ps_h8 bl = *reinterpret_cast<const ps_h8*>(xl + xi);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, bh, acc[q], 0, 0, 0);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc[q], 0, 0, 0);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[q], 0, 0, 0);
+        }
+    }
+    const float o = 16.f / (sc * 2048.0f);                    // n_band x the exact unscale
+    float* yb = a.y + (int64_t)b * a.y_sb;
+#pragma unroll
+    for (int q = 0; q < kPsBlk; ++q) {
+        const int t = n0 + fb + q * 16 + col;
+        if (t >= a.t_in) continue;
+        const pq_f32x4 v = {o * acc[q][3], o * acc[q][2], o * acc[q][1], o * acc[q][0]};
+        *reinterpret_cast<pq_f32x4*>(yb + (int64_t)t * nb + 12 - 4 * g) = v;
+    }
+}
+
 #ifdef RAVE_STAMPS
 extern "C" int rave_diag_pqmf_stamps(void* p) {
     RAVE_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pq_stamps), &p, sizeof(p)));
@@ -266,6 +510,19 @@ extern "C" int rave_pqmf_analysis(const rave_pqmf_analysis_args* p, void* stream
     if ((a.taps + 3) / 4 != kAnaSteps) {
         set_error("pqmf_analysis: kernel is built for the 513-tap RAVE prototype");
         return RAVE_ERR_UNSUPPORTED;
+    }
+    RAVE_CHECK_ARG(a.precision == RAVE_PREC_F32 || a.precision == RAVE_PREC_SPLIT16,
+                   "pqmf_analysis: precision must be RAVE_PREC_F32 or RAVE_PREC_SPLIT16");
+    if (a.precision == RAVE_PREC_SPLIT16) {
+        const int wframes = kPsFrames + (32 * kPsK + 15) / 16 + 1;
+        const int ws = ps_xi(wframes * 16) + 8;
+        const size_t lds = (size_t)(2 * 16 * kPsKP + 2 * ws) * 2 + kPsWaves * 4;
+        dim3 grid(ceil_div(a.t_out, kPsFrames), a.batch);
+        if (a.n_out_bands == 6)
+            launch(pqmf_analysis_split_kernel<6>, grid, dim3(64 * kPsWaves), lds, as_stream(stream), a, wframes);
+        else
+            launch(pqmf_analysis_split_kernel<16>, grid, dim3(64 * kPsWaves), lds, as_stream(stream), a, wframes);
+        return launch_status("pqmf_analysis_split_kernel");
     }
     const int wframes = kPqFrames + (4 * kAnaSteps + 15) / 16 + 1;
     const size_t lds = (size_t)(16 * kAnaHR + wframes * 17) * sizeof(float);
@@ -290,6 +547,15 @@ extern "C" int rave_pqmf_synthesis(const rave_pqmf_synthesis_args* p, void* stre
     }
     RAVE_CHECK_ARG(reinterpret_cast<uintptr_t>(a.y) % 16 == 0 && a.y_sb % 4 == 0,
                    "pqmf_synthesis: output must be 16-byte aligned");
+    RAVE_CHECK_ARG(a.precision == RAVE_PREC_F32 || a.precision == RAVE_PREC_SPLIT16,
+                   "pqmf_synthesis: precision must be RAVE_PREC_F32 or RAVE_PREC_SPLIT16");
+    if (a.precision == RAVE_PREC_SPLIT16) {
+        const size_t lds = (size_t)(2 * 16 * kPsKP + 2 * kPsXW * kPsXP) * 2 + kPsWaves * 4;
+        dim3 grid(ceil_div(a.t_in, kPsFrames), a.batch);
+        const unsigned xw_magic = (unsigned)((0x100000000ull + kPsXW - 1) / kPsXW);
+        launch(pqmf_synthesis_split_kernel, grid, dim3(64 * kPsWaves), lds, as_stream(stream), a, xw_magic);
+        return launch_status("pqmf_synthesis_split_kernel");
+    }
     const int xw = kSynXW;
     const size_t lds = (size_t)(16 * kSynHR + 16 * kSynXR) * sizeof(float);
     dim3 grid(ceil_div(a.t_in, kPqFrames), a.batch);

@@ -187,10 +187,13 @@ def test_conv_every_config(N, dev, case, precision):
 
 
 # ------------------------------------------------------------------ PQMF
+@pytest.mark.parametrize("precision", ["f32", "split16"])
 @pytest.mark.parametrize("causal", [False, True])
-def test_pqmf_golden(N, dev, golden, causal):
+def test_pqmf_golden(N, dev, golden, causal, precision):
     """rave_pqmf_analysis / rave_pqmf_synthesis (CachedPQMF.forward / inverse)
-    through the C-ABI against the reference's PQMF fixtures, both paddings."""
+    through the C-ABI against the reference's PQMF fixtures, both paddings, in
+    both arithmetics."""
+    prec = N.PRECISION[precision]
     from oracle.rave_oracle import get_padding
     from rave_amd.pqmf import kernels
     g = golden("pqmf")
@@ -204,7 +207,7 @@ def test_pqmf_golden(N, dev, golden, causal):
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     a = N.AnalysisArgs(n_band=16, taps=hkf.shape[-1], n_out_bands=16, batch=B, t_in=T,
                        pad_left=get_padding(hkf.shape[-1], causal=causal)[0], t_out=F, x=x.data_ptr(), x_sb=T,
-                       y=y.data_ptr(), y_sb=16 * F, y_sc=F, hkf=hkf_d.data_ptr())
+                       y=y.data_ptr(), y_sb=16 * F, y_sc=F, hkf=hkf_d.data_ptr(), precision=prec)
     N.check(N.lib.rave_pqmf_analysis(C.byref(a), st))
     bands = torch.from_numpy(g["bands"]).to(dev)
     Fb = bands.shape[-1]
@@ -212,13 +215,59 @@ def test_pqmf_golden(N, dev, golden, causal):
     s_ = N.SynthesisArgs(n_band=16, taps=hki.shape[-1], batch=B, t_in=Fb,
                          pad_left=get_padding(hki.shape[-1], causal=causal)[0], mode=0, frame0=0, x_len=0,
                          x=bands.data_ptr(), x_sb=16 * Fb, x_sc=Fb, y=out.data_ptr(), y_sb=16 * Fb,
-                         hki=hki_d.data_ptr())
+                         hki=hki_d.data_ptr(), precision=prec)
     N.check(N.lib.rave_pqmf_synthesis(C.byref(s_), st))
     torch.cuda.synchronize()
     ref_a = g[f"analysis_{mode}"]
     ref_s = g[f"synthesis_{mode}"]
     assert maxabs(y.cpu().numpy(), ref_a) <= 1e-5 * max(1, np.abs(ref_a).max())
     assert maxabs(out.cpu().numpy(), ref_s) <= 1e-5 * max(1, np.abs(ref_s).max())
+
+
+@pytest.mark.parametrize("case", [
+    # (B, frames, mode, noise, pad, x_len, frame0, n_out)  -- offline and streaming shapes
+    (3, 300, 1, True, 16, 0, 0, 6), (2, 257, 2, True, 32, 0, 0, 16), (1, 2, 1, False, 0, 34, -32, 6),
+    (2, 4096, 1, False, 16, 0, 0, 6), (1, 64, 0, False, 0, 96, 7, 16)])
+def test_pqmf_split16_matches_f32(N, dev, golden, case):
+    """The split-f16 PQMF kernels against the exact-fp32 ones on every staging
+    path the plans use: amplitude modulation / noise / plain synthesis, cached
+    history (pad 0, x_len > frames, odd frame0), ragged lengths, 6 or 16 bands."""
+    from rave_amd.pqmf import kernels
+    B, Fr, mode, with_noise, pad, x_len, frame0, n_out = case
+    hkf, hki = kernels(golden("pqmf")["hk"])
+    hkf_d, hki_d = torch.from_numpy(hkf).to(dev), torch.from_numpy(hki).to(dev)
+    g = torch.Generator().manual_seed(7)
+    xl = x_len if x_len else Fr
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    # synthesis
+    z = torch.randn(B, 32, xl, generator=g).to(dev)
+    nz = (0.1 * torch.rand(B, 16, xl, generator=g)).to(dev) if with_noise else None
+    outs = []
+    for prec in (N.PREC_F32, N.PREC_SPLIT16):
+        y = torch.empty(B, 1, Fr * 16, device=dev)
+        a = N.SynthesisArgs(n_band=16, taps=hki.shape[-1], batch=B, t_in=Fr, pad_left=pad, mode=mode,
+                            frame0=frame0, x_len=x_len, x=z.data_ptr(), x_sb=32 * xl, x_sc=xl,
+                            noise=nz.data_ptr() if nz is not None else None, n_sb=16 * xl, n_sc=xl,
+                            y=y.data_ptr(), y_sb=16 * Fr, hki=hki_d.data_ptr(), precision=prec)
+        N.check(N.lib.rave_pqmf_synthesis(C.byref(a), st))
+        outs.append(y)
+    torch.cuda.synchronize()
+    ref = outs[0].cpu().numpy()
+    assert maxabs(outs[1].cpu().numpy(), ref) <= 2e-6 * max(1.0, np.abs(ref).max())
+    # analysis over the same number of frames
+    T = Fr * 16
+    x = (0.5 * torch.randn(B, 1, T, generator=g)).to(dev)
+    outs = []
+    for prec in (N.PREC_F32, N.PREC_SPLIT16):
+        y = torch.full((B, n_out, Fr), 7.0, device=dev)
+        a = N.AnalysisArgs(n_band=16, taps=hkf.shape[-1], n_out_bands=n_out, batch=B, t_in=T, pad_left=256,
+                           t_out=Fr, x=x.data_ptr(), x_sb=T, y=y.data_ptr(), y_sb=n_out * Fr, y_sc=Fr,
+                           hkf=hkf_d.data_ptr(), precision=prec)
+        N.check(N.lib.rave_pqmf_analysis(C.byref(a), st))
+        outs.append(y)
+    torch.cuda.synchronize()
+    ref = outs[0].cpu().numpy()
+    assert maxabs(outs[1].cpu().numpy(), ref) <= 2e-6 * max(1.0, np.abs(ref).max())
 
 
 # ------------------------------------------------------------------ full model vs golden
