@@ -15,6 +15,9 @@ LIB_PATH = os.path.join(_HERE, "librave_amd.so")
 # build (rave_amd/librave_amd_diag.so).  The product always loads LIB_PATH.
 if os.environ.get("RAVE_AMD_DIAG_LIB") == "1":
     LIB_PATH = os.path.join(_HERE, "librave_amd_diag.so")
+# ... or at an A/B experiment build (csrc/Makefile: OUT=../librave_amd_<name>.so)
+if os.environ.get("RAVE_AMD_LIB_VARIANT"):
+    LIB_PATH = os.path.join(_HERE, f"librave_amd_{os.environ['RAVE_AMD_LIB_VARIANT']}.so")
 
 RAVE_OK = 0
 RAVE_ERR_ARG = -1

@@ -140,7 +140,7 @@ __device__ __forceinline__ u32x4_t raw_rsrc(const void* p, int bytes) {
 // family's VC virtual channels -- more K-steps per barrier and per window DMA
 // round, and enough of them for four K-groups on the short-N layers (C >= 512
 // at 64-128 frames), which would otherwise need split-K slabs in HBM.
-template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 4096 / WM, int VCX = 1>
+template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 4096 / WM, int VCX = 1, int NS_ = 3>
 struct SGeo {
     using F = SFam<KT>;
     static constexpr int Q = F::Q, S = F::S, VC0 = F::VC, VC = VC0 * VCX;
@@ -162,17 +162,26 @@ struct SGeo {
     static constexpr int RS_MAX = XV ? ((XW_MAX * S + 3 + 3) / 4) * 4 : XW_MAX * S;
     static constexpr int RAW_F = CPC * RS_MAX;               // raw window floats of one chunk
     static constexpr int PF = XV ? 4 : 1;                    // floats per lane per DMA
-    static constexpr int XI = (RAW_F + 64 * PF * NW - 1) / (64 * PF * NW);   // window DMA pieces per wave
-    static constexpr int RAW = XI * NW * 256 * PF;           // raw window bytes (with slack)
-    static constexpr int STAGE = RAW;
-    // window DMA ring depth: a chunk's window is issued three chunks ahead and
-    // waited for one chunk before its split pass, so its load has two chunks of
-    // K-steps to land
-    static constexpr int NS = 4;
+    static constexpr int PB = 256 * PF;                      // bytes per wave DMA piece
+    static constexpr int NPIECE = (RAW_F * 4 + PB - 1) / PB; // pieces one chunk's window needs
+    static constexpr int XI = (NPIECE + NW - 1) / NW;        // window DMA pieces per wave
+    // ring slot: the pieces the window needs; every wave still issues XI DMAs
+    // (uniform hand counts), the surplus ones land in one dump piece
+    static constexpr int STAGE = NPIECE * PB;
+    // window DMA ring of NS slots: chunk c's window is issued at the top of
+    // chunk c - NS (into the slot chunk c - NS's window left: split during
+    // chunk c - NS - 1) and split during chunk c - 1, so it has NS - 1 chunks
+    // of K-steps to land (NS = 2 trades that for room for wider chunks)
+    static constexpr int NS = NS_;
+    // hand-counted vmcnt waits (kernel body): prologue, end of chunk, weights
+    static constexpr int WAIT_PRO = (NS - 1) * XI + 2 * KS0 * NJ;
+    static constexpr int WAIT_END = (NS - 1) * 2 * KS0 * NJ + (NS - 2) * XI;
+    static constexpr int WAIT_MAX = WAIT_PRO > WAIT_END ? WAIT_PRO : WAIT_END;
     static constexpr int ALPHA = 4096;                       // Snake alphas (<= 1024 channels)
     static constexpr int EROW = WN + 4;                      // epilogue transpose row stride (floats)
     static constexpr int EPI = NW * WM * EROW * 4;           // epilogue transpose area (reuses the ring)
-    static constexpr int MAIN = NS * STAGE + 2 * 2 * XPLANE + ALPHA;  // ring + two (hi, lo) plane pairs
+    // ring + two (hi, lo) plane pairs + Snake alphas + the surplus DMAs' dump piece
+    static constexpr int MAIN = NS * STAGE + 2 * 2 * XPLANE + ALPHA + PB;
     static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
     static constexpr int LDS_ALL = LDS + 16;                 // + the split-K "last arriver" word
     static constexpr int G8 = VC / 8;                        // 8-channel groups per row
@@ -182,16 +191,17 @@ struct SGeo {
     static_assert(KG == 1 || KG == 2 || KG == 4, "K-groups");
     // a configuration is built only if its hand-counted waits fit the vmcnt
     // field, its LDS fits the CU and every K-group has a K-step
-    static constexpr bool VALID = 2 * WR + 2 * XI <= 63 && LDS_ALL <= 160 * 1024 && ks_of(KG - 1) >= 1;
+    static constexpr bool VALID = WAIT_MAX <= 63 && WR + XI <= 63 && LDS_ALL <= 160 * 1024 && ks_of(KG - 1) >= 1 &&
+                                  (NS == 2 || NS == 3);
 };
 
 template <int V> struct IC {
     static constexpr int value = V;
 };
 
-template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX>
+template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX, int NS>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split_kernel(ConvKArgs a) {
-    using G = SGeo<KT, BM, BN, WM, XV, KG, WN_, VCX>;
+    using G = SGeo<KT, BM, BN, WM, XV, KG, WN_, VCX, NS>;
     constexpr int S = G::S, CPC = G::CPC, PH = G::PH;
     constexpr int NT = G::NT, NW = G::NW, NWT = G::NWT, WGM = G::WGM, G8 = G::G8, XT = G::XT;
     constexpr int NI = G::NI, NJ = G::NJ, WN = G::WN;
@@ -285,6 +295,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
     }
 
     // window of chunk c -> ring slot (per-lane offsets, out-of-range -> zeros)
+    const uint32_t dump = lds0 + G::NS * G::STAGE + 4 * G::XPLANE + G::ALPHA;
     auto issue = [&](int c, int stage) __attribute__((always_inline)) {
         const uint32_t sbase = lds0 + stage * G::STAGE;
         const int ci0 = c * CPC;
@@ -298,8 +309,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
             const int t = ta + tt * G::PF;
             const bool ok = (cl < CPC) && (ci < ci_lim) && (t >= 0) && (t < a.t_in);
             const unsigned voff = ok ? (unsigned)(ci * a.x_sc + t) * 4u : kOOB;
-            if constexpr (XV) dma16b(xrs, voff, sbase + piece * 1024);
-            else dma4(xrs, voff, sbase + piece * 256);
+            const uint32_t dst = piece < G::NPIECE ? sbase + piece * G::PB : dump;
+            if constexpr (XV) dma16b(xrs, voff, dst);
+            else dma4(xrs, voff, dst);
         }
     };
     // this wave's weight fragments: register ring, one chunk ahead (chunks past
@@ -382,26 +394,25 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
         constexpr int KS = G::ks_of(GG);                // own K-steps per chunk
         constexpr int ST0 = G::st_of(GG);               // first own K-step
         constexpr int WR = KS * NJ * 2, XI = G::XI;
-        issue(c_begin, 0);
-        issue(c_begin + 1, 1);
-        issue(c_begin + 2, 2);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) issue(c_begin + i, i);
 #pragma unroll
         for (int k = 0; k < KS; ++k) load_w(c_begin, k, ST0 + k);
-        wait_vm<2 * XI + WR>();                 // window c_begin landed
+        wait_vm<(NS - 1) * XI + WR>();          // window c_begin landed
         __syncthreads();
         convert(c_begin, 0, 0);
-        wait_vm<XI + WR>();                     // window c_begin+1 landed
+        wait_vm<(NS - 2) * XI + WR>();          // window c_begin+1 landed
         __syncthreads();
         stamp(1);
 
-        // per chunk c: DMA window c+3 | own K-steps (weights of c from the ring,
-        // refill with c+1) | split window c+1 into the other plane pair | wait + barrier
+        // per chunk c: DMA window c+NS into window c's slot (split during chunk
+        // c-1) | own K-steps (weights of c from the ring, refill with c+1) | split
+        // window c+1 into the other plane pair | wait + barrier
         int stage = 0;
         for (int c = c_begin; c < c_end; ++c) {
             const int pb = (c - c_begin) & 1;
-            const int s1 = (stage + 1) & 3;
-            const int s3 = (stage + 3) & 3;
-            issue(c + 3, s3);
+            const int s1 = stage + 1 == NS ? 0 : stage + 1;
+            issue(c + NS, stage);
             AFrag f[2];
             read_a(pb, ST0, f[0]);
 #pragma unroll
@@ -443,8 +454,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                     for (int i = k; i < XT; i += KS) convert_task(c + 1, s1, pb ^ 1, i);
                 }
             }
-            // window c+2 landed (window c+3 and the weights of c+1 and c+2 may fly)
-            wait_vm<2 * WR + XI>();
+            // window c+2 landed: younger are, per chunk since its issue, the
+            // weight refills and the next windows
+            wait_vm<(NS - 1) * WR + (NS - 2) * XI>();
             __syncthreads();
             stage = s1;
             if (c == c_begin) stamp(2);
@@ -718,36 +730,42 @@ struct SplitCfg {
 // (what the autotuner picks on every RAVE layer, profiles/r01_final/
 // tuning.json); slots 0-7 (round 1's retired 64-row / 128-column wave tiles,
 // which never won) now hold the wide-chunk tiles for the short-N layers:
-// two or four K-groups on 2- or 4-chunk windows (slots 4 and 6 measured no
-// better than these on any v2 layer and are not built).  Only the rows marked
-// built are instantiated.  Split-K counts of wide-chunk tiles are in staged chunks.
+// two or four K-groups on 2- or 4-chunk windows; slot 4 stages 4 packed chunks
+// in a two-slot ring (NS = 2: the LDS of a third slot buys the wider chunk;
+// picked for the ConvT / strided layers and some C = 512 k3).  Slot 6 (32 x 64,
+// four K-groups, 4-chunk windows) measured no better than these on any v2 layer
+// and is not built; neither are 64-row wave tiles with K-groups or eight
+// K-groups on 4/8-chunk windows, tried in round 2.  Only
+// the rows marked built are instantiated.  Split-K counts of wide-chunk tiles
+// are in staged chunks.
 constexpr int kNumSplitTiles = 16;
-[[maybe_unused]] constexpr int kSplitTiles[kNumSplitTiles][6] = {   // BM, BN, WM, KG, WN, VCX
-    {64, 64, 32, 4, 64, 2},   {64, 64, 32, 4, 64, 4},   {128, 64, 32, 2, 64, 2},  {32, 64, 32, 4, 64, 2},
-    {128, 64, 32, 4, 64, 2},  {64, 128, 32, 2, 64, 2},  {32, 64, 32, 4, 64, 4},   {64, 64, 32, 2, 64, 2},
-    {128, 128, 32, 2, 128, 1}, {256, 64, 64, 2, 64, 1}, {128, 64, 32, 1, 64, 1},  {64, 128, 32, 1, 64, 1},
-    {256, 64, 32, 1, 64, 1},  {256, 64, 32, 2, 64, 1},  {128, 64, 32, 2, 64, 1},  {64, 128, 32, 2, 64, 1}};
-[[maybe_unused]] constexpr bool kSplitTileBuilt[kNumSplitTiles] = {true,  true,  true,  true,  false, true,  false, true,
+[[maybe_unused]] constexpr int kSplitTiles[kNumSplitTiles][7] = {   // BM, BN, WM, KG, WN, VCX, NS
+    {64, 64, 32, 4, 64, 2, 3},   {64, 64, 32, 4, 64, 4, 3},   {128, 64, 32, 2, 64, 2, 3},  {32, 64, 32, 4, 64, 2, 3},
+    {64, 64, 32, 4, 64, 4, 2},   {64, 128, 32, 2, 64, 2, 3},  {32, 64, 32, 4, 64, 4, 3},   {64, 64, 32, 2, 64, 2, 3},
+    {128, 128, 32, 2, 128, 1, 3}, {256, 64, 64, 2, 64, 1, 3}, {128, 64, 32, 1, 64, 1, 3},  {64, 128, 32, 1, 64, 1, 3},
+    {256, 64, 32, 1, 64, 1, 3},  {256, 64, 32, 2, 64, 1, 3},  {128, 64, 32, 2, 64, 1, 3},  {64, 128, 32, 2, 64, 1, 3}};
+[[maybe_unused]] constexpr bool kSplitTileBuilt[kNumSplitTiles] = {true,  true,  true,  true,  true,  true,  false, true,
                                                   false, false, true,  true,  true,  true,  true,  true};
 [[maybe_unused]] constexpr int kSplitDefaultTile = 10;
 
-// Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>, IC<WN>, IC<VCX>) for a built tile
+// Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>, IC<WN>, IC<VCX>, IC<NS>) for a built tile
 // index ti (compile-time dispatch; callers check kSplitTileBuilt first).
 template <typename Fn>
 static inline auto with_tile(int ti, Fn&& f) {
     switch (ti) {
-        case 0: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<2>{});
-        case 1: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<4>{});
-        case 2: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{});
-        case 3: return f(IC<32>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<2>{});
-        case 5: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{});
-        case 7: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{});
-        case 11: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{});
-        case 12: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{});
-        case 13: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{});
-        case 14: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{});
-        case 15: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{});
-        default: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{});   // 10
+        case 0: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<2>{}, IC<3>{});
+        case 1: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<4>{}, IC<3>{});
+        case 2: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{}, IC<3>{});
+        case 3: return f(IC<32>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<2>{}, IC<3>{});
+        case 4: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<4>{}, IC<2>{});
+        case 5: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{}, IC<3>{});
+        case 7: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{}, IC<3>{});
+        case 11: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});
+        case 12: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});
+        case 13: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{}, IC<3>{});
+        case 14: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{}, IC<3>{});
+        case 15: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{}, IC<3>{});
+        default: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});   // 10
     }
 }
 
@@ -759,9 +777,9 @@ template <int KT, bool SNAKE, bool XV>
 int split_launch_inst(ConvKArgs k, int tile, hipStream_t st);
 
 #ifdef RAVE_SPLIT_KT
-template <int KT, int BM, int BN, int WM, int KG, int WN, int VCX, bool SNAKE, bool XV>
+template <int KT, int BM, int BN, int WM, int KG, int WN, int VCX, int NS, bool SNAKE, bool XV>
 static int split_launch_xv(ConvKArgs k, hipStream_t st) {
-    using G = SGeo<KT, BM, BN, WM, XV, KG, WN, VCX>;
+    using G = SGeo<KT, BM, BN, WM, XV, KG, WN, VCX, NS>;
     if constexpr (!G::VALID) {
         set_error("conv1d(split16): tile exceeds LDS or the vmcnt range");
         return RAVE_ERR_UNSUPPORTED;
@@ -773,7 +791,7 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
         constexpr size_t lds = (size_t)G::LDS_ALL;
         static_assert(lds <= 160 * 1024, "LDS budget");
         dim3 grid(k.gx * k.gy * k.B * k.S);
-        auto kern = conv1d_split_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN, VCX>;
+        auto kern = conv1d_split_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN, VCX, NS>;
         if (lds > 64 * 1024) {
             static bool done = false;
             if (!done) {
@@ -789,10 +807,11 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
 
 template <int KT, bool SNAKE, bool XV>
 int split_launch_inst(ConvKArgs k, int tile, hipStream_t st) {
-    return with_tile(tile, [&](auto bm, auto bn, auto wm, auto kg, auto wn, auto vcx) {
+    return with_tile(tile, [&](auto bm, auto bn, auto wm, auto kg, auto wn, auto vcx, auto ns) {
         constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
-                      KG = decltype(kg)::value, WN = decltype(wn)::value, VCX = decltype(vcx)::value;
-        return split_launch_xv<KT, BM, BN, WM, KG, WN, VCX, SNAKE, XV>(k, st);
+                      KG = decltype(kg)::value, WN = decltype(wn)::value, VCX = decltype(vcx)::value,
+                      NS = decltype(ns)::value;
+        return split_launch_xv<KT, BM, BN, WM, KG, WN, VCX, NS, SNAKE, XV>(k, st);
     });
 }
 template int split_launch_inst<RAVE_SPLIT_KT, (RAVE_SPLIT_SNAKE != 0), (RAVE_SPLIT_XV != 0)>(ConvKArgs, int,
@@ -850,10 +869,12 @@ static inline int tile_waves(int ti) {   // waves per workgroup
 
 template <int KT>
 static bool split_tile_fits(int idx) {   // both DMA variants must fit
-    return with_tile(idx, [](auto bm, auto bn, auto wm, auto kg, auto wn, auto vcx) {
+    return with_tile(idx, [](auto bm, auto bn, auto wm, auto kg, auto wn, auto vcx, auto ns) {
         constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
-                      KG = decltype(kg)::value, WN = decltype(wn)::value, VCX = decltype(vcx)::value;
-        return SGeo<KT, BM, BN, WM, true, KG, WN, VCX>::VALID && SGeo<KT, BM, BN, WM, false, KG, WN, VCX>::VALID;
+                      KG = decltype(kg)::value, WN = decltype(wn)::value, VCX = decltype(vcx)::value,
+                      NS = decltype(ns)::value;
+        return SGeo<KT, BM, BN, WM, true, KG, WN, VCX, NS>::VALID &&
+               SGeo<KT, BM, BN, WM, false, KG, WN, VCX, NS>::VALID;
     });
 }
 static bool split_fits(int taps, int idx) {
