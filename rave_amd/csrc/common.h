@@ -64,6 +64,21 @@ inline void launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st
     }
 }
 
+// Logical workgroup id of a 1-D grid, XCD-major: blocks are dealt round-robin
+// over the 8 XCDs, so block i runs on XCD i % 8; the remap hands every XCD a
+// contiguous run of logical ids (batch-major tile orders: a contiguous run of
+// batch items).  Every kernel of the path uses the same batch-major order, so
+// an XCD reads the activations of the batch items it wrote in the previous
+// launch out of its own L2 instead of another XCD's (via the Infinity Cache).
+// A bijection for any grid, so correctness never depends on the placement.
+__device__ __forceinline__ int xcd_major(int lin, int grid) {
+#ifndef RAVE_LEGACY_MAP
+    if ((grid & 7) == 0) return (lin & 7) * (grid >> 3) + (lin >> 3);
+#endif
+    (void)grid;
+    return lin;
+}
+
 constexpr int ceil_div(int a, int b) { return (a + b - 1) / b; }
 constexpr int64_t ceil_div64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

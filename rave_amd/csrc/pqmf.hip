@@ -57,8 +57,10 @@ __global__ __launch_bounds__(64 * kPqWaves) void pqmf_analysis_kernel(rave_pqmf_
     float* hs = smem;                                  // [16][kAnaHR]
     float* xs = smem + 16 * kAnaHR;                    // [wframes][17]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int t0 = blockIdx.x * kPqFrames;
-    const int b = blockIdx.y;
+    const int lg_ = __builtin_amdgcn_readfirstlane(
+        xcd_major(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y));
+    const int b = lg_ / gridDim.x;
+    const int t0 = (lg_ - b * gridDim.x) * kPqFrames;
     const float* xb = a.x + (int64_t)b * a.x_sb;
     // filter rows >= NBO are zero; rows < NBO: taps, zero-padded to 4*ksteps.
     // All loads of a thread are issued before its first LDS store.
@@ -152,8 +154,10 @@ __global__ __launch_bounds__(64 * kPqWaves) void pqmf_synthesis_kernel(rave_pqmf
     float* hs = smem;                        // [16][kSynHR]
     float* xs = smem + 16 * kSynHR;          // [16][xr]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n0 = blockIdx.x * kPqFrames;
-    const int b = blockIdx.y;
+    const int lg_ = __builtin_amdgcn_readfirstlane(
+        xcd_major(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y));
+    const int b = lg_ / gridDim.x;
+    const int n0 = (lg_ - b * gridDim.x) * kPqFrames;
     PQ_STAMP(0);
     // every load of a thread is issued before its first LDS store
     constexpr int NT = 64 * kPqWaves;
@@ -296,8 +300,10 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_analysis_split_kernel(rave
     float* red = reinterpret_cast<float*>(xl + WS);
     constexpr int NT = 64 * kPsWaves;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int t0 = blockIdx.x * kPsFrames;
-    const int b = blockIdx.y;
+    const int lg_ = __builtin_amdgcn_readfirstlane(
+        xcd_major(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y));
+    const int b = lg_ / gridDim.x;
+    const int t0 = (lg_ - b * gridDim.x) * kPsFrames;
     const float* xb = a.x + (int64_t)b * a.x_sb;
     // filter: rows < NBO, taps < a.taps (all loads before the first LDS store)
     constexpr int KW = 32 * kPsK;                             // 544
@@ -396,8 +402,10 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_synthesis_split_kernel(rav
     constexpr int nb = 16, taps = kSynTaps, kdim = nb * taps;
     constexpr int NT = 64 * kPsWaves;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n0 = blockIdx.x * kPsFrames;
-    const int b = blockIdx.y;
+    const int lg_ = __builtin_amdgcn_readfirstlane(
+        xcd_major(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y));
+    const int b = lg_ / gridDim.x;
+    const int n0 = (lg_ - b * gridDim.x) * kPsFrames;
     constexpr int KW = 32 * kPsK;                             // 544
     constexpr int HT = (16 * KW + NT - 1) / NT;
     float hv[HT];

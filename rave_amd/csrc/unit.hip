@@ -125,8 +125,9 @@ __global__ __launch_bounds__(kUnitThreads) void residual_unit_kernel(UnitKArgs a
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int b = blockIdx.x / a.ntiles;
-    const int n0 = (blockIdx.x - b * a.ntiles) * G::BN;
+    const int lg = __builtin_amdgcn_readfirstlane(xcd_major(blockIdx.x, gridDim.x));
+    const int b = lg / a.ntiles;
+    const int n0 = (lg - b * a.ntiles) * G::BN;
     const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
 
     const auto xrs = unit_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);

@@ -125,8 +125,9 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     const int twave = wave - kg * G::NWT;
     const int wm = twave % G::WGM, wn = twave / G::WGM;
     const int hh = lane >> 5, l32 = lane & 31;
-    const int b = blockIdx.x / a.ntiles;
-    const int n0 = (blockIdx.x - b * a.ntiles) * G::BN;
+    const int lg = __builtin_amdgcn_readfirstlane(xcd_major(blockIdx.x, gridDim.x));
+    const int b = lg / a.ntiles;
+    const int n0 = (lg - b * a.ntiles) * G::BN;
     const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
     const int XW = a.XW;
     const int ntask = XW * G8;
