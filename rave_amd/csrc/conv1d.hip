@@ -101,10 +101,18 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
     const int h = lane >> 5;
     const int l32 = lane & 31;
 
-    const int n0 = blockIdx.x * BN;
-    const int m0 = blockIdx.y * BM;
-    const int b = __builtin_amdgcn_readfirstlane(blockIdx.z / a.S);
-    const int split = __builtin_amdgcn_readfirstlane(blockIdx.z - b * a.S);
+    // XCD-major order over the (column tile, row tile, batch x split) grid:
+    // every XCD runs a contiguous run of batch items (common.h xcd_major)
+    const int gxy = gridDim.x * gridDim.y;
+    const int lg = __builtin_amdgcn_readfirstlane(
+        xcd_major(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), gxy * gridDim.z));
+    const int bz = __builtin_amdgcn_readfirstlane(lg / gxy);
+    const int bxy = lg - bz * gxy;
+    const int by = __builtin_amdgcn_readfirstlane(bxy / gridDim.x);
+    const int n0 = (bxy - by * gridDim.x) * BN;
+    const int m0 = by * BM;
+    const int b = __builtin_amdgcn_readfirstlane(bz / a.S);
+    const int split = __builtin_amdgcn_readfirstlane(bz - b * a.S);
     const int c_begin = split * a.cps;
     const int c_end = min(a.nchunks, c_begin + a.cps);
     const int in0 = n0 * ST - ((m0 < a.split_row) ? a.pad_l : a.pad_g1);   // ConvT phase groups
