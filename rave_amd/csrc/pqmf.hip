@@ -259,8 +259,11 @@ __global__ __launch_bounds__(64 * kPqWaves) void pqmf_synthesis_kernel(rave_pqmf
 typedef _Float16 ps_h8 __attribute__((ext_vector_type(8)));
 typedef float ps_f32x8 __attribute__((ext_vector_type(8)));
 constexpr int kPsWaves = 4;
-constexpr int kPsBlk = 4;
-constexpr int kPsFrames = kPsWaves * kPsBlk * 16;            // frames per workgroup (256)
+#ifndef RAVE_PS_BLK
+#define RAVE_PS_BLK 2                   // measured (profiles/r02_xcd/ab_pqmf_blk.txt): 2 beats 4 and 1
+#endif
+constexpr int kPsBlk = RAVE_PS_BLK;                         // 16-frame blocks per wave
+constexpr int kPsFrames = kPsWaves * kPsBlk * 16;            // frames per workgroup (128)
 constexpr int kPsK = 17;                                     // 32-deep K-steps (<= 544 taps / K rows)
 constexpr int kPsKP = 552;                                   // halves per filter row: 1104 B = 20 banks mod 64
 
