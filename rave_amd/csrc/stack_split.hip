@@ -411,6 +411,17 @@ extern "C" int rave_residual_stack(const rave_stack_args* p, void* stream) {
     // 8 centre blocks, 5 blocks per wave (2 column waves share each weight row
     // block): 40.0 us against 46.5 us for the three unit launches; C = 128 (2
     // centre blocks, 2 per wave) 43.6 against 43.1 -- the autotuner keeps the units
-    if (C == 64) return ss_launch<64, 8, 5>(k, p->batch, snake, st);
-    return ss_launch<128, 2, 2>(k, p->batch, snake, st);
+    // Round 2 (same-box A/Bs in the bench step, profiles/r02_xcd/ab_stack_geometry.txt):
+    // C = 64 with two blocks per wave (10 waves: 5 column waves per 32-row block)
+    // 38.2 -> 35.5 us against five blocks per wave (4 waves)
+#ifndef RAVE_S64_NB
+#define RAVE_S64_NB 8
+#define RAVE_S64_CB 2
+#endif
+#ifndef RAVE_S128_NB
+#define RAVE_S128_NB 2
+#define RAVE_S128_CB 2
+#endif
+    if (C == 64) return ss_launch<64, RAVE_S64_NB, RAVE_S64_CB>(k, p->batch, snake, st);
+    return ss_launch<128, RAVE_S128_NB, RAVE_S128_CB>(k, p->batch, snake, st);
 }
