@@ -508,8 +508,17 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
     // (WGN, CB) per C, measured (tools/layer_bench.py unit_*): C=256 with one
     // column block per wave 19.6 -> 14.4 us; C=128 11.6 -> 11.3 us; wider waves
     // (CB 3-4, one column wave) measured slower for C=64 and C=128
-    if (C == 64) return go(IC<64>{}, IC<2>{}, IC<1>{}, IC<1>{}, IC<2>{});
-    if (C == 128) return go(IC<128>{}, IC<2>{}, IC<1>{}, IC<1>{}, IC<1>{});
+#ifndef RAVE_U64_CB
+#define RAVE_U64_CB 2
+#endif
+#ifndef RAVE_U64_WGN
+#define RAVE_U64_WGN 2
+#endif
+#ifndef RAVE_U128_WGN
+#define RAVE_U128_WGN 2
+#endif
+    if (C == 64) return go(IC<64>{}, IC<RAVE_U64_WGN>{}, IC<1>{}, IC<1>{}, IC<RAVE_U64_CB>{});
+    if (C == 128) return go(IC<128>{}, IC<RAVE_U128_WGN>{}, IC<1>{}, IC<1>{}, IC<1>{});
     if (C == 256) return go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{});
     return go(IC<512>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{});
 }
