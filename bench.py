@@ -57,8 +57,12 @@ FAMILIES = {
     "unit_split16": ("unit_split_kernel, split-f16 MFMA 32x32x16 (3 per fp32 MAC)", PEAK_SPLIT16_TFLOPS),
     "stack_split16": ("stack_split_kernel (3 residual units per launch), split-f16 MFMA 32x32x16",
                       PEAK_SPLIT16_TFLOPS),
-    "pqmf_analysis": ("pqmf_analysis_kernel, fp32 MFMA 16x16x4", PEAK_FP32_TFLOPS),
-    "pqmf_synthesis": ("pqmf_synthesis_kernel, fp32 MFMA 16x16x4", PEAK_FP32_TFLOPS),
+    "pqmf_analysis_f32": ("pqmf_analysis_kernel, fp32 MFMA 16x16x4", PEAK_FP32_TFLOPS),
+    "pqmf_synthesis_f32": ("pqmf_synthesis_kernel, fp32 MFMA 16x16x4", PEAK_FP32_TFLOPS),
+    "pqmf_analysis_split16": ("pqmf_analysis_split_kernel, split-f16 MFMA 16x16x32 (3 per fp32 MAC)",
+                              PEAK_SPLIT16_TFLOPS),
+    "pqmf_synthesis_split16": ("pqmf_synthesis_split_kernel, split-f16 MFMA 16x16x32 (3 per fp32 MAC)",
+                               PEAK_SPLIT16_TFLOPS),
 }
 
 
@@ -72,9 +76,9 @@ def op_family(kind: int, precision: int) -> str:
     if kind == N.OP_STACK:
         return "stack_split16"
     if kind == N.OP_PQMF_ANALYSIS:
-        return "pqmf_analysis"
+        return "pqmf_analysis_" + prec
     if kind == N.OP_PQMF_SYNTHESIS:
-        return "pqmf_synthesis"
+        return "pqmf_synthesis_" + prec
     return "other"
 
 

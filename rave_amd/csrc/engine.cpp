@@ -998,6 +998,7 @@ void Model::analysis_op(Plan& p, int B, int T, const View& x, const View& y, int
                                 });
     }
     PlanOp& o = p.add(RAVE_OP_PQMF_ANALYSIS, a, "pqmf_analysis");
+    o.prec = a.precision;
     rave_pqmf_analysis_args& A = *reinterpret_cast<rave_pqmf_analysis_args*>(o.op.u.raw);
     View h = arena_view(hkf_off);
     p.bind(o, A, A.x, &x);
@@ -1041,6 +1042,7 @@ void Model::synthesis_op(Plan& p, int B, int F, const View& x, const View& y, co
                                 });
     }
     PlanOp& o = p.add(RAVE_OP_PQMF_SYNTHESIS, a, "pqmf_synthesis");
+    o.prec = a.precision;
     rave_pqmf_synthesis_args& A = *reinterpret_cast<rave_pqmf_synthesis_args*>(o.op.u.raw);
     View h = arena_view(hki_off);
     p.bind(o, A, A.x, &x);

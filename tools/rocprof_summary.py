@@ -31,8 +31,10 @@ FAMILIES = {
     "unit_f32": ("residual_unit_kernel", ()),
     "unit_split16": ("unit_split_kernel", ()),
     "stack_split16": ("stack_split_kernel", ()),
-    "pqmf_analysis": ("pqmf_analysis_kernel", ()),
-    "pqmf_synthesis": ("pqmf_synthesis_kernel", ()),
+    "pqmf_analysis_f32": ("pqmf_analysis_kernel", ()),
+    "pqmf_synthesis_f32": ("pqmf_synthesis_kernel", ()),
+    "pqmf_analysis_split16": ("pqmf_analysis_split_kernel", ()),
+    "pqmf_synthesis_split16": ("pqmf_synthesis_split_kernel", ()),
 }
 _KERNEL_FAMILY = {}
 for _fam, (_main, _helpers) in FAMILIES.items():
