@@ -735,17 +735,20 @@ struct SplitCfg {
 // picked for the ConvT / strided layers and some C = 512 k3).  Slot 6 (32 x 64,
 // four K-groups, 4-chunk windows) measured no better than these on any v2 layer
 // and is not built; neither are 64-row wave tiles with K-groups or eight
-// K-groups on 4/8-chunk windows, tried in round 2.  Only
+// K-groups on 4/8-chunk windows, tried in round 2.  Slots
+// 8-9 (round 2, last session): 256-column tiles of 32x64 waves for the layers
+// with few rows and a long time axis (the edge convs, the C = 64 ConvT), so
+// that one round of workgroups covers the layer.  Only
 // the rows marked built are instantiated.  Split-K counts of wide-chunk tiles
 // are in staged chunks.
 constexpr int kNumSplitTiles = 16;
 [[maybe_unused]] constexpr int kSplitTiles[kNumSplitTiles][7] = {   // BM, BN, WM, KG, WN, VCX, NS
     {64, 64, 32, 4, 64, 2, 3},   {64, 64, 32, 4, 64, 4, 3},   {128, 64, 32, 2, 64, 2, 3},  {32, 64, 32, 4, 64, 2, 3},
     {64, 64, 32, 4, 64, 4, 2},   {64, 128, 32, 2, 64, 2, 3},  {32, 64, 32, 4, 64, 4, 3},   {64, 64, 32, 2, 64, 2, 3},
-    {128, 128, 32, 2, 128, 1, 3}, {256, 64, 64, 2, 64, 1, 3}, {128, 64, 32, 1, 64, 1, 3},  {64, 128, 32, 1, 64, 1, 3},
+    {32, 256, 32, 1, 64, 1, 3},  {64, 256, 32, 1, 64, 1, 3},  {128, 64, 32, 1, 64, 1, 3},  {64, 128, 32, 1, 64, 1, 3},
     {256, 64, 32, 1, 64, 1, 3},  {256, 64, 32, 2, 64, 1, 3},  {128, 64, 32, 2, 64, 1, 3},  {64, 128, 32, 2, 64, 1, 3}};
 [[maybe_unused]] constexpr bool kSplitTileBuilt[kNumSplitTiles] = {true,  true,  true,  true,  true,  true,  false, true,
-                                                  false, false, true,  true,  true,  true,  true,  true};
+                                                  true,  true,  true,  true,  true,  true,  true,  true};
 [[maybe_unused]] constexpr int kSplitDefaultTile = 10;
 
 // Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>, IC<WN>, IC<VCX>, IC<NS>) for a built tile
@@ -760,6 +763,8 @@ static inline auto with_tile(int ti, Fn&& f) {
         case 4: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<4>{}, IC<2>{});
         case 5: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{}, IC<3>{});
         case 7: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{}, IC<3>{});
+        case 8: return f(IC<32>{}, IC<256>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});
+        case 9: return f(IC<64>{}, IC<256>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});
         case 11: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});
         case 12: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});
         case 13: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{}, IC<3>{});
