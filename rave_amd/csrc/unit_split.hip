@@ -518,8 +518,14 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
 #define RAVE_U128_WGN 2
 #endif
     if (C == 64) return go(IC<64>{}, IC<RAVE_U64_WGN>{}, IC<1>{}, IC<1>{}, IC<RAVE_U64_CB>{});
-    if (C == 128) return go(IC<128>{}, IC<RAVE_U128_WGN>{}, IC<1>{}, IC<1>{}, IC<1>{});
-    if (C == 256) return go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{});
+#ifndef RAVE_U128_KG
+#define RAVE_U128_KG 1
+#endif
+#ifndef RAVE_U256_KG
+#define RAVE_U256_KG 1
+#endif
+    if (C == 128) return go(IC<128>{}, IC<RAVE_U128_WGN>{}, IC<1>{}, IC<RAVE_U128_KG>{}, IC<1>{});
+    if (C == 256) return go(IC<256>{}, IC<1>{}, IC<1>{}, IC<RAVE_U256_KG>{}, IC<1>{});
     return go(IC<512>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{});
 }
 }  // namespace rave

@@ -3,8 +3,8 @@
 # parity subset per variant, then the alternating bench A/B.
 set -e -o pipefail
 O=gpurun_out/ugeo; mkdir -p $O
-for v in ue uf; do
+for v in ug; do
   RAVE_AMD_LIB_VARIANT=$v timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -k "unit or stack or model_golden" --timeout 120 --timeout-method thread > $O/pytest_$v.log 2>&1
   echo "$v: $(tail -1 $O/pytest_$v.log)"
 done
-TAG=ugeo bash tools/ab_xcd.sh "" ue uf
+TAG=ugeo bash tools/ab_xcd.sh "" ug
