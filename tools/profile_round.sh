@@ -4,7 +4,8 @@
 #   2. rocprofv3 --kernel-trace --stats of the same command (per-kernel times),
 #   3./4. separate --pmc FETCH_SIZE / WRITE_SIZE passes (HBM traffic; the two
 #      counters do not fit one gfx950 pass),
-# then tools/rocprof_summary.py.  Every GPU step has its own time limit and the
+#   5. a --pmc SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE pass (MFMA utilisation per family),
+# then tools/rocprof_summary.py and tools/mfma_util.py.  Every GPU step has its own time limit and the
 # script stops at the first failure.
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -28,6 +29,14 @@ timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv 
     python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --pipeline 1 \
     --tuning-in "$OUT/tuning.json" > "$OUT/bench_write.json" 2> "$OUT/bench_write.err"
 echo "write pass done"
+timeout -k 10 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/mfma" -o run -- \
+    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --pipeline 1 --no-f32 \
+    --tuning-in "$OUT/tuning.json" > "$OUT/bench_mfma.json" 2> "$OUT/bench_mfma.err"
+echo "mfma pass done"
+MF=$(find "$OUT/mfma" -name '*counter_collection.csv' | head -n 1)
+python3 "$R/tools/mfma_util.py" "$MF" "$OUT/bench.json" > "$OUT/mfma_util.json"
+head -n 1 "$MF" > "$MF.gemm"; grep -E 'conv1d|split_reduce|unit_kernel|unit_split|stack_split|pqmf' "$MF" >> "$MF.gemm" || true
+rm -f "$MF"
 KT=$(find "$OUT/kt" -name '*kernel_trace.csv' | head -n 1)
 FE=$(find "$OUT/fetch" -name '*counter_collection.csv' | head -n 1)
 WR=$(find "$OUT/write" -name '*counter_collection.csv' | head -n 1)
