@@ -79,6 +79,13 @@ __device__ __forceinline__ int xcd_major(int lin, int grid) {
     return lin;
 }
 
+// Cache-policy bits of the layer-output stores (buffer instruction aux field;
+// 16 = sc1, write-through).  Default: plain stores (the line stays in the
+// writing XCD's L2 for the next kernel's reads).
+#ifndef RAVE_YAUX
+#define RAVE_YAUX 0
+#endif
+
 constexpr int ceil_div(int a, int b) { return (a + b - 1) / b; }
 constexpr int64_t ceil_div64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

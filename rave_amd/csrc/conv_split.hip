@@ -628,7 +628,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                         if (a.bias) v += a.bias[m];
                         if (a.res) v += rv[it];
                         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), yrs,
-                                                               (unsigned)(m * a.y_sc + n) * 4u, 0, 0);
+                                                               (unsigned)(m * a.y_sc + n) * 4u, 0, RAVE_YAUX);
                     }
                 }
             } else {
@@ -664,7 +664,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                 const s_f32x4 v = *reinterpret_cast<const s_f32x4*>(et + r * G::EROW + cc) + rv[it];
                 if (m < a.M && n + 3 < a.U) {
                     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), yrs,
-                                                           (unsigned)(m * a.y_sc + n) * 4u, 0, 0);
+                                                           (unsigned)(m * a.y_sc + n) * 4u, 0, RAVE_YAUX);
                 } else {
                     float vv[4];
                     *reinterpret_cast<s_f32x4*>(vv) = *reinterpret_cast<const s_f32x4*>(et + r * G::EROW + cc);
@@ -674,7 +674,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                         const float rs = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                             rrs, ok ? (unsigned)(m * a.r_sc + n + e) * 4u : kOOB, 0, 0));
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, vv[e] + rs), yrs,
-                                                              ok ? (unsigned)(m * a.y_sc + n + e) * 4u : kOOB, 0, 0);
+                                                              ok ? (unsigned)(m * a.y_sc + n + e) * 4u : kOOB, 0, RAVE_YAUX);
                     }
                 }
             }
@@ -690,7 +690,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                     const float rs = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                         rrs, ok ? (unsigned)(m * a.r_sc + n + e) * 4u : kOOB, 0, 0));
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, vp[e] + rs), yrs,
-                                                          ok ? (unsigned)(m * a.y_sc + n + e) * 4u : kOOB, 0, 0);
+                                                          ok ? (unsigned)(m * a.y_sc + n + e) * 4u : kOOB, 0, RAVE_YAUX);
                 }
             }
         }
@@ -712,7 +712,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                     const int n = n0 + wn * WN + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                     const int t = n * a.R + q;
                     const unsigned off = (rowok && n < a.U && t < a.t_y) ? (unsigned)(co * a.y_sc + t) * 4u : kOOB;
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][j][r] + bv), yrs, off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][j][r] + bv), yrs, off, 0, RAVE_YAUX);
                 }
         }
         stamp(4);

@@ -328,7 +328,7 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
         for (int r = 0; r < 16; ++r) {
             const int m = mrow0 + 8 * (r >> 2) + (r & 3);
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, yv[j][r]), yrs,
-                                                  ok ? (unsigned)(m * a.y_sc + t) * 4u : kSSOOB, 0, 0);
+                                                  ok ? (unsigned)(m * a.y_sc + t) * 4u : kSSOOB, 0, RAVE_YAUX);
         }
     }
 }

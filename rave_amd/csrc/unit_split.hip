@@ -370,7 +370,7 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
                     for (int e = 0; e < 4; ++e)
                         __builtin_amdgcn_raw_buffer_store_b32(
                             __builtin_bit_cast(unsigned, acc[i][j][4 * g + e] * rs[e] + bb[e] + res[i][j][4 * g + e]),
-                            yrs, nok ? (unsigned)((m + e) * a.y_sc + n) * 4u : kUSOOB, 0, 0);
+                            yrs, nok ? (unsigned)((m + e) * a.y_sc + n) * 4u : kUSOOB, 0, RAVE_YAUX);
                 }
             }
     }
