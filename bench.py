@@ -139,6 +139,8 @@ def cpu_baseline(cfg, params, spk, B: int, T: int, seconds: float, threads: int)
 
 
 DTYPE = {"f32": "fp32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32)",
+         "f32_tuned": "fp32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32; launch configurations and fused/unfused "
+                      "units autotuned)",
          "split16": "fp32 I/O, split-f16 GEMMs (3 f16 MFMA passes hi*hi+hi*lo+lo*hi on ~22-bit operands, "
                     "fp32 accumulate)",
          "auto": "fp32 I/O; per op the faster of exact-fp32 MFMA and split-f16 GEMMs (3 f16 MFMA passes on "
@@ -338,7 +340,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
     ap.add_argument("--samples", type=int, default=65536, help="samples per clip")
     ap.add_argument("--config", default="v2")
-    ap.add_argument("--precision", default="auto", choices=["f32", "split16", "auto"],
+    ap.add_argument("--precision", default="auto", choices=["f32", "f32_tuned", "split16", "auto"],
                     help="conv/unit GEMM arithmetic of the headline (include/rave_amd.h RAVE_PREC_*); "
                          "auto = the faster of the two per op, timed when the plans are built")
     ap.add_argument("--no-f32", action="store_true",
@@ -377,8 +379,9 @@ def main():
 
     head, y_head = run_mode(a, cfg, params, spk, a.precision, x, dev, world, rank, rank == 0)
     exact = None
-    if a.precision != "f32" and not a.no_f32:
-        exact, y_f32 = run_mode(a, cfg, params, spk, "f32", x, dev, world, rank, False)
+    if a.precision not in ("f32", "f32_tuned") and not a.no_f32:
+        # exact fp32 on every op, with the same launch-configuration autotuning as the headline
+        exact, y_f32 = run_mode(a, cfg, params, spk, "f32_tuned", x, dev, world, rank, False)
         # the same input through both arithmetic modes (north star: <= 1e-4 max-abs)
         exact["headline_vs_f32_max_abs"] = float((y_head - y_f32).abs().max())
         del y_f32

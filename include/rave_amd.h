@@ -498,7 +498,9 @@ int rave_maxpool(const rave_maxpool_args* a, void* stream);
  */
 #define RAVE_MAX_RATIOS 8
 #define RAVE_MAX_DILATIONS 8
-enum { RAVE_PREC_AUTO = 2 };   /* per op the faster of F32 / SPLIT16, timed at plan build */
+enum { RAVE_PREC_AUTO = 2,     /* per op the faster of F32 / SPLIT16, timed at plan build */
+       RAVE_PREC_F32_TUNED = 3 /* exact fp32 on every op; launch configurations and fused /
+                                  unfused unit choices timed at plan build as in AUTO */ };
 
 typedef struct rave_model_config {
     int32_t n_band;               /* PQMF bands (v1.gin: 16)                                */

@@ -46,6 +46,7 @@ SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the 
 PREC_F32 = 0
 PREC_SPLIT16 = 1
 PREC_AUTO = 2
+PREC_F32_TUNED = 3      # exact fp32, launch choices autotuned (RAVE_PREC_F32_TUNED)
 PRECISION = {"f32": PREC_F32, "split16": PREC_SPLIT16}
 STREAM_GRAPH = 1
 

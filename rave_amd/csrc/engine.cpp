@@ -1245,8 +1245,9 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
     build_graph(cfg, m->g);
     if (precision == RAVE_PREC_AUTO) m->precs = {RAVE_PREC_F32, RAVE_PREC_SPLIT16};
     else if (precision == RAVE_PREC_F32 || precision == RAVE_PREC_SPLIT16) m->precs = {precision};
-    else fail(RAVE_ERR_ARG, "precision must be RAVE_PREC_F32, RAVE_PREC_SPLIT16 or RAVE_PREC_AUTO");
-    m->autotune = precision == RAVE_PREC_AUTO;
+    else if (precision == RAVE_PREC_F32_TUNED) m->precs = {RAVE_PREC_F32};
+    else fail(RAVE_ERR_ARG, "precision must be RAVE_PREC_F32, RAVE_PREC_SPLIT16, RAVE_PREC_AUTO or RAVE_PREC_F32_TUNED");
+    m->autotune = precision == RAVE_PREC_AUTO || precision == RAVE_PREC_F32_TUNED;
     m->hop = cfg.n_band;
     for (int i = 0; i < cfg.n_ratios; ++i) m->hop *= cfg.ratios[i];
     m->dec_in = cfg.latent_size + cfg.speaker_size;

@@ -45,7 +45,8 @@ class RAVE:
 
     ``precision``: "f32" (exact fp32 MFMA), "split16" (split-f16 GEMMs), or
     "auto" (per op the faster of the two, with every launch configuration,
-    fused unit and residual stack timed at plan build).  ``tuning`` replays the
+    fused unit and residual stack timed at plan build), or "f32_tuned" (exact
+    fp32 on every op, launch configurations and fused units timed as in auto).  ``tuning`` replays the
     choices of an earlier model's ``tuning()`` without timing runs."""
 
     def __init__(self, cfg: RaveConfig, params: Mapping[str, np.ndarray], speaker: np.ndarray,
@@ -53,8 +54,8 @@ class RAVE:
                  adain_stats: Optional[Mapping] = None, fuse_units: bool = True,
                  precision: str = "f32", tuning: Optional[list] = None):
         check_params(cfg, params)
-        if precision not in list(N.PRECISION) + ["auto"]:
-            raise ValueError(f"precision must be one of {sorted(N.PRECISION) + ['auto']}")
+        if precision not in list(N.PRECISION) + ["auto", "f32_tuned"]:
+            raise ValueError(f"precision must be one of {sorted(N.PRECISION) + ['auto', 'f32_tuned']}")
         self.precision = precision
         self.cfg = cfg
         self.graph = build_graph(cfg)          # reference names (AdaIN modules, tests)
@@ -77,7 +78,8 @@ class RAVE:
             keep.append(a)
             plist.append(N.Param(name.encode(), a.ctypes.data, a.size))
         parr = (N.Param * len(plist))(*plist)
-        prec = N.PREC_AUTO if precision == "auto" else N.PRECISION[precision]
+        prec = {"auto": N.PREC_AUTO, "f32_tuned": N.PREC_F32_TUNED}.get(precision) \
+            if precision in ("auto", "f32_tuned") else N.PRECISION[precision]
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             N.check(N.lib.rave_model_create(C.byref(ccfg), parr, len(plist), spk.ctypes.data, prec, C.byref(h)),

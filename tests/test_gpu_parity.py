@@ -279,9 +279,11 @@ def _model(cfg, g, dev, golden, precision="f32"):
 
 
 PRECISIONS = ["f32", "split16", "auto"]
+# model-level modes: + exact fp32 with autotuned launch choices (bench.py's f32_exact pass)
+MODEL_PRECISIONS = PRECISIONS + ["f32_tuned"]
 
 
-@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("precision", MODEL_PRECISIONS)
 @pytest.mark.parametrize("name", ["v2", "causal", "discrete"])
 def test_model_golden(dev, golden, name, precision):
     from rave_amd import config as rcfg
@@ -352,7 +354,7 @@ def test_rvq_kernels_golden(dev, golden, N):
 
 
 # ------------------------------------------------------------------ larger sizes vs oracle
-@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("precision", MODEL_PRECISIONS)
 def test_v2_full_clip_vs_oracle(dev, precision):
     """One 65536-sample clip (BASELINE config 1 size) against the oracle."""
     from oracle.rave_oracle import Oracle
