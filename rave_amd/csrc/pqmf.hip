@@ -258,7 +258,10 @@ __global__ __launch_bounds__(64 * kPqWaves) void pqmf_synthesis_kernel(rave_pqmf
 // A wave owns kPsBlk blocks of 16 frames; a workgroup kPsWaves waves.
 typedef _Float16 ps_h8 __attribute__((ext_vector_type(8)));
 typedef float ps_f32x8 __attribute__((ext_vector_type(8)));
-constexpr int kPsWaves = 4;
+#ifndef RAVE_PS_WAVES
+#define RAVE_PS_WAVES 4
+#endif
+constexpr int kPsWaves = RAVE_PS_WAVES;
 #ifndef RAVE_PS_BLK
 #define RAVE_PS_BLK 2                   // measured (profiles/r02_xcd/ab_pqmf_blk.txt): 2 beats 4 and 1
 #endif
