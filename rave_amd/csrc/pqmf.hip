@@ -267,11 +267,22 @@ constexpr int kPsWaves = RAVE_PS_WAVES;
 #endif
 constexpr int kPsBlk = RAVE_PS_BLK;                         // 16-frame blocks per wave
 constexpr int kPsFrames = kPsWaves * kPsBlk * 16;            // frames per workgroup (128)
+// analysis: the same 128 frames per workgroup as 8 waves of one 16-frame block
+// (12.9 -> 11.0 us against 4 waves of two, profiles/r02_xcd/ab_pqmf_waves.txt;
+// synthesis keeps 4 x 2, which 8 x 1 slows)
+#ifndef RAVE_PA_WAVES
+#define RAVE_PA_WAVES 8
+#endif
+constexpr int kPaWaves = RAVE_PA_WAVES;
+constexpr int kPaBlk = kPsFrames / (16 * kPaWaves);
+constexpr int kPaFrames = kPaWaves * kPaBlk * 16;
+static_assert(kPaFrames == kPsFrames && kPaBlk >= 1, "analysis geometry");
 constexpr int kPsK = 17;                                     // 32-deep K-steps (<= 544 taps / K rows)
 constexpr int kPsKP = 552;                                   // halves per filter row: 1104 B = 20 banks mod 64
 
 // power-of-two scale 2^e with max |v 2^e| in [8, 16) over the workgroup's values
 // (wave max via LDS; `red` holds kPsWaves floats)
+template <int W>
 __device__ __forceinline__ float ps_scale(float amax, float* red) {
     for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -279,7 +290,7 @@ __device__ __forceinline__ float ps_scale(float amax, float* red) {
     __syncthreads();
     float m = red[0];
 #pragma unroll
-    for (int w = 1; w < kPsWaves; ++w) m = fmaxf(m, red[w]);
+    for (int w = 1; w < W; ++w) m = fmaxf(m, red[w]);
     if (!(m > 0.f)) return 1.f;
     int e;
     (void)frexpf(m, &e);                  // m in [2^(e-1), 2^e)
@@ -296,7 +307,7 @@ __device__ __forceinline__ void ps_split(float v, _Float16& hi, _Float16& lo) {
 // 128 samples: the 16 frames of a read land on 16 distinct bank quads)
 __host__ __device__ constexpr int ps_xi(int i) { return i + 8 * (i >> 7); }
 template <int NBO>
-__global__ __launch_bounds__(64 * kPsWaves) void pqmf_analysis_split_kernel(rave_pqmf_analysis_args a, int wframes) {
+__global__ __launch_bounds__(64 * kPaWaves) void pqmf_analysis_split_kernel(rave_pqmf_analysis_args a, int wframes) {
     extern __shared__ __attribute__((aligned(16))) char ps_smem[];
     _Float16* fh = reinterpret_cast<_Float16*>(ps_smem);     // [16][kPsKP]
     _Float16* fl = fh + 16 * kPsKP;
@@ -304,12 +315,12 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_analysis_split_kernel(rave
     const int WS = ps_xi(wframes * 16) + 8;
     _Float16* xl = xh + WS;
     float* red = reinterpret_cast<float*>(xl + WS);
-    constexpr int NT = 64 * kPsWaves;
+    constexpr int NT = 64 * kPaWaves;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int lg_ = __builtin_amdgcn_readfirstlane(
         xcd_major(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y));
     const int b = lg_ / gridDim.x;
-    const int t0 = (lg_ - b * gridDim.x) * kPsFrames;
+    const int t0 = (lg_ - b * gridDim.x) * kPaFrames;
     const float* xb = a.x + (int64_t)b * a.x_sb;
     // filter: rows < NBO, taps < a.taps (all loads before the first LDS store)
     constexpr int KW = 32 * kPsK;                             // 544
@@ -325,7 +336,7 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_analysis_split_kernel(rave
         amax = fmaxf(amax, fabsf(hv[it]));
     }
     const int s0 = t0 * 16 - a.pad_left;
-    constexpr int XT = ((kPsFrames + 40) * 16 + NT - 1) / NT;
+    constexpr int XT = ((kPaFrames + 40) * 16 + NT - 1) / NT;
     float xv[XT];
 #pragma unroll
     for (int it = 0; it < XT; ++it) {
@@ -334,7 +345,7 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_analysis_split_kernel(rave
         const float v = xb[min(max(t, 0), a.t_in - 1)];
         xv[it] = (i < wframes * 16 && t >= 0 && t < a.t_in) ? v : 0.f;
     }
-    const float sc = ps_scale(amax, red);
+    const float sc = ps_scale<kPaWaves>(amax, red);
     for (int i = tid; i < (16 - NBO) * kPsKP; i += NT) {
         fh[NBO * kPsKP + i] = (_Float16)0.f;
         fl[NBO * kPsKP + i] = (_Float16)0.f;
@@ -354,10 +365,10 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_analysis_split_kernel(rave
     }
     __syncthreads();
     const int g = lane >> 4, col = lane & 15;
-    const int fb = wave * kPsBlk * 16;
-    pq_f32x4 acc[kPsBlk];
+    const int fb = wave * kPaBlk * 16;
+    pq_f32x4 acc[kPaBlk];
 #pragma unroll
-    for (int q = 0; q < kPsBlk; ++q) acc[q] = pq_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < kPaBlk; ++q) acc[q] = pq_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < kPsK; ++s) {
         const int ka = col * kPsKP + 32 * s + 8 * g;
@@ -365,7 +376,7 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_analysis_split_kernel(rave
         const ps_h8 al = *reinterpret_cast<const ps_h8*>(fl + ka);
         const ps_h8 a2 = ah * (_Float16)2048.0f;
 #pragma unroll
-        for (int q = 0; q < kPsBlk; ++q) {
+        for (int q = 0; q < kPaBlk; ++q) {
             const int xi = ps_xi(16 * (fb + 16 * q + col) + 32 * s + 8 * g);
             const ps_h8 bh = *reinterpret_cast<const ps_h8*>(xh + xi);
             const ps_h8 bl = *reinterpret_cast<const ps_h8*>(xl + xi);
@@ -377,7 +388,7 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_analysis_split_kernel(rave
     const float unscale = 1.0f / (sc * 2048.0f);              // exact: powers of two
     float* yb = a.y + (int64_t)b * a.y_sb;
 #pragma unroll
-    for (int q = 0; q < kPsBlk; ++q) {
+    for (int q = 0; q < kPaBlk; ++q) {
         const int t = t0 + fb + q * 16 + col;
         if (t >= a.t_out) continue;
 #pragma unroll
@@ -442,7 +453,7 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_synthesis_split_kernel(rav
         av[it] = xb[(int64_t)(a.mode == 1 ? cc + 16 : cc) * a.x_sc + ff];
         nv[it] = nzb ? nzb[(int64_t)cc * a.n_sc + ff] : 0.f;
     }
-    const float sc = ps_scale(amax, red);
+    const float sc = ps_scale<kPsWaves>(amax, red);
 #pragma unroll
     for (int it = 0; it < HT; ++it) {
         const int i = tid + it * NT;
@@ -530,12 +541,12 @@ extern "C" int rave_pqmf_analysis(const rave_pqmf_analysis_args* p, void* stream
     if (a.precision == RAVE_PREC_SPLIT16) {
         const int wframes = kPsFrames + (32 * kPsK + 15) / 16 + 1;
         const int ws = ps_xi(wframes * 16) + 8;
-        const size_t lds = (size_t)(2 * 16 * kPsKP + 2 * ws) * 2 + kPsWaves * 4;
-        dim3 grid(ceil_div(a.t_out, kPsFrames), a.batch);
+        const size_t lds = (size_t)(2 * 16 * kPsKP + 2 * ws) * 2 + kPaWaves * 4;
+        dim3 grid(ceil_div(a.t_out, kPaFrames), a.batch);
         if (a.n_out_bands == 6)
-            launch(pqmf_analysis_split_kernel<6>, grid, dim3(64 * kPsWaves), lds, as_stream(stream), a, wframes);
+            launch(pqmf_analysis_split_kernel<6>, grid, dim3(64 * kPaWaves), lds, as_stream(stream), a, wframes);
         else
-            launch(pqmf_analysis_split_kernel<16>, grid, dim3(64 * kPsWaves), lds, as_stream(stream), a, wframes);
+            launch(pqmf_analysis_split_kernel<16>, grid, dim3(64 * kPaWaves), lds, as_stream(stream), a, wframes);
         return launch_status("pqmf_analysis_split_kernel");
     }
     const int wframes = kPqFrames + (4 * kAnaSteps + 15) / 16 + 1;
