@@ -332,9 +332,56 @@ def run_mode(a, cfg, params, spk, precision, x, dev, world, rank, log_ops):
     return res, y
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``--gpus N`` without a torch.distributed environment: start N rank
+    processes (one per GPU) under torch.distributed.run on 127.0.0.1 as a CHILD
+    process -- this parent never touches the GPU and never execs -- and return
+    its exit code.  Rank 0's JSON line reaches stdout unchanged."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    log(f"bench: launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(a, world: int, rank: int) -> None:
+    """``--dry-run``: the launcher and rank bookkeeping without a GPU -- gloo
+    process group, barrier, max-over-ranks of a dummy timing -- and the same
+    rank-0 JSON line skeleton (tests/test_bench_launcher.py)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+        t = torch.tensor([float(rank)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        seen = dist.get_world_size()
+    else:
+        seen = 1
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "samples/s", "n_gpus": a.gpus,
+                          "ranks_seen": seen, "steps": a.steps, "warmup": a.warmup, "dry_run": True}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment bench.py launches them")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: exercise the launcher / process group on gloo and print a skeleton line")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
@@ -356,13 +403,26 @@ def main():
                     help="also time this many independent steps in flight on as many streams (N=1 only; "
                          "reported as 'pipelined' beside the headline; 1 = off)")
     a = ap.parse_args()
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ:
+        if a.gpus > 1:
+            sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != a.gpus:
+            log(f"bench: WORLD_SIZE={world} but --gpus {a.gpus}; refusing to report a mislabelled run")
+            sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dry_run:
+        dry_run(a, world, rank)
+        return
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
@@ -393,6 +453,7 @@ def main():
     if rank == 0:
         out = {
             "metric": METRIC, "value": head["value"], "unit": "samples/s", "n_gpus": world,
+            "ranks_seen": dist.get_world_size() if world > 1 else 1,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": head["ms_per_step"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": head["dtype"],

@@ -9,8 +9,11 @@ full batch's ``encode`` output (B_global, C, T/hop) available on every rank;
 each rank then decodes its own shard, so audio is never gathered.
 
 The collective is latency-bound at these sizes (C2: 164 KB per rank), a single
-``all_gather_into_tensor`` per step.  With the gloo backend (CPU tests) the
-list form of all_gather is used.
+``all_gather_into_tensor`` per step.  Every backend runs the same code: RCCL
+(backend "nccl") on the GPU box and gloo in the CPU tests take the same
+``all_gather_into_tensor`` calls on the same dtypes (RVQ codes narrowed to
+int16 and carried as bytes), so the world-2 gloo tests exercise the RCCL path's
+logic.
 """
 from __future__ import annotations
 
@@ -43,11 +46,7 @@ def gather_latents(z_local: torch.Tensor, out: Optional[torch.Tensor] = None,
     if out is None:
         out = torch.empty((size * z_local.shape[0],) + tuple(z_local.shape[1:]),
                           dtype=z_local.dtype, device=z_local.device)
-    if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, z_local, group=group)
-    else:
-        parts = list(out.chunk(size, 0))
-        dist.all_gather(parts, z_local, group=group)
+    dist.all_gather_into_tensor(out, z_local, group=group)
     return out
 
 
@@ -84,8 +83,7 @@ class ShardedRunner:
 
     def _narrow_codes(self) -> bool:
         rvq = getattr(getattr(self.model, "cfg", None), "rvq", None)
-        return (self.mode == "codes" and rvq is not None and rvq.codebook_size <= 32767
-                and dist.get_backend(self.group) == "nccl")
+        return self.mode == "codes" and rvq is not None and rvq.codebook_size <= 32767
 
     def sizes(self, b: int, device) -> List[int]:
         """Every rank's shard size."""
@@ -100,10 +98,7 @@ class ShardedRunner:
         dev = device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
         mine = torch.tensor([b], dtype=torch.int64, device=dev)
         out = torch.empty(size, dtype=torch.int64, device=dev)
-        if dist.get_backend(self.group) == "nccl":
-            dist.all_gather_into_tensor(out, mine, group=self.group)
-        else:
-            dist.all_gather(list(out.chunk(size)), mine, group=self.group)
+        dist.all_gather_into_tensor(out, mine, group=self.group)
         return [int(v) for v in out.tolist()]
 
     def _gather(self, t: torch.Tensor, sizes: List[int]) -> torch.Tensor:
@@ -111,7 +106,9 @@ class ShardedRunner:
         if size == 1:
             return t
         narrow = self._narrow_codes()
-        src = t.to(torch.int16) if narrow else t
+        # codes travel as int16 (1024-entry codebooks), viewed as bytes: every
+        # backend moves uint8 (gloo has no int16 collectives)
+        src = t.to(torch.int16).view(torch.uint8) if narrow else t
         bmax = max(sizes)
         if src.shape[0] < bmax:                  # unequal shards travel padded to the largest
             pad = torch.zeros((bmax - src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
@@ -122,7 +119,7 @@ class ShardedRunner:
         out = gather_latents(src, self._all, self.group)
         if any(n != bmax for n in sizes):
             out = torch.cat([out[r * bmax:r * bmax + n] for r, n in enumerate(sizes)], 0)
-        return out.to(t.dtype) if narrow else out
+        return out.view(torch.int16).to(t.dtype) if narrow else out
 
     def step(self, x_local: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """(what every rank holds after the exchange, this rank's decoded audio)."""

@@ -90,18 +90,22 @@ def _run_world2(x_all, mode, fixed_sizes=False):
     return sorted(res, key=lambda t: t[0])
 
 
-def test_sharded_codes_gather_matches_single_process():
-    """C4's path: encode_codes per shard -> all-gather of the RVQ indices ->
-    decode_codes of the local rows; every rank holds the batch's indices."""
+@pytest.mark.parametrize("n", [4, 3])
+def test_sharded_codes_gather_matches_single_process(n):
+    """C4's path: encode_codes per shard -> all-gather of the RVQ indices (as
+    int16 bytes, the RCCL path's own code) -> decode_codes of the local rows;
+    every rank holds the batch's indices.  n=3: unequal shards travel padded."""
+    from rave_amd.distributed import shard_bounds
     rng = np.random.default_rng(1)
-    x_all = torch.from_numpy((0.2 * rng.standard_normal((4, 1, 2048))).astype(np.float32))
+    x_all = torch.from_numpy((0.2 * rng.standard_normal((n, 1, 2048))).astype(np.float32))
     m = _OracleCodesModel()
     idx_ref = m.encode_codes(x_all)
     y_ref = m.decode_codes(idx_ref)
     for rank, idx_all, y in _run_world2(x_all, "codes"):
+        lo, hi = shard_bounds(n, rank, 2)
         assert idx_all.dtype == np.int64
         np.testing.assert_array_equal(idx_all, idx_ref.numpy())
-        np.testing.assert_allclose(y, y_ref.numpy()[rank * 2:(rank + 1) * 2], atol=1e-6)
+        np.testing.assert_allclose(y, y_ref.numpy()[lo:hi], atol=1e-6)
 
 
 def test_sharded_decode_mode_has_no_exchange():
