@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 10
+#define RAVE_ABI_VERSION 11
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 
@@ -576,9 +576,11 @@ int rave_model_decode_codes(rave_model* m, const int64_t* idx, int batch, int fr
 int rave_model_noise_shape(const rave_model* m, int batch, int frames, int64_t* out4);
 
 /* AdaIN (rave/blocks.py:856-919; nn~ learn/reset attributes, scripts/export.py:
- * 248-265).  learn_x / learn_y: -1 keeps, 0/1 sets; reset_*: nonzero resets.
- * row0: first buffer row this process's batch uses (data-parallel shards). */
-int rave_model_adain_control(rave_model* m, int learn_x, int learn_y, int reset_x, int reset_y);
+ * 248-265).  learn_x / learn_y: -1 keeps, 0/1 sets; reset_*: nonzero resets
+ * (asynchronous on `stream`, after the work already queued there).
+ * row0: first buffer row this process's batch uses (data-parallel shards);
+ * existing streams pick a new row0 up at their next block. */
+int rave_model_adain_control(rave_model* m, int learn_x, int learn_y, int reset_x, int reset_y, void* stream);
 int rave_model_set_row0(rave_model* m, int row0);
 /* Replace the constant speaker embedding the encode / decode_codes paths
  * concatenate (speaker_size floats, host or device memory) -- the nn~
@@ -613,18 +615,29 @@ int rave_model_op_times(rave_model* m, int which, int batch, int t, float* ms, i
 
 /* ---------------------------------------------------------------- streaming
  * cached_conv's streaming mode (cc.use_cached_conv(True), scripts/export.py:
- * 543) for a causal model: per-call blocks of `block` samples (a multiple of
- * hop) with persistent per-layer caches (zeroed at creation and by reset).
- * Decoded audio lags one-shot causal decoding by rave_stream_delay samples;
- * the encoder is exact.  AdaIN statistics are per block, as the reference
- * computes them per call.  RAVE_STREAM_GRAPH: each block replays a captured
- * hipGraph (inputs and outputs pass through stream-owned staging buffers). */
-enum { RAVE_STREAM_GRAPH = 1 };
+ * 543, any padding mode): per-call blocks of `block` samples (a multiple of
+ * hop) with persistent per-layer caches (zeroed at creation and by reset),
+ * each conv in its cached form (CachedConv1d / CachedConvTranspose1d,
+ * Residual's AlignBranches delays).  Decoded audio lags one-shot decoding by
+ * rave_stream_delay samples (928 for v2 causal, 13280 for v2 centred); a
+ * causal encoder is exact.  AdaIN statistics are per block, as the reference
+ * computes them per call.
+ * RAVE_STREAM_GRAPH: each block replays a captured hipGraph (inputs and
+ * outputs pass through stream-owned staging buffers).
+ * RAVE_STREAM_ENCODE_ONLY / _DECODE_ONLY: build one direction only (half the
+ * plans, workspaces and graphs).
+ * Discrete configs stream indices (DiscreteScriptedRAVE, scripts/export.py:
+ * 503-517): rave_stream_encode_codes -> (B, n_q, block / hop) int64,
+ * rave_stream_decode_codes clamps them to the codebook; the float entry
+ * points refuse such a stream, and the _codes ones any other. */
+enum { RAVE_STREAM_GRAPH = 1, RAVE_STREAM_ENCODE_ONLY = 2, RAVE_STREAM_DECODE_ONLY = 4 };
 int rave_stream_create(rave_model* m, int batch, int block, int flags, rave_stream** out);
 int rave_stream_destroy(rave_stream* s);
 int rave_stream_reset(rave_stream* s, void* stream);
 int rave_stream_encode(rave_stream* s, const float* x, float* z, void* stream);
 int rave_stream_decode(rave_stream* s, const float* z, float* y, const float* noise_u, void* stream);
+int rave_stream_encode_codes(rave_stream* s, const float* x, int64_t* idx, void* stream);
+int rave_stream_decode_codes(rave_stream* s, const int64_t* idx, float* y, const float* noise_u, void* stream);
 int rave_stream_delay(const rave_stream* s);
 
 #ifdef __cplusplus

@@ -39,7 +39,7 @@ OP_NOISE = 9
 OP_ADAIN = 10
 OP_UNIT = 11
 OP_STACK = 12
-ABI_VERSION = 10
+ABI_VERSION = 11
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 
 # GEMM arithmetic of conv / unit ops (include/rave_amd.h RAVE_PREC_*)
@@ -49,6 +49,8 @@ PREC_AUTO = 2
 PREC_F32_TUNED = 3      # exact fp32, launch choices autotuned (RAVE_PREC_F32_TUNED)
 PRECISION = {"f32": PREC_F32, "split16": PREC_SPLIT16}
 STREAM_GRAPH = 1
+STREAM_ENCODE_ONLY = 2
+STREAM_DECODE_ONLY = 4
 
 i32, i64, f32, vp = C.c_int32, C.c_int64, C.c_float, C.c_void_p
 
@@ -234,7 +236,8 @@ EXPORTS = [
     "rave_model_adain_count", "rave_model_adain_info", "rave_model_adain_get", "rave_model_adain_set",
     "rave_model_tuning_get", "rave_model_tuning_set", "rave_model_plan_ops", "rave_model_profile",
     "rave_model_op_times", "rave_stream_create", "rave_stream_destroy", "rave_stream_reset",
-    "rave_stream_encode", "rave_stream_decode", "rave_stream_delay",
+    "rave_stream_encode", "rave_stream_decode", "rave_stream_encode_codes", "rave_stream_decode_codes",
+    "rave_stream_delay",
     "rave_fir", "rave_row_stats", "rave_attn_pool", "rave_linear", "rave_maxpool",
 ]
 
@@ -300,7 +303,7 @@ def _load():
     lib.rave_model_encode_codes.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp]
     lib.rave_model_decode_codes.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp]
     lib.rave_model_noise_shape.argtypes = [vp, C.c_int, C.c_int, C.POINTER(i64)]
-    lib.rave_model_adain_control.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int]
+    lib.rave_model_adain_control.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp]
     lib.rave_model_set_row0.argtypes = [vp, C.c_int]
     lib.rave_model_set_speaker.argtypes = [vp, vp, vp]
     lib.rave_model_adain_count.argtypes = [vp]
@@ -318,6 +321,8 @@ def _load():
     lib.rave_stream_reset.argtypes = [vp, vp]
     lib.rave_stream_encode.argtypes = [vp, vp, vp, vp]
     lib.rave_stream_decode.argtypes = [vp, vp, vp, vp, vp]
+    lib.rave_stream_encode_codes.argtypes = [vp, vp, vp, vp]
+    lib.rave_stream_decode_codes.argtypes = [vp, vp, vp, vp, vp]
     lib.rave_stream_delay.argtypes = [vp]
     # ABI self-check
     n = lib.rave_struct_sizes(None, 0)

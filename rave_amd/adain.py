@@ -56,6 +56,11 @@ class AdainState:
         return self._touched or self.learn_x or self.learn_y
 
     # ------------------------------------------------------------ controls
+    def _st(self):
+        """The model device's current stream: resets queue behind the work on it."""
+        import torch
+        return C.c_void_p(torch.cuda.current_stream(self._m.device).cuda_stream)
+
     def set_learn(self, learn_x: bool = None, learn_y: bool = None) -> None:
         if learn_x is not None:
             self.learn_x = bool(learn_x)
@@ -64,15 +69,15 @@ class AdainState:
         if self.learn_x or self.learn_y:
             self._touched = True
         N.check(N.lib.rave_model_adain_control(self._m.handle, -1 if learn_x is None else int(bool(learn_x)),
-                                               -1 if learn_y is None else int(bool(learn_y)), 0, 0), "adain")
+                                               -1 if learn_y is None else int(bool(learn_y)), 0, 0, self._st()), "adain")
 
     def reset_x(self) -> None:
         """AdaptiveInstanceNormalization.reset_x (rave/blocks.py:876-879)."""
-        N.check(N.lib.rave_model_adain_control(self._m.handle, -1, -1, 1, 0), "adain")
+        N.check(N.lib.rave_model_adain_control(self._m.handle, -1, -1, 1, 0, self._st()), "adain")
 
     def reset_y(self) -> None:
         """AdaptiveInstanceNormalization.reset_y (rave/blocks.py:881-884)."""
-        N.check(N.lib.rave_model_adain_control(self._m.handle, -1, -1, 0, 1), "adain")
+        N.check(N.lib.rave_model_adain_control(self._m.handle, -1, -1, 0, 1, self._st()), "adain")
 
     def _get(self, i: int) -> Tuple[np.ndarray, np.ndarray]:
         c = self.modules[i][1]

@@ -103,6 +103,7 @@ void build_graph(const rave_model_config& c, Graph& g) {
         Node b = conv(u + ".3", ch, ch, 1, 1, 1, {0, 0}, mid, dst);
         act_of(u + ".2", b);
         b.residual = src;
+        b.res_delay = (a.pad_r + a.stride_delay()) / a.stride;   // Residual's AlignBranches(delays=[d, 0])
         out.push_back(b);
     };
 
@@ -332,6 +333,7 @@ struct Model {
     // AdaIN buffers (rave/blocks.py:858-868), device
     int max_batch = 64;
     float* ad_stats = nullptr;
+    float* ad_init = nullptr;          // the reset image of ad_stats (mean 0, std 1)
     float* ad_counters = nullptr;
     uint32_t* ad_tickets = nullptr;
     std::vector<int64_t> ad_off;
@@ -400,6 +402,8 @@ struct Model {
     void synthesis_op(Plan& p, int B, int F, const View& x, const View& y, const View* noise, int pad, int frame0,
                       int x_len);
     void fill_speaker(Plan& p, int B, int Fz, const View& z);
+    void rvq_encode_op(Plan& p, int B, int Fz, const View& lat, const View& idx);
+    void rvq_decode_op(Plan& p, int B, int Fz, const View& idx, const View& z);
     Plan& encode_plan(int B, int T, bool codes);
     Plan& decode_plan(int B, int Fz, bool codes);
     Plan& plan_of(int which, int B, int T);
@@ -412,7 +416,7 @@ struct Model {
 
 Model::~Model() {
     plans.clear();
-    for (void* p : {(void*)arena, (void*)ad_stats, (void*)ad_counters, (void*)ad_tickets, (void*)fwd_z, (void*)noise,
+    for (void* p : {(void*)arena, (void*)ad_stats, (void*)ad_init, (void*)ad_counters, (void*)ad_tickets, (void*)fwd_z, (void*)noise,
                     (void*)scratch})
         if (p) (void)hipFree(p);
 }
@@ -1068,6 +1072,56 @@ void Model::fill_speaker(Plan& p, int B, int Fz, const View& z) {
     p.bind(o, A, A.values, &s);
 }
 
+// ResidualVectorQuantization.encode (rave/quantization.py:302-310): latents
+// (B, latent, Fz) at `lat` -> indices (B, n_q, Fz) int64 at `idx`
+void Model::rvq_encode_op(Plan& p, int B, int Fz, const View& lat, const View& idx) {
+    rave_rvq_args r{};
+    r.n_q = cfg.rvq_quantizers;
+    r.codebook_size = cfg.rvq_codebook_size;
+    r.dim = cfg.latent_size;
+    r.batch = B;
+    r.t_len = Fz;
+    r.z_sb = lat.sb;
+    r.z_sc = lat.sc;
+    r.i_sb = (int64_t)cfg.rvq_quantizers * Fz;
+    r.i_sq = Fz;
+    const int64_t nw = rave_rvq_workspace(&r);
+    if (nw < 0) fail(RAVE_ERR_ARG, std::string("rvq_workspace: ") + rave_last_error());
+    View work = ws_view(p.ws.alloc(std::max<int64_t>(nw, 1)), 0, 0);
+    PlanOp& o = p.add(RAVE_OP_RVQ_ENCODE, r, "rvq_encode");
+    rave_rvq_args& R = *reinterpret_cast<rave_rvq_args*>(o.op.u.raw);
+    View cb = arena_view(cb_off);
+    p.bind(o, R, R.codebooks, &cb);
+    p.bind(o, R, R.z, &lat);
+    p.bind(o, R, R.idx, &idx);
+    p.bind(o, R, R.y, nullptr);
+    p.bind(o, R, R.work, &work);
+}
+
+// ResidualVectorQuantization.decode (rave/quantization.py:312-318) with
+// DiscreteScriptedRAVE's clamp (scripts/export.py:507-509): indices at `idx`
+// -> the latent channels of `z`
+void Model::rvq_decode_op(Plan& p, int B, int Fz, const View& idx, const View& z) {
+    rave_rvq_args r{};
+    r.n_q = cfg.rvq_quantizers;
+    r.codebook_size = cfg.rvq_codebook_size;
+    r.dim = cfg.latent_size;
+    r.batch = B;
+    r.t_len = Fz;
+    r.i_sb = (int64_t)cfg.rvq_quantizers * Fz;
+    r.i_sq = Fz;
+    r.y_sb = z.sb;
+    r.y_sc = z.sc;
+    PlanOp& o = p.add(RAVE_OP_RVQ_DECODE, r, "rvq_decode");
+    rave_rvq_args& R = *reinterpret_cast<rave_rvq_args*>(o.op.u.raw);
+    View cb = arena_view(cb_off);
+    p.bind(o, R, R.codebooks, &cb);
+    p.bind(o, R, R.z, nullptr);
+    p.bind(o, R, R.idx, &idx);
+    p.bind(o, R, R.y, &z);
+    p.bind(o, R, R.work, nullptr);
+}
+
 // ------------------------------------------------------------------ plans
 static std::vector<const Node*> ptrs_of(const std::vector<Node>& v) {
     std::vector<const Node*> out;
@@ -1090,27 +1144,7 @@ Plan& Model::encode_plan(int B, int T, bool codes) {
     else lat = io_view(1, (int64_t)(cfg.latent_size + cfg.speaker_size) * Fz, Fz);
     run_stack(p, ptrs_of(g.encoder), B, {{"enc_in", {bands, F}}}, {{"latent", lat}});
     if (codes) {
-        rave_rvq_args r{};
-        r.n_q = cfg.rvq_quantizers;
-        r.codebook_size = cfg.rvq_codebook_size;
-        r.dim = cfg.latent_size;
-        r.batch = B;
-        r.t_len = Fz;
-        r.z_sb = lat.sb;
-        r.z_sc = lat.sc;
-        r.i_sb = (int64_t)cfg.rvq_quantizers * Fz;
-        r.i_sq = Fz;
-        const int64_t nw = rave_rvq_workspace(&r);
-        if (nw < 0) fail(RAVE_ERR_ARG, std::string("rvq_workspace: ") + rave_last_error());
-        View work = ws_view(p.ws.alloc(std::max<int64_t>(nw, 1)), 0, 0);
-        PlanOp& o = p.add(RAVE_OP_RVQ_ENCODE, r, "rvq_encode");
-        rave_rvq_args& R = *reinterpret_cast<rave_rvq_args*>(o.op.u.raw);
-        View cb = arena_view(cb_off), idx = io_view(1, 0, 0);
-        p.bind(o, R, R.codebooks, &cb);
-        p.bind(o, R, R.z, &lat);
-        p.bind(o, R, R.idx, &idx);
-        p.bind(o, R, R.y, nullptr);
-        p.bind(o, R, R.work, &work);
+        rvq_encode_op(p, B, Fz, lat, io_view(1, 0, 0));
     } else {
         fill_speaker(p, B, Fz, lat.at((int64_t)cfg.latent_size * Fz));
     }
@@ -1128,24 +1162,7 @@ Plan& Model::decode_plan(int B, int Fz, bool codes) {
     View z;
     if (codes) {
         z = ws_view(p.ws.alloc((int64_t)B * dec_in * Fz), (int64_t)dec_in * Fz, Fz);
-        rave_rvq_args r{};
-        r.n_q = cfg.rvq_quantizers;
-        r.codebook_size = cfg.rvq_codebook_size;
-        r.dim = cfg.latent_size;
-        r.batch = B;
-        r.t_len = Fz;
-        r.i_sb = (int64_t)cfg.rvq_quantizers * Fz;
-        r.i_sq = Fz;
-        r.y_sb = z.sb;
-        r.y_sc = z.sc;
-        PlanOp& o = p.add(RAVE_OP_RVQ_DECODE, r, "rvq_decode");
-        rave_rvq_args& R = *reinterpret_cast<rave_rvq_args*>(o.op.u.raw);
-        View cb = arena_view(cb_off), idx = io_view(0, 0, 0);
-        p.bind(o, R, R.codebooks, &cb);
-        p.bind(o, R, R.z, nullptr);
-        p.bind(o, R, R.idx, &idx);
-        p.bind(o, R, R.y, &z);
-        p.bind(o, R, R.work, nullptr);
+        rvq_decode_op(p, B, Fz, io_view(0, 0, 0), z);
         fill_speaker(p, B, Fz, z.at((int64_t)cfg.latent_size * Fz));
     } else {
         z = io_view(0, (int64_t)dec_in * Fz, Fz);
@@ -1378,6 +1395,8 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
         const size_t na = m->g.adain_modules.size();
         RAVE_HIP_OR_THROW(hipMalloc(&m->ad_stats, init.size() * 4));
         RAVE_HIP_OR_THROW(hipMemcpy(m->ad_stats, init.data(), init.size() * 4, hipMemcpyHostToDevice));
+        RAVE_HIP_OR_THROW(hipMalloc(&m->ad_init, init.size() * 4));
+        RAVE_HIP_OR_THROW(hipMemcpy(m->ad_init, init.data(), init.size() * 4, hipMemcpyHostToDevice));
         RAVE_HIP_OR_THROW(hipMalloc(&m->ad_counters, na * 2 * 4));
         RAVE_HIP_OR_THROW(hipMemset(m->ad_counters, 0, na * 2 * 4));
         RAVE_HIP_OR_THROW(hipMalloc(&m->ad_tickets, na * 4));
@@ -1458,10 +1477,22 @@ extern "C" int rave_model_destroy(rave_model* m) {
     return RAVE_OK;
 }
 
+// NoiseGeneratorV2 reshapes its amplitudes per noise frame (rave/blocks.py:283-285):
+// the band-rate length must divide by prod(noise ratios), as the reference's
+// reshape requires
+static void check_noise_frames(Model* m, int frames) {
+    if (!m->cfg.noise) return;
+    const int64_t F = (int64_t)frames * m->hop / m->cfg.n_band;
+    if (F % m->noise_target)
+        fail(RAVE_ERR_ARG, "noise synthesizer: " + std::to_string(F) + " band frames do not divide by prod(noise ratios) = " +
+                               std::to_string(m->noise_target));
+}
+
 static void check_len(Model* m, int batch, int t) {
     if (batch <= 0 || t <= 0) fail(RAVE_ERR_ARG, "batch and length must be positive");
     if (t % m->hop) fail(RAVE_ERR_ARG, "T=" + std::to_string(t) + " must be a multiple of " + std::to_string(m->hop) +
                                            " (n_band * prod(ratios))");
+    check_noise_frames(m, t / m->hop);
 }
 
 extern "C" int rave_model_encode(rave_model* h, const float* x, int batch, int t, float* z, void* stream) {
@@ -1479,6 +1510,7 @@ extern "C" int rave_model_decode(rave_model* h, const float* z, int batch, int f
         Model* m = model_of(h);
         if (!z || !y) fail(RAVE_ERR_ARG, "decode: null tensor");
         if (batch <= 0 || frames <= 0) fail(RAVE_ERR_ARG, "batch and frames must be positive");
+        check_noise_frames(m, frames);
         m->run_kind(1, batch, frames, z, y, m->noise_ptr(noise_u, batch, frames, as_stream(stream)),
                     as_stream(stream));
     });
@@ -1521,6 +1553,7 @@ extern "C" int rave_model_decode_codes(rave_model* h, const int64_t* idx, int ba
         if (m->cfg.rvq_quantizers <= 0) fail(RAVE_ERR_ARG, "decode_codes needs a discrete (RVQ) config");
         if (!idx || !y) fail(RAVE_ERR_ARG, "decode_codes: null tensor");
         if (batch <= 0 || frames <= 0) fail(RAVE_ERR_ARG, "batch and frames must be positive");
+        check_noise_frames(m, frames);
         m->run_kind(3, batch, frames, idx, y, m->noise_ptr(noise_u, batch, frames, as_stream(stream)),
                     as_stream(stream));
     });
@@ -1540,26 +1573,29 @@ extern "C" int rave_model_noise_shape(const rave_model* h, int batch, int frames
 }
 
 // ------------------------------------------------------------------ AdaIN controls
-extern "C" int rave_model_adain_control(rave_model* h, int learn_x, int learn_y, int reset_x, int reset_y) {
+extern "C" int rave_model_adain_control(rave_model* h, int learn_x, int learn_y, int reset_x, int reset_y,
+                                        void* stream) {
     return guarded([&] {
         Model* m = model_of(h);
         if (m->ad_index.empty()) return;
         if (learn_x >= 0) m->learn_x = learn_x != 0;
         if (learn_y >= 0) m->learn_y = learn_y != 0;
         if (m->learn_x || m->learn_y) m->touched = true;
+        // resets are ordered on the caller's stream after the learning-mode
+        // kernels already queued there (device-to-device from the reset image)
+        hipStream_t st = as_stream(stream);
         for (size_t i = 0; i < m->g.adain_modules.size() && (reset_x || reset_y); ++i) {
             const int64_t plane = (int64_t)m->max_batch * m->g.adain_modules[i].second;
-            std::vector<float> zeros((size_t)plane, 0.f), ones((size_t)plane, 1.f);
             float* base = m->ad_stats + m->ad_off[i];
+            const float* init = m->ad_init + m->ad_off[i];
             if (reset_x) {   // AdaptiveInstanceNormalization.reset_x (rave/blocks.py:876-879)
-                RAVE_HIP_OR_THROW(hipMemcpy(base, zeros.data(), plane * 4, hipMemcpyHostToDevice));
-                RAVE_HIP_OR_THROW(hipMemcpy(base + plane, ones.data(), plane * 4, hipMemcpyHostToDevice));
-                RAVE_HIP_OR_THROW(hipMemset(m->ad_counters + 2 * i, 0, 4));
+                RAVE_HIP_OR_THROW(hipMemcpyAsync(base, init, 2 * plane * 4, hipMemcpyDeviceToDevice, st));
+                RAVE_HIP_OR_THROW(hipMemsetAsync(m->ad_counters + 2 * i, 0, 4, st));
             }
             if (reset_y) {   // reset_y (rave/blocks.py:881-884)
-                RAVE_HIP_OR_THROW(hipMemcpy(base + 2 * plane, zeros.data(), plane * 4, hipMemcpyHostToDevice));
-                RAVE_HIP_OR_THROW(hipMemcpy(base + 3 * plane, ones.data(), plane * 4, hipMemcpyHostToDevice));
-                RAVE_HIP_OR_THROW(hipMemset(m->ad_counters + 2 * i + 1, 0, 4));
+                RAVE_HIP_OR_THROW(hipMemcpyAsync(base + 2 * plane, init + 2 * plane, 2 * plane * 4,
+                                                 hipMemcpyDeviceToDevice, st));
+                RAVE_HIP_OR_THROW(hipMemsetAsync(m->ad_counters + 2 * i + 1, 0, 4, st));
             }
         }
     });
@@ -1695,25 +1731,40 @@ extern "C" int rave_model_op_times(rave_model* h, int which, int batch, int t, f
     return rc == RAVE_OK ? runs : rc;
 }
 
+
 // =================================================================== streaming
 // cached_conv's streaming mode (third-party cached-conv>=2.5.0, selected by
-// cc.use_cached_conv(True), scripts/export.py:543) restated on the same kernels:
-//   * a causal Conv1d with padding (p-1, 0) keeps the last p-1 samples of its
-//     input (CachedPadding1d): every conv input is a persistent buffer
-//     [history | block]; the conv reads it with zero padding 0 and after the
-//     block the newest `history` columns move to the front (SHIFT_HISTORY).  The
-//     cached values are pre-activation (the activation is the conv prologue;
-//     act(0) = 0 keeps the zero start state identical);
+// cc.use_cached_conv(True), scripts/export.py:543) restated on the same
+// kernels, for causal and centred (non-causal) padding alike:
+//   * CachedConv1d with padding (l, r) prepends a cache of the last l + r
+//     input samples (CachedPadding1d(l + r)) after a stride_delay crop-pad,
+//     then convolves with padding 0: it is a conv over the persistent buffer
+//     [history | block] read from history offset l + r + stride_delay.  Its
+//     output lags the offline (zero-padded) conv by (r + stride_delay) / stride
+//     frames -- 0 in causal mode.  After each block the newest `history`
+//     columns move to the front (one batched SHIFT_HISTORY launch).  Cached
+//     values are pre-activation (the activation is the conv prologue; act(0)
+//     = 0 keeps the zero start state identical);
+//   * Residual = AlignBranches(unit, Identity, delays=[d, 0]) (rave/blocks.py:
+//     32-46): the identity branch is delayed by the unit's cumulative delay d
+//     (its k3 conv's r), i.e. the residual add reads the unit's input buffer d
+//     columns back;
 //   * CachedConvTranspose1d (overlap-add of a 2*(r//2) cache) is the polyphase
-//     2-tap conv with one input history column and no output crop;
-//   * CachedPQMF: analysis keeps taps-1 audio samples, synthesis taps-1 frames;
+//     2-tap conv with one input history column and no output crop; it lags by
+//     r//2 output samples in both padding modes;
+//   * CachedPQMF: analysis keeps taps-1 audio samples, synthesis taps-1 frames
+//     (its conv padding (256,256)/(16,16) centred, (512,0)/(32,0) causal: the
+//     same l + r either way);
 //   * NoiseGeneratorV2's convs (padding (r, 0), stride r) keep r samples; its
 //     filter stage is per noise frame, so it streams as is, into a buffer with
-//     the synthesis history so the noise lines up with the waveform bands;
+//     the synthesis history so the noise lines up with the waveform bands as
+//     the reference's per-call tensors do;
 //   * AdaIN runs on the block's columns (its statistics are per call, as the
 //     reference computes them on each streamed chunk), in place, so the history
 //     holds the normalised values the cached conv saw;
-//   * Residual/AlignBranches delays are 0 in causal mode.
+//   * discrete configs (DiscreteScriptedRAVE, scripts/export.py:503-517): the
+//     encoder plan ends with rvq.encode of the block's frames, the decoder plan
+//     starts with rvq.decode (clamped) + the speaker channels.
 namespace rave {
 
 Stream::~Stream() {
@@ -1725,10 +1776,10 @@ Stream::~Stream() {
     if (stage) (void)hipFree(stage);
 }
 
+// history columns the cached form of a conv reads before the block
 static int stream_need(const Node& n) {
     if (n.transposed) return 1;
-    if (n.pad_r != 0) fail(RAVE_ERR_ARG, n.name + ": streaming needs causal padding");
-    return n.pad_l;
+    return n.pad_l + n.pad_r + n.stride_delay();
 }
 
 static void tensor_sizes(const std::vector<const Node*>& nodes, std::map<std::string, std::pair<int, int>>& sizes) {
@@ -1741,7 +1792,10 @@ static void tensor_sizes(const std::vector<const Node*>& nodes, std::map<std::st
 static std::map<std::string, StreamBuf> stream_buffers(Plan& p, const std::vector<const Node*>& nodes, int B,
                                                        const std::map<std::string, std::pair<int, int>>& sizes,
                                                        std::map<std::string, int> need) {
-    for (const Node* n : nodes) need[n->src] = std::max(need[n->src], stream_need(*n));
+    for (const Node* n : nodes) {
+        need[n->src] = std::max(need[n->src], stream_need(*n));
+        if (!n->residual.empty()) need[n->residual] = std::max(need[n->residual], n->res_delay);
+    }
     std::map<std::string, StreamBuf> bufs;
     for (auto& kv : sizes) {
         StreamBuf b;
@@ -1760,6 +1814,7 @@ static void conv_stream(Model* m, Plan& p, const Node& n, int B, std::map<std::s
     const StreamBuf& src = bufs.at(n.src);
     const StreamBuf& dst = bufs.at(n.dst);
     const int need = stream_need(n);
+    const int sd = n.stride_delay();
     if (!n.adain.empty() && !m->ad_index.empty()) {
         adain_ops.push_back((int)p.ops.size());
         m->adain_op(p, n.adain, B, n.c_in, src.t, src.v.at(src.h));
@@ -1768,7 +1823,10 @@ static void conv_stream(Model* m, Plan& p, const Node& n, int B, std::map<std::s
     const View y = dst.v.p.kind == PRef::WS ? dst.v.at(dst.h) : dst.v;
     View res;
     const bool has_res = !n.residual.empty();
-    if (has_res) res = bufs.at(n.residual).v.at(bufs.at(n.residual).h);
+    if (has_res) {
+        const StreamBuf& rb = bufs.at(n.residual);
+        res = rb.v.at(rb.h - n.res_delay);    // AlignBranches: the identity branch, delayed
+    }
     rave_conv1d_args a{};
     a.c_in = n.c_in;
     a.c_out = n.c_out;
@@ -1781,7 +1839,7 @@ static void conv_stream(Model* m, Plan& p, const Node& n, int B, std::map<std::s
     a.act = n.act;
     a.leaky_slope = m->cfg.leaky_slope;
     a.batch = B;
-    a.t_in = need + src.t;
+    a.t_in = need - sd + src.t;       // [cache l+r | block delayed by sd]
     a.t_out = dst.t;
     a.x_sb = x.sb;
     a.x_sc = x.sc;
@@ -1848,12 +1906,25 @@ static void copy_op(Plan& p, int B, int C, int T, const View& x, const View& y) 
     p.bind(o, A, A.y, &y);
 }
 
+// Samples by which the streamed decoder lags one-shot decoding: each cached
+// conv adds (r + stride_delay) / stride frames at its output rate, each cached
+// ConvTranspose1d multiplies the lag by its stride and adds r//2, the PQMF
+// inverse conv adds its right padding (16 centred, 0 causal) in band frames.
+static int decode_delay(const Model* m) {
+    std::map<std::string, int> d{{"dec_in", 0}};
+    for (const Node& n : m->g.decoder) {
+        const int in = d.at(n.src);
+        d[n.dst] = n.transposed ? in * n.stride + n.stride / 2 : (in + n.pad_r + n.stride_delay()) / n.stride;
+    }
+    return (d.at("wave") + get_padding(m->taps_s, 1, m->cfg.causal != 0).second) * m->cfg.n_band;
+}
+
 static void build_stream(Stream& s) {
     Model* m = s.m;
     const rave_model_config& cfg = m->cfg;
     const int B = s.B;
     // ------------------------------------------------------------ encoder
-    {
+    if (!(s.flags & RAVE_STREAM_DECODE_ONLY)) {
         s.enc = std::make_unique<Plan>();
         Plan& p = *s.enc;
         std::vector<const Node*> nodes = ptrs_of(m->g.encoder);
@@ -1864,7 +1935,8 @@ static void build_stream(Stream& s) {
         s.enc_bufs = stream_buffers(p, nodes, B, sizes, {{"audio", ha}});
         const int zc = cfg.latent_size + cfg.speaker_size;
         StreamBuf lat;
-        lat.v = io_view(1, (int64_t)zc * s.Fz, s.Fz);
+        lat.v = s.codes ? ws_view(p.ws.alloc((int64_t)B * cfg.latent_size * s.Fz), (int64_t)cfg.latent_size * s.Fz, s.Fz)
+                        : io_view(1, (int64_t)zc * s.Fz, s.Fz);
         lat.c = cfg.latent_size;
         lat.t = s.Fz;
         s.enc_bufs["latent"] = lat;
@@ -1873,12 +1945,13 @@ static void build_stream(Stream& s) {
         const StreamBuf& e = s.enc_bufs.at("enc_in");
         m->analysis_op(p, B, s.block, a.v, e.v.at(e.h), cfg.enc_bands, 0, ha + s.block);
         for (const Node* n : nodes) conv_stream(m, p, *n, B, s.enc_bufs, s.enc_adain);
-        m->fill_speaker(p, B, s.Fz, io_view(1, (int64_t)zc * s.Fz, s.Fz).at((int64_t)cfg.latent_size * s.Fz));
+        if (s.codes) m->rvq_encode_op(p, B, s.Fz, lat.v, io_view(1, 0, 0));
+        else m->fill_speaker(p, B, s.Fz, io_view(1, (int64_t)zc * s.Fz, s.Fz).at((int64_t)cfg.latent_size * s.Fz));
         shift_all(p, B, s.enc_bufs);
         p.finalize(m->arena);
     }
     // ------------------------------------------------------------ decoder (+ noise synthesizer)
-    {
+    if (!(s.flags & RAVE_STREAM_ENCODE_ONLY)) {
         s.dec = std::make_unique<Plan>();
         Plan& p = *s.dec;
         std::vector<const Node*> nodes = ptrs_of(m->g.decoder);
@@ -1893,7 +1966,12 @@ static void build_stream(Stream& s) {
         }
         s.dec_bufs = stream_buffers(p, nodes, B, sizes, need);
         const StreamBuf& z = s.dec_bufs.at("dec_in");
-        copy_op(p, B, m->dec_in, s.Fz, io_view(0, (int64_t)m->dec_in * s.Fz, s.Fz), z.v.at(z.h));
+        if (s.codes) {
+            m->rvq_decode_op(p, B, s.Fz, io_view(0, 0, 0), z.v.at(z.h));
+            m->fill_speaker(p, B, s.Fz, z.v.at(z.h).at((int64_t)cfg.latent_size * z.v.sc));
+        } else {
+            copy_op(p, B, m->dec_in, s.Fz, io_view(0, (int64_t)m->dec_in * s.Fz, s.Fz), z.v.at(z.h));
+        }
         for (const Node* n : nodes) conv_stream(m, p, *n, B, s.dec_bufs, s.dec_adain);
         const StreamBuf& w = s.dec_bufs.at("wave");
         View noise_v;
@@ -1924,17 +2002,19 @@ static void build_stream(Stream& s) {
         shift_all(p, B, s.dec_bufs);
         p.finalize(m->arena);
     }
-    // decoded audio lags one-shot causal decoding by sum(r//2 * upsampling)
-    s.delay = 0;
-    int up = m->hop;
-    for (int i = cfg.n_ratios - 1; i >= 0; --i) {
-        up /= cfg.ratios[i];
-        s.delay += (cfg.ratios[i] / 2) * up;
-    }
+    s.delay = decode_delay(m);
 }
 
 static int64_t noise_count(const Stream& s) {
     return s.m->cfg.noise ? (int64_t)s.B * (s.F / s.m->noise_target) * s.m->cfg.n_band * s.m->noise_target : 0;
+}
+
+// bytes of one block's encoder output / decoder input: latents (+ speaker) in
+// floats, or int64 RVQ indices for a discrete config
+static int64_t latent_bytes(const Stream& s, bool dec_side) {
+    const rave_model_config& c = s.m->cfg;
+    if (s.codes) return (int64_t)s.B * c.rvq_quantizers * s.Fz * 8;
+    return (int64_t)s.B * (dec_side ? s.m->dec_in : c.latent_size + c.speaker_size) * s.Fz * 4;
 }
 
 static void capture(Stream& s, Plan& p, void* const* slots, int n, hipGraph_t& g, hipGraphExec_t& e) {
@@ -1956,23 +2036,39 @@ static void capture(Stream& s, Plan& p, void* const* slots, int n, hipGraph_t& g
 }
 
 static void recapture(Stream& s) {
-    void* es[2] = {s.x_st, s.z_st};
-    capture(s, *s.enc, es, 2, s.enc_graph, s.enc_exec);
-    void* ds[3] = {s.zi_st, s.y_st, s.u_st ? (void*)s.u_st : (void*)s.y_st};
-    capture(s, *s.dec, ds, 3, s.dec_graph, s.dec_exec);
+    if (s.has_enc()) {
+        void* es[2] = {s.x_st, s.z_st};
+        capture(s, *s.enc, es, 2, s.enc_graph, s.enc_exec);
+    }
+    if (s.has_dec()) {
+        void* ds[3] = {s.zi_st, s.y_st, s.u_st ? (void*)s.u_st : (void*)s.y_st};
+        capture(s, *s.dec, ds, 3, s.dec_graph, s.dec_exec);
+    }
 }
 
-// AdaIN ops carry the learn mode in their arguments: patch them when the
-// model's flags have changed since the last block (and re-capture graphs)
+// AdaIN ops carry the learn mode and the first buffer row in their arguments:
+// patch them when the model's flags or row0 have changed since the last block
+// (and re-capture the graphs)
 static void sync_adain(Stream& s) {
     Model* m = s.m;
     if (m->ad_index.empty()) return;
     const int mode = m->adain_mode();
-    if (mode == s.ad_mode) return;
-    const int off = (int)offsetof(rave_adain_args, mode);
-    for (int i : s.enc_adain) check_rc(plan_patch(s.enc->handle, i, off, &mode, 4), "plan_patch");
-    for (int i : s.dec_adain) check_rc(plan_patch(s.dec->handle, i, off, &mode, 4), "plan_patch");
+    const int row0 = m->row0;
+    if (mode == s.ad_mode && row0 == s.ad_row0) return;
+    if (row0 + s.B > m->max_batch)
+        fail(RAVE_ERR_ARG, "AdaIN statistics hold " + std::to_string(m->max_batch) + " batch rows; stream batch " +
+                               std::to_string(s.B) + " at row " + std::to_string(row0) + " exceeds them");
+    const int off_mode = (int)offsetof(rave_adain_args, mode);
+    const int off_row0 = (int)offsetof(rave_adain_args, row0);
+    for (auto* pl : {&s.enc, &s.dec}) {
+        if (!*pl) continue;
+        for (int i : (pl == &s.enc ? s.enc_adain : s.dec_adain)) {
+            check_rc(plan_patch((*pl)->handle, i, off_mode, &mode, 4), "plan_patch");
+            check_rc(plan_patch((*pl)->handle, i, off_row0, &row0, 4), "plan_patch");
+        }
+    }
     s.ad_mode = mode;
+    s.ad_row0 = row0;
     if (s.flags & RAVE_STREAM_GRAPH) recapture(s);
 }
 
@@ -1992,10 +2088,13 @@ extern "C" int rave_stream_create(rave_model* mh, int batch, int block, int flag
         Model* m = model_of(mh);
         if (!out) fail(RAVE_ERR_ARG, "null output");
         *out = nullptr;
-        if (!m->cfg.causal) fail(RAVE_ERR_ARG, "streaming requires a causal config (causal.gin)");
-        if (m->cfg.rvq_quantizers > 0) fail(RAVE_ERR_UNSUPPORTED, "streaming of a discrete config");
+        if (flags & ~(RAVE_STREAM_GRAPH | RAVE_STREAM_ENCODE_ONLY | RAVE_STREAM_DECODE_ONLY))
+            fail(RAVE_ERR_ARG, "unknown stream flags");
+        if ((flags & RAVE_STREAM_ENCODE_ONLY) && (flags & RAVE_STREAM_DECODE_ONLY))
+            fail(RAVE_ERR_ARG, "RAVE_STREAM_ENCODE_ONLY and RAVE_STREAM_DECODE_ONLY exclude each other");
         if (batch <= 0 || block <= 0 || block % m->hop)
             fail(RAVE_ERR_ARG, "block must be a positive multiple of " + std::to_string(m->hop));
+        check_noise_frames(m, block / m->hop);
         if (!m->ad_index.empty() && m->row0 + batch > m->max_batch)
             fail(RAVE_ERR_ARG, "AdaIN statistics hold " + std::to_string(m->max_batch) + " batch rows");
         auto h = std::make_unique<rave_stream>();
@@ -2005,14 +2104,16 @@ extern "C" int rave_stream_create(rave_model* mh, int batch, int block, int flag
         s.B = batch;
         s.block = block;
         s.flags = flags;
+        s.codes = m->cfg.rvq_quantizers > 0;
         s.Fz = block / m->hop;
         s.F = block / m->cfg.n_band;
         s.ad_mode = m->adain_mode();
+        s.ad_row0 = m->row0;
         m->cur_stream = nullptr;
         build_stream(s);
         // staging buffers (graph mode) and the capture stream
-        const int64_t nx = (int64_t)batch * block, nz = (int64_t)batch * (m->cfg.latent_size + m->cfg.speaker_size) * s.Fz,
-                      nzi = (int64_t)batch * m->dec_in * s.Fz, nu = noise_count(s);
+        const int64_t nx = (int64_t)batch * block, nz = (latent_bytes(s, false) + 3) / 4,
+                      nzi = (latent_bytes(s, true) + 3) / 4, nu = noise_count(s);
         const int64_t total = nx + nz + nzi + nx + std::max<int64_t>(nu, 1) + 5 * 64;
         RAVE_HIP_OR_THROW(hipMalloc(&s.stage, (size_t)total * 4));
         RAVE_HIP_OR_THROW(hipMemset(s.stage, 0, (size_t)total * 4));
@@ -2028,15 +2129,39 @@ extern "C" int rave_stream_create(rave_model* mh, int batch, int block, int flag
         s.y_st = take(nx);
         s.u_st = nu > 0 ? take(nu) : nullptr;
         // one warm run of each plan (kernel attributes are set on first launch,
-        // outside any capture), then the zero start state
+        // outside any capture), then the zero start state.  The warm run must
+        // not leave a trace in the model's shared AdaIN statistics (a learning
+        // mode would fold the all-zero staging block into them): they are
+        // saved and restored around it.
         {
-            void* es[2] = {s.x_st, s.z_st};
-            s.enc->run(es, 2, nullptr);
-            void* ds[3] = {s.zi_st, s.y_st, s.u_st ? (void*)s.u_st : (void*)s.y_st};
-            s.dec->run(ds, 3, nullptr);
+            float* ad_save = nullptr;
+            int64_t ad_n = 0;
+            const size_t na = m->g.adain_modules.size();
+            if (na) {
+                for (size_t i = 0; i < na; ++i) ad_n += 4LL * m->max_batch * m->g.adain_modules[i].second;
+                RAVE_HIP_OR_THROW(hipDeviceSynchronize());
+                RAVE_HIP_OR_THROW(hipMalloc(&ad_save, (size_t)(ad_n + 3 * na) * 4));
+                RAVE_HIP_OR_THROW(hipMemcpy(ad_save, m->ad_stats, (size_t)ad_n * 4, hipMemcpyDeviceToDevice));
+                RAVE_HIP_OR_THROW(hipMemcpy(ad_save + ad_n, m->ad_counters, na * 2 * 4, hipMemcpyDeviceToDevice));
+                RAVE_HIP_OR_THROW(hipMemcpy(ad_save + ad_n + 2 * na, m->ad_tickets, na * 4, hipMemcpyDeviceToDevice));
+            }
+            if (s.has_enc()) {
+                void* es[2] = {s.x_st, s.z_st};
+                s.enc->run(es, 2, nullptr);
+            }
+            if (s.has_dec()) {
+                void* ds[3] = {s.zi_st, s.y_st, s.u_st ? (void*)s.u_st : (void*)s.y_st};
+                s.dec->run(ds, 3, nullptr);
+            }
             RAVE_HIP_OR_THROW(hipDeviceSynchronize());
-            RAVE_HIP_OR_THROW(hipMemset(s.enc->ws_dev, 0, (size_t)s.enc->ws_floats * 4));
-            RAVE_HIP_OR_THROW(hipMemset(s.dec->ws_dev, 0, (size_t)s.dec->ws_floats * 4));
+            if (ad_save) {
+                RAVE_HIP_OR_THROW(hipMemcpy(m->ad_stats, ad_save, (size_t)ad_n * 4, hipMemcpyDeviceToDevice));
+                RAVE_HIP_OR_THROW(hipMemcpy(m->ad_counters, ad_save + ad_n, na * 2 * 4, hipMemcpyDeviceToDevice));
+                RAVE_HIP_OR_THROW(hipMemcpy(m->ad_tickets, ad_save + ad_n + 2 * na, na * 4, hipMemcpyDeviceToDevice));
+                RAVE_HIP_OR_THROW(hipFree(ad_save));
+            }
+            if (s.has_enc()) RAVE_HIP_OR_THROW(hipMemset(s.enc->ws_dev, 0, (size_t)s.enc->ws_floats * 4));
+            if (s.has_dec()) RAVE_HIP_OR_THROW(hipMemset(s.dec->ws_dev, 0, (size_t)s.dec->ws_floats * 4));
         }
         if (flags & RAVE_STREAM_GRAPH) {
             RAVE_HIP_OR_THROW(hipStreamCreateWithFlags(&s.cap, hipStreamNonBlocking));
@@ -2054,26 +2179,65 @@ extern "C" int rave_stream_destroy(rave_stream* s) {
 extern "C" int rave_stream_reset(rave_stream* h, void* stream) {
     return guarded([&] {
         Stream* s = stream_of(h);
-        RAVE_HIP_OR_THROW(hipMemsetAsync(s->enc->ws_dev, 0, (size_t)s->enc->ws_floats * 4, as_stream(stream)));
-        RAVE_HIP_OR_THROW(hipMemsetAsync(s->dec->ws_dev, 0, (size_t)s->dec->ws_floats * 4, as_stream(stream)));
+        if (s->has_enc())
+            RAVE_HIP_OR_THROW(hipMemsetAsync(s->enc->ws_dev, 0, (size_t)s->enc->ws_floats * 4, as_stream(stream)));
+        if (s->has_dec())
+            RAVE_HIP_OR_THROW(hipMemsetAsync(s->dec->ws_dev, 0, (size_t)s->dec->ws_floats * 4, as_stream(stream)));
     });
 }
+
+namespace rave {
+// one encoder block: audio (B, 1, block) -> latents or indices (latent_bytes)
+static void stream_enc(Stream* s, const void* x, void* out, hipStream_t st) {
+    if (!s->has_enc()) fail(RAVE_ERR_STATE, "stream was created RAVE_STREAM_DECODE_ONLY");
+    sync_adain(*s);
+    if (s->flags & RAVE_STREAM_GRAPH) {
+        RAVE_HIP_OR_THROW(hipMemcpyAsync(s->x_st, x, (size_t)s->B * s->block * 4, hipMemcpyDeviceToDevice, st));
+        RAVE_HIP_OR_THROW(hipGraphLaunch(s->enc_exec, st));
+        RAVE_HIP_OR_THROW(hipMemcpyAsync(out, s->z_st, (size_t)latent_bytes(*s, false), hipMemcpyDeviceToDevice, st));
+    } else {
+        void* slots[2] = {(void*)x, out};
+        s->enc->run(slots, 2, st);
+    }
+}
+
+// one decoder block: latents or indices -> audio (B, 1, block)
+static void stream_dec(Stream* s, const void* in, float* y, const float* noise_u, hipStream_t st) {
+    if (!s->has_dec()) fail(RAVE_ERR_STATE, "stream was created RAVE_STREAM_ENCODE_ONLY");
+    sync_adain(*s);
+    Model* m = s->m;
+    const int64_t nu = noise_count(*s);
+    const float* u = nullptr;
+    if (nu > 0) {
+        if (noise_u && !(s->flags & RAVE_STREAM_GRAPH)) {
+            u = noise_u;
+        } else if (noise_u) {
+            RAVE_HIP_OR_THROW(hipMemcpyAsync(s->u_st, noise_u, (size_t)nu * 4, hipMemcpyDeviceToDevice, st));
+            u = s->u_st;
+        } else {
+            check_rc(rave_fill_uniform(s->u_st, nu, 0x13198A2E03707344ull + 0x9E3779B97F4A7C15ull * ++m->noise_calls,
+                                       0.f, 1.f, st),
+                     "noise draw");
+            u = s->u_st;
+        }
+    }
+    if (s->flags & RAVE_STREAM_GRAPH) {
+        RAVE_HIP_OR_THROW(hipMemcpyAsync(s->zi_st, in, (size_t)latent_bytes(*s, true), hipMemcpyDeviceToDevice, st));
+        RAVE_HIP_OR_THROW(hipGraphLaunch(s->dec_exec, st));
+        RAVE_HIP_OR_THROW(hipMemcpyAsync(y, s->y_st, (size_t)s->B * s->block * 4, hipMemcpyDeviceToDevice, st));
+    } else {
+        void* slots[3] = {(void*)in, (void*)y, (void*)(u ? u : y)};
+        s->dec->run(slots, 3, st);
+    }
+}
+}  // namespace rave
 
 extern "C" int rave_stream_encode(rave_stream* h, const float* x, float* z, void* stream) {
     return guarded([&] {
         Stream* s = stream_of(h);
         if (!x || !z) fail(RAVE_ERR_ARG, "stream encode: null tensor");
-        sync_adain(*s);
-        hipStream_t st = as_stream(stream);
-        if (s->flags & RAVE_STREAM_GRAPH) {
-            const size_t nz = (size_t)s->B * (s->m->cfg.latent_size + s->m->cfg.speaker_size) * s->Fz * 4;
-            RAVE_HIP_OR_THROW(hipMemcpyAsync(s->x_st, x, (size_t)s->B * s->block * 4, hipMemcpyDeviceToDevice, st));
-            RAVE_HIP_OR_THROW(hipGraphLaunch(s->enc_exec, st));
-            RAVE_HIP_OR_THROW(hipMemcpyAsync(z, s->z_st, nz, hipMemcpyDeviceToDevice, st));
-        } else {
-            void* slots[2] = {(void*)x, (void*)z};
-            s->enc->run(slots, 2, st);
-        }
+        if (s->codes) fail(RAVE_ERR_ARG, "discrete config: stream with rave_stream_encode_codes");
+        stream_enc(s, x, z, as_stream(stream));
     });
 }
 
@@ -2081,38 +2245,27 @@ extern "C" int rave_stream_decode(rave_stream* h, const float* z, float* y, cons
     return guarded([&] {
         Stream* s = stream_of(h);
         if (!z || !y) fail(RAVE_ERR_ARG, "stream decode: null tensor");
-        sync_adain(*s);
-        hipStream_t st = as_stream(stream);
-        Model* m = s->m;
-        const int64_t nu = noise_count(*s);
-        if (s->flags & RAVE_STREAM_GRAPH) {
-            RAVE_HIP_OR_THROW(hipMemcpyAsync(s->zi_st, z, (size_t)s->B * m->dec_in * s->Fz * 4,
-                                             hipMemcpyDeviceToDevice, st));
-            if (nu > 0) {
-                if (noise_u)
-                    RAVE_HIP_OR_THROW(hipMemcpyAsync(s->u_st, noise_u, (size_t)nu * 4, hipMemcpyDeviceToDevice, st));
-                else
-                    check_rc(rave_fill_uniform(s->u_st, nu, 0x13198A2E03707344ull + 0x9E3779B97F4A7C15ull * ++m->noise_calls,
-                                               0.f, 1.f, st),
-                             "noise draw");
-            }
-            RAVE_HIP_OR_THROW(hipGraphLaunch(s->dec_exec, st));
-            RAVE_HIP_OR_THROW(hipMemcpyAsync(y, s->y_st, (size_t)s->B * s->block * 4, hipMemcpyDeviceToDevice, st));
-        } else {
-            const float* u = nullptr;
-            if (nu > 0) {
-                if (noise_u) {
-                    u = noise_u;
-                } else {
-                    check_rc(rave_fill_uniform(s->u_st, nu, 0x13198A2E03707344ull + 0x9E3779B97F4A7C15ull * ++m->noise_calls,
-                                               0.f, 1.f, st),
-                             "noise draw");
-                    u = s->u_st;
-                }
-            }
-            void* slots[3] = {(void*)z, (void*)y, (void*)(u ? u : y)};
-            s->dec->run(slots, 3, st);
-        }
+        if (s->codes) fail(RAVE_ERR_ARG, "discrete config: stream with rave_stream_decode_codes");
+        stream_dec(s, z, y, noise_u, as_stream(stream));
+    });
+}
+
+extern "C" int rave_stream_encode_codes(rave_stream* h, const float* x, int64_t* idx, void* stream) {
+    return guarded([&] {
+        Stream* s = stream_of(h);
+        if (!x || !idx) fail(RAVE_ERR_ARG, "stream encode_codes: null tensor");
+        if (!s->codes) fail(RAVE_ERR_ARG, "encode_codes needs a discrete (RVQ) config");
+        stream_enc(s, x, idx, as_stream(stream));
+    });
+}
+
+extern "C" int rave_stream_decode_codes(rave_stream* h, const int64_t* idx, float* y, const float* noise_u,
+                                        void* stream) {
+    return guarded([&] {
+        Stream* s = stream_of(h);
+        if (!idx || !y) fail(RAVE_ERR_ARG, "stream decode_codes: null tensor");
+        if (!s->codes) fail(RAVE_ERR_ARG, "decode_codes needs a discrete (RVQ) config");
+        stream_dec(s, idx, y, noise_u, as_stream(stream));
     });
 }
 

@@ -48,7 +48,14 @@ struct Node {
     std::string src, dst;       // tensor ids
     std::string residual;       // tensor id added to the output ("" = none)
     std::string adain;          // AdaIN module applied to the input first ("" = none)
+    // cached (streaming) mode: AlignBranches delay of the residual identity
+    // branch (rave/blocks.py:36-41: the unit's cumulative_delay, i.e. its k3
+    // conv's right padding; 0 in causal mode)
+    int res_delay = 0;
     int out_len(int t_in) const;
+    // cached_conv's CachedConv1d crop-pad that makes (r + cd) a multiple of the
+    // stride (cd = 0: no conv of these graphs passes cumulative_delay)
+    int stride_delay() const { return transposed ? 0 : (stride - (pad_r % stride)) % stride; }
 };
 
 struct Graph {
@@ -169,6 +176,7 @@ struct StreamBuf {
 struct Stream {
     Model* m = nullptr;
     int B = 1, block = 0, Fz = 0, F = 0, flags = 0;
+    bool codes = false;                            // discrete config: the plans end / start with RVQ
     std::unique_ptr<Plan> enc, dec;
     std::map<std::string, StreamBuf> enc_bufs, dec_bufs;
     // graph mode: staging buffers and captured executables
@@ -179,6 +187,9 @@ struct Stream {
     hipStream_t cap = nullptr;
     int delay = 0;
     int ad_mode = -1;                              // AdaIN mode baked into the plans
+    int ad_row0 = 0;                               // AdaIN buffer row baked into the plans
+    bool has_enc() const { return enc != nullptr; }
+    bool has_dec() const { return dec != nullptr; }
     std::vector<int> enc_adain, dec_adain;         // AdaIN op indices
     ~Stream();
 };

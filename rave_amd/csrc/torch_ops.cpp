@@ -160,11 +160,13 @@ struct Engine : torch::CustomClassHolder {
         return y;
     }
     // cached_conv streaming (one block of stream_block samples per call)
-    rave_stream* stream_for(rave_stream*& s, int64_t& sb, int64_t batch) {
+    // (one stream object per direction, each built for that direction only)
+    rave_stream* stream_for(rave_stream*& s, int64_t& sb, int64_t batch, int direction) {
         if (!s || sb != batch) {
             if (s) rave_stream_destroy(s);
             s = nullptr;
-            check(rave_stream_create(m, (int)batch, (int)stream_block, RAVE_STREAM_GRAPH, &s), "rave_stream_create");
+            check(rave_stream_create(m, (int)batch, (int)stream_block, RAVE_STREAM_GRAPH | direction, &s),
+                  "rave_stream_create");
             sb = batch;
         }
         return s;
@@ -174,7 +176,7 @@ struct Engine : torch::CustomClassHolder {
         TORCH_CHECK_VALUE(x.dim() == 3 && x.size(1) == 1 && x.size(2) == stream_block, "x must be (B, 1, block)");
         c10::hip::HIPGuard g((c10::DeviceIndex)device);
         x = x.contiguous();
-        rave_stream* s = stream_for(s_enc, s_enc_b, x.size(0));
+        rave_stream* s = stream_for(s_enc, s_enc_b, x.size(0), RAVE_STREAM_ENCODE_ONLY);
         auto z = at::empty({x.size(0), zc(), stream_block / hop}, x.options());
         check(rave_stream_encode(s, x.data_ptr<float>(), z.data_ptr<float>(), cur()), "stream_encode");
         return z;
@@ -185,9 +187,33 @@ struct Engine : torch::CustomClassHolder {
                           "z must be (B, latent + speaker, block / hop)");
         c10::hip::HIPGuard g((c10::DeviceIndex)device);
         z = z.contiguous();
-        rave_stream* s = stream_for(s_dec, s_dec_b, z.size(0));
+        rave_stream* s = stream_for(s_dec, s_dec_b, z.size(0), RAVE_STREAM_DECODE_ONLY);
         auto y = at::empty({z.size(0), 1, stream_block}, z.options());
         check(rave_stream_decode(s, z.data_ptr<float>(), y.data_ptr<float>(), nullptr, cur()), "stream_decode");
+        return y;
+    }
+    // discrete configs: one block of RVQ indices (B, n_q, block / hop) int64
+    at::Tensor stream_encode_codes(at::Tensor x) {
+        on_device(x, "x");
+        TORCH_CHECK_VALUE(x.dim() == 3 && x.size(1) == 1 && x.size(2) == stream_block, "x must be (B, 1, block)");
+        c10::hip::HIPGuard g((c10::DeviceIndex)device);
+        x = x.contiguous();
+        rave_stream* s = stream_for(s_enc, s_enc_b, x.size(0), RAVE_STREAM_ENCODE_ONLY);
+        auto idx = at::empty({x.size(0), (int64_t)cfg.rvq_quantizers, stream_block / hop}, x.options().dtype(at::kLong));
+        check(rave_stream_encode_codes(s, x.data_ptr<float>(), idx.data_ptr<int64_t>(), cur()), "stream_encode_codes");
+        return idx;
+    }
+    at::Tensor stream_decode_codes(at::Tensor idx) {
+        on_device(idx, "idx");
+        TORCH_CHECK_VALUE(idx.dim() == 3 && idx.size(1) == cfg.rvq_quantizers && idx.size(2) == stream_block / hop &&
+                              idx.scalar_type() == at::kLong,
+                          "idx must be (B, n_q, block / hop) int64");
+        c10::hip::HIPGuard g((c10::DeviceIndex)device);
+        idx = idx.contiguous();
+        rave_stream* s = stream_for(s_dec, s_dec_b, idx.size(0), RAVE_STREAM_DECODE_ONLY);
+        auto y = at::empty({idx.size(0), 1, stream_block}, idx.options().dtype(at::kFloat));
+        check(rave_stream_decode_codes(s, idx.data_ptr<int64_t>(), y.data_ptr<float>(), nullptr, cur()),
+              "stream_decode_codes");
         return y;
     }
     void stream_reset() {
@@ -196,7 +222,7 @@ struct Engine : torch::CustomClassHolder {
     }
     // AdaIN controls (ScriptedRAVE.update_adain): -1 keeps a flag
     void adain_control(int64_t learn_x, int64_t learn_y, bool reset_x, bool reset_y) {
-        check(rave_model_adain_control(m, (int)learn_x, (int)learn_y, reset_x, reset_y), "adain_control");
+        check(rave_model_adain_control(m, (int)learn_x, (int)learn_y, reset_x, reset_y, cur()), "adain_control");
     }
     // the constant speaker embedding encode concatenates (nn~ `speaker` choice)
     void set_speaker(at::Tensor emb) {
@@ -276,6 +302,8 @@ TORCH_LIBRARY(rave_amd, lib) {
         .def("decode_codes", &Engine::decode_codes)
         .def("stream_encode", &Engine::stream_encode)
         .def("stream_decode", &Engine::stream_decode)
+        .def("stream_encode_codes", &Engine::stream_encode_codes)
+        .def("stream_decode_codes", &Engine::stream_decode_codes)
         .def("stream_reset", &Engine::stream_reset)
         .def("adain_control", &Engine::adain_control)
         .def("set_speaker", &Engine::set_speaker)

@@ -12,8 +12,11 @@ for a ``rave_amd.RAVE``:
 * attributes through ``register_attribute`` and ``get_<name>`` / ``set_<name>``
   that store 1-tuples and return 0 from setters (:120-126, :427-479);
 * ``encode`` (:298-314), ``decode`` with the stereo duplication (:317-336) and
-  ``forward`` (:338-339), in streaming mode (cached_conv, one block per call)
-  for a causal config, offline otherwise.
+  ``forward`` (:338-339), in streaming mode (cached_conv, one block per call;
+  causal or centred padding) or offline (the default follows cfg.causal);
+* a discrete config behaves as DiscreteScriptedRAVE (:503-517): ``encode``
+  returns the RVQ indices as float, ``decode`` clamps and truncates them before
+  rvq.decode.
 
 nn~ itself loads a TorchScript module; the kernels here are reached through
 ctypes, which TorchScript cannot script, so this is the method table and call
@@ -39,13 +42,9 @@ class NNTildeRAVE:
         cfg = model.cfg
         self.model, self.cfg, self.stereo = model, cfg, bool(stereo)
         self.streaming = cfg.causal if streaming is None else bool(streaming)
-        if self.streaming and not cfg.causal:
-            raise ValueError("streaming requires a causal config (causal.gin)")
         if self.stereo and getattr(model, "adain", None) is not None:
             raise ValueError("Stereo mode not yet supported with AdaIN")      # export.py:115-116
-        if cfg.rvq is not None:
-            raise ValueError("discrete configs export through encode_codes / decode_codes "
-                             "(DiscreteScriptedRAVE), not this method table")
+        self.discrete = cfg.rvq is not None
         self.block, self.batch = block, batch
         self.sr = getattr(cfg, "sampling_rate", 48000)                       # v2.gin SAMPLING_RATE
         self.speakers = None if speakers is None else [torch.as_tensor(e, dtype=torch.float32).reshape(-1)
@@ -58,7 +57,8 @@ class NNTildeRAVE:
             self.resampler = Resampler(int(target_sr), self.sr, device=getattr(model, "device", None), causal=cfg.causal,
                                        streaming=self.streaming)
             self.sr = int(target_sr)
-        self.latent_size = cfg.latent_size + cfg.speaker_size                # encode's channels
+        # encode's channels: latents + speaker, or the RVQ indices (DiscreteScriptedRAVE)
+        self.latent_size = cfg.rvq.num_quantizers if self.discrete else cfg.latent_size + cfg.speaker_size
         self._methods: Dict[str, Tuple[int, int, int, int, List[str], List[str]]] = {}
         self._attrs: Dict[str, tuple] = {}
         self._enc_stream = self._dec_stream = None
@@ -172,13 +172,13 @@ class NNTildeRAVE:
         without touching the decode stream's caches."""
         from rave_amd.streaming import StreamingRAVE
         if self._enc_stream is None or self._enc_stream.B != batch:
-            self._enc_stream = StreamingRAVE(self.model, batch=batch, block=self.block)
+            self._enc_stream = StreamingRAVE(self.model, batch=batch, block=self.block, direction="encode")
         return self._enc_stream
 
     def _dec_streamer(self, batch: int):
         from rave_amd.streaming import StreamingRAVE
         if self._dec_stream is None or self._dec_stream.B != batch:
-            self._dec_stream = StreamingRAVE(self.model, batch=batch, block=self.block)
+            self._dec_stream = StreamingRAVE(self.model, batch=batch, block=self.block, direction="decode")
         return self._dec_stream
 
     def _blocks(self, t: torch.Tensor, per_block: int) -> List[torch.Tensor]:
@@ -204,6 +204,13 @@ class NNTildeRAVE:
         self._select_speaker()
         if self.resampler is not None:
             x = self.resampler.to_model_sampling_rate(x)
+        if self.discrete:        # post_process_latent: rvq.encode(z).float()
+            if self.streaming:
+                st = self._enc_streamer(x.shape[0])
+                idx = torch.cat([st.encode_codes(b) for b in self._blocks(x, self.block)], -1)
+            else:
+                idx = self.model.encode_codes(x)
+            return idx.float()
         if self.streaming:
             st = self._enc_streamer(x.shape[0])
             return torch.cat([st.encode(b) for b in self._blocks(x, self.block)], -1)
@@ -218,7 +225,14 @@ class NNTildeRAVE:
             self.update_adain()
         if self.stereo:
             z = torch.cat([z, z], 0)
-        if self.streaming:
+        if self.discrete:        # pre_process_latent: clamp(z, 0, codebook_size - 1).long()
+            idx = torch.clamp(z, 0, self.cfg.rvq.codebook_size - 1).long()
+            if self.streaming:
+                st = self._dec_streamer(idx.shape[0])
+                y = torch.cat([st.decode_codes(b) for b in self._blocks(idx, self.block // self.cfg.hop)], -1)
+            else:
+                y = self.model.decode_codes(idx)
+        elif self.streaming:
             st = self._dec_streamer(z.shape[0])
             y = torch.cat([st.decode(b) for b in self._blocks(z, self.block // self.cfg.hop)], -1)
         else:

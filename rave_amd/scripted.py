@@ -8,6 +8,13 @@ upstream encode / decode / forward table of :172-227), 1-tuple attributes
 with @torch.jit.export getters / setters (:120-126, :427-479), update_adain
 (:248-265), stereo decode (:317-336), and export_to_ts (:618).
 
+Streaming (cc.use_cached_conv(True), :543) works for causal and centred
+configs alike.  A discrete config exports as DiscreteScriptedRAVE
+(scripts/export.py:503-517): ``encode`` returns the RVQ indices as float
+(post_process_latent, ``rvq.encode(z).float()``), ``decode`` clamps them to the
+codebook and truncates to int64 (pre_process_latent) before rvq.decode ->
+speaker concat -> decoder.
+
 (No ``from __future__ import annotations`` here: TorchScript must see the
 attribute annotations as types.)
 """
@@ -59,6 +66,8 @@ class ScriptedRAVE(torch.nn.Module):
     is_using_adain: bool
     stereo: bool
     streaming: bool
+    discrete: bool
+    codebook_size: int
     hop: int
     latent_size: int
     active_speaker: int
@@ -82,10 +91,8 @@ class ScriptedRAVE(torch.nn.Module):
         from . import pqmf as P
         load_torch_ops()
         self.streaming = bool(cfg.causal if streaming is None else streaming)
-        if self.streaming and not cfg.causal:
-            raise ValueError("streaming requires a causal config (causal.gin)")
-        if cfg.rvq is not None:
-            raise ValueError("discrete configs export through encode_codes / decode_codes")
+        self.discrete = cfg.rvq is not None
+        self.codebook_size = int(cfg.rvq.codebook_size) if self.discrete else 0
         self.is_using_adain = bool(cfg.adain)
         if self.is_using_adain and stereo:
             raise ValueError("Stereo mode not yet supported with AdaIN")      # export.py:115-116
@@ -99,7 +106,8 @@ class ScriptedRAVE(torch.nn.Module):
         self.engine = torch.classes.rave_amd.Engine(config_ints(cfg), float(cfg.leaky_slope), names, tensors, spk,
                                                     prec, int(block))
         self.hop = int(cfg.hop)
-        self.latent_size = int(cfg.latent_size + cfg.speaker_size)
+        # the encode method's channels: latents + speaker, or the RVQ indices
+        self.latent_size = int(cfg.rvq.num_quantizers if self.discrete else cfg.latent_size + cfg.speaker_size)
         spks = [speaker] if speakers is None else list(speakers)
         self.register_buffer("speakers", torch.from_numpy(
             np.stack([np.asarray(e, np.float32).reshape(-1) for e in spks])) if spks else
@@ -276,6 +284,12 @@ class ScriptedRAVE(torch.nn.Module):
         self._select_speaker()
         if self.use_resampler:
             x = self._fir(x, True)                         # to_model_sampling_rate
+        if self.discrete:       # DiscreteScriptedRAVE.post_process_latent: rvq.encode(z).float()
+            if self.streaming:
+                idx = torch.cat([self.engine.stream_encode_codes(b) for b in self._blocks(x, self.engine.block())], -1)
+            else:
+                idx = self.engine.encode_codes(x)
+            return idx.float()
         if self.streaming:
             return torch.cat([self.engine.stream_encode(b) for b in self._blocks(x, self.engine.block())], -1)
         return self.engine.encode(x)
@@ -286,7 +300,14 @@ class ScriptedRAVE(torch.nn.Module):
             self.update_adain()
         if self.stereo:
             z = torch.cat([z, z], 0)
-        if self.streaming:
+        if self.discrete:       # pre_process_latent: clamp(z, 0, codebook_size - 1).long() -> rvq.decode
+            idx = torch.clamp(z, 0, self.codebook_size - 1).long()
+            if self.streaming:
+                y = torch.cat([self.engine.stream_decode_codes(b)
+                               for b in self._blocks(idx, self.engine.block() // self.hop)], -1)
+            else:
+                y = self.engine.decode_codes(idx)
+        elif self.streaming:
             y = torch.cat([self.engine.stream_decode(b) for b in self._blocks(z, self.engine.block() // self.hop)], -1)
         else:
             y = self.engine.decode(z)

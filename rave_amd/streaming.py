@@ -1,4 +1,4 @@
-"""Block streaming of a causal model -- the cached_conv streaming mode.
+"""Block streaming -- the cached_conv streaming mode, causal or centred.
 
 ``cc.use_cached_conv(True)`` (scripts/export.py:543, README.md:186-190;
 cached_conv is the third-party ``cached-conv>=2.5.0``) turns every operator of
@@ -9,9 +9,16 @@ input, the cached ConvTranspose1d as a polyphase 2-tap conv with one history
 column, CachedPQMF's analysis / synthesis caches, NoiseGeneratorV2's cached
 strided convs and per-frame filter, and AdaIN on each block's columns.
 
-The decoder output equals one-shot causal decoding delayed by
-sum(r//2 * upsampling) = 928 samples for v2 once the receptive field is
-filled; the encoder is exact (zero delay).  State is created zeroed at
+Centred (non-causal) configs stream the way the reference's default model
+exports with ``--streaming`` (README.md:187-190): every CachedConv1d reads an
+(l + r)-column cache, so it lags its offline conv by r, and Residual's
+AlignBranches delays the identity branch by the unit's delay
+(rave/blocks.py:32-46).  The decoder output equals one-shot decoding delayed
+by ``decode_delay`` samples (928 for v2 causal, 13280 for v2 centred) once the
+receptive field is filled; a causal encoder is exact (zero delay), a centred
+one decimates its delayed signal on the strided convs' own phase, as the
+reference's does.  Discrete configs stream RVQ indices (``encode_codes`` /
+``decode_codes``, DiscreteScriptedRAVE).  State is created zeroed at
 construction (the reference creates it lazily on the first call) and is not
 re-entrant: one StreamingRAVE per stream, like one nn~ instance.  With
 ``graph=True`` every block replays a captured hipGraph.
@@ -28,20 +35,24 @@ from .model import RAVE, _stream
 
 
 class StreamingRAVE:
-    """Per-block encode / decode of a causal RAVE with persistent caches."""
+    """Per-block encode / decode of a RAVE with persistent caches.
+    ``direction``: "both", "encode" or "decode" (build one side only)."""
 
-    def __init__(self, model: RAVE, batch: int = 1, block: int = 2048, graph: bool = True):
+    def __init__(self, model: RAVE, batch: int = 1, block: int = 2048, graph: bool = True,
+                 direction: str = "both"):
         cfg = model.cfg
-        if not cfg.causal:
-            raise ValueError("streaming requires a causal config (causal.gin)")
         if block % cfg.hop:
             raise ValueError(f"block must be a multiple of {cfg.hop}")
+        flags = {"both": 0, "encode": N.STREAM_ENCODE_ONLY, "decode": N.STREAM_DECODE_ONLY}
+        if direction not in flags:
+            raise ValueError(f"direction must be one of {sorted(flags)}")
         self.model, self.cfg, self.B, self.block = model, cfg, batch, block
         self.Fz = block // cfg.hop
         self.F = block // cfg.n_band
         h = C.c_void_p()
         with torch.cuda.device(model.device):
-            N.check(N.lib.rave_stream_create(model.handle, batch, block, N.STREAM_GRAPH if graph else 0,
+            N.check(N.lib.rave_stream_create(model.handle, batch, block,
+                                             (N.STREAM_GRAPH if graph else 0) | flags[direction],
                                              C.byref(h)), "stream_create")
         self.handle = h
 
@@ -85,10 +96,51 @@ class StreamingRAVE:
                     "stream_decode")
         return y
 
+    def _noise_arg(self, noise_u):
+        if noise_u is None:
+            return None
+        if self.cfg.noise is None:
+            raise ValueError("noise_u given for a config without a noise synthesizer")
+        shape = self.model.noise_shape(self.B, self.Fz)
+        if tuple(noise_u.shape) != shape or noise_u.dtype != torch.float32 or noise_u.device.type != "cuda":
+            raise ValueError(f"noise_u must be a float32 CUDA tensor of shape {shape}")
+        return noise_u.contiguous()
+
+    def encode_codes(self, x: torch.Tensor) -> torch.Tensor:
+        """One block -> RVQ indices (B, n_q, block / hop) int64 (discrete config)."""
+        if self.cfg.rvq is None:
+            raise ValueError("encode_codes needs a discrete (RVQ) config")
+        if tuple(x.shape) != (self.B, 1, self.block) or x.dtype != torch.float32 or x.device.type != "cuda":
+            raise ValueError(f"x must be a float32 CUDA tensor of shape {(self.B, 1, self.block)}")
+        x = x.contiguous()
+        idx = torch.empty(self.B, self.cfg.rvq.num_quantizers, self.Fz, dtype=torch.int64, device=x.device)
+        with torch.cuda.device(x.device):
+            N.check(N.lib.rave_stream_encode_codes(self.handle, x.data_ptr(), idx.data_ptr(), _stream(x.device)),
+                    "stream_encode_codes")
+        return idx
+
+    def decode_codes(self, idx: torch.Tensor, noise_u: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One block of RVQ indices (clamped to the codebook) -> audio (B, 1, block)."""
+        if self.cfg.rvq is None:
+            raise ValueError("decode_codes needs a discrete (RVQ) config")
+        shape = (self.B, self.cfg.rvq.num_quantizers, self.Fz)
+        if tuple(idx.shape) != shape or idx.dtype != torch.int64 or idx.device.type != "cuda":
+            raise ValueError(f"idx must be an int64 CUDA tensor of shape {shape}")
+        idx = idx.contiguous()
+        u = self._noise_arg(noise_u)
+        y = torch.empty(self.B, 1, self.block, device=idx.device)
+        with torch.cuda.device(idx.device):
+            N.check(N.lib.rave_stream_decode_codes(self.handle, idx.data_ptr(), y.data_ptr(),
+                                                   None if u is None else u.data_ptr(), _stream(idx.device)),
+                    "stream_decode_codes")
+        return y
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.cfg.rvq is not None:
+            return self.decode_codes(self.encode_codes(x))
         return self.decode(self.encode(x))
 
     @property
     def decode_delay(self) -> int:
-        """Samples by which streamed decoding lags one-shot causal decoding."""
+        """Samples by which streamed decoding lags one-shot decoding."""
         return int(N.lib.rave_stream_delay(self.handle))

@@ -309,8 +309,10 @@ def gen_rvq(mods, out, seed=0):
                         gap=gaps, seed=np.int64(seed))
 
 
-def gen_streaming(mods, cfg, out, seed=0, n_blocks=12, block=2048):
-    """Causal cached-conv streaming of the reference (cc.use_cached_conv(True))."""
+def gen_streaming(mods, cfg, out, seed=0, n_blocks=12, block=2048, fname="causal_stream.npz"):
+    """Cached-conv streaming of the reference (cc.use_cached_conv(True)), causal
+    or centred padding (the latter is the reference's default model exported
+    with --streaming, README.md:187-190), next to the one-shot outputs."""
     m_s = build_reference(mods, cfg, cached=True)
     params = init_params(cfg, seed=seed)
     load_params(m_s, cfg, params)
@@ -335,8 +337,64 @@ def gen_streaming(mods, cfg, out, seed=0, n_blocks=12, block=2048):
         res["y_stream"] = torch.cat(ys, -1).numpy()
         res["z_oneshot"] = ref_encode(m_o, cfg, x, speaker).numpy()
         res["y_oneshot"] = ref_decode(m_o, z).numpy()
-    np.savez_compressed(os.path.join(out, "causal_stream.npz"), **res)
+    np.savez_compressed(os.path.join(out, fname), **res)
     return res
+
+
+def gen_stream_discrete(mods, cfg, out, seed=0, n_blocks=8, block=2048, fname="discrete_stream.npz"):
+    """DiscreteScriptedRAVE streamed (scripts/export.py:503-517 under
+    cc.use_cached_conv(True)): per block, PQMF -> encoder -> rvq.encode
+    (post_process_latent) with the top-2 gaps of every decision (tie margin),
+    and, in a separate pass over fresh caches, the reference's own streamed
+    codes -> rvq.decode (pre_process_latent's clamp) -> speaker concat ->
+    decoder -> PQMF inverse."""
+    m = build_reference(mods, cfg, cached=True)
+    params = init_params(cfg, seed=seed)
+    load_params(m, cfg, params)
+    speaker = torch.from_numpy(init_speaker(cfg, seed=seed))
+    x = torch.from_numpy(synth_audio(1, n_blocks * block, seed0=17))
+    frames = block // cfg.hop
+    res = {"x": x.numpy(), "speaker": speaker.numpy(), "block": np.int64(block), "seed": np.int64(seed)}
+    with torch.no_grad():
+        idxs, gaps = [], []
+        for i in range(n_blocks):
+            ze = ref_encode(m, cfg, x[..., i * block:(i + 1) * block], speaker)
+            idxs.append(m.encoder.rvq.encode(ze))
+            gaps.append(rvq_gaps(m.encoder.rvq, ze).reshape(cfg.rvq.num_quantizers, 1, frames))
+        idx = torch.cat(idxs, -1)
+        m2 = build_reference(mods, cfg, cached=True)     # fresh caches for the decoder pass
+        load_params(m2, cfg, params)
+        ys = []
+        for i in range(n_blocks):
+            zq = m2.encoder.rvq.decode(torch.clamp(idx[..., i * frames:(i + 1) * frames], 0,
+                                                   cfg.rvq.codebook_size - 1).long())
+            emb = speaker.reshape(1, -1, 1).repeat(zq.shape[0], 1, zq.shape[-1])
+            ys.append(ref_decode(m2, torch.cat((zq, emb), 1)))
+    res["idx_stream"] = idx.numpy()
+    res["gap_stream"] = np.concatenate(gaps, -1)
+    res["y_stream"] = torch.cat(ys, -1).numpy()
+    np.savez_compressed(os.path.join(out, fname), **res)
+    return res
+
+
+def write_manifest(out, extra=None):
+    """Hash every fixture (tests/golden/*.npz) into MANIFEST.json, keeping the
+    keys an earlier full run wrote."""
+    path = os.path.join(out, "MANIFEST.json")
+    manifest = {}
+    if os.path.exists(path):
+        with open(path) as fh:
+            manifest = json.load(fh)
+    manifest.update(extra or {})
+    manifest["generator"] = "tests/golden/make_golden.py"
+    manifest["reference"] = "abargum/RAVE @ 2024-10-16 (path-imported, see docstring)"
+    manifest["torch"] = torch.__version__
+    files = sorted(f for f in os.listdir(out) if f.endswith(".npz"))
+    manifest["files"] = {f: hashlib.sha256(open(os.path.join(out, f), "rb").read()).hexdigest()[:16]
+                         for f in files}
+    with open(path, "w") as fh:
+        json.dump(manifest, fh, indent=1, sort_keys=True)
+    return manifest
 
 
 def gen_stream_v3(mods, cfg, out, fname="v3_noise_causal_stream.npz", seed=0, n_blocks=6, block=2048):
@@ -560,18 +618,29 @@ def main():
     mods = install_shims()
     if a.only == "stream_v3":
         gen_stream_v3(mods, rcfg.v3_noise(causal=True, capacity=16), a.out)
+        gen_stream_v3(mods, rcfg.v3_noise(capacity=16), a.out, fname="v3_noise_stream.npz")
+        write_manifest(a.out)
+        return
+    if a.only == "stream":
+        gen_streaming(mods, rcfg.v2(), a.out, fname="v2_stream.npz")
+        gen_stream_discrete(mods, rcfg.discrete(), a.out)
+        gen_stream_v3(mods, rcfg.v3_noise(capacity=16), a.out, fname="v3_noise_stream.npz")
+        write_manifest(a.out)
         return
     if a.only == "speaker":
         gen_speaker(mods, a.out)
         gen_resampler(mods, a.out)
+        write_manifest(a.out)
         return
     if a.only == "adain":
         gen_adain(mods, rcfg.v3(), a.out)
         gen_adain(mods, rcfg.v3(capacity=8), a.out, fname="v3_adain_small.npz", t=4096)
+        write_manifest(a.out)
         return
-    manifest = {"generator": "tests/golden/make_golden.py",
-                "reference": "abargum/RAVE @ 2024-10-16 (path-imported, see docstring)",
-                "torch": torch.__version__}
+    if a.only == "manifest":
+        write_manifest(a.out)
+        return
+    manifest = {}
     manifest["residual_semantics"] = check_residual_semantics(mods)
     assert all(v[0] for v in manifest["residual_semantics"].values()), manifest["residual_semantics"]
 
@@ -581,6 +650,7 @@ def main():
     gen_model(mods, rcfg.v2(), a.out, "v2.npz")
     gen_model(mods, rcfg.causal(), a.out, "causal.npz")
     gen_streaming(mods, rcfg.causal(), a.out)
+    gen_streaming(mods, rcfg.v2(), a.out, fname="v2_stream.npz")
     gen_model(mods, rcfg.discrete(), a.out, "discrete.npz")
     gen_rvq(mods, a.out)
     gen_model(mods, rcfg.v3_noise(), a.out, "v3_noise.npz")
@@ -589,15 +659,11 @@ def main():
     gen_adain(mods, rcfg.v3(), a.out)
     gen_adain(mods, rcfg.v3(capacity=8), a.out, fname="v3_adain_small.npz", t=4096)
     gen_stream_v3(mods, rcfg.v3_noise(causal=True, capacity=16), a.out)
+    gen_stream_v3(mods, rcfg.v3_noise(capacity=16), a.out, fname="v3_noise_stream.npz")
+    gen_stream_discrete(mods, rcfg.discrete(), a.out)
     gen_speaker(mods, a.out)
     gen_resampler(mods, a.out)
-
-    files = sorted(f for f in os.listdir(a.out) if f.endswith(".npz"))
-    manifest["files"] = {f: hashlib.sha256(open(os.path.join(a.out, f), "rb").read()).hexdigest()[:16]
-                         for f in files}
-    with open(os.path.join(a.out, "MANIFEST.json"), "w") as fh:
-        json.dump(manifest, fh, indent=1, sort_keys=True)
-    print(json.dumps(manifest, indent=1))
+    print(json.dumps(write_manifest(a.out, manifest), indent=1))
 
 
 if __name__ == "__main__":

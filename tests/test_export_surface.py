@@ -31,10 +31,17 @@ def test_stereo_and_causal():
     assert w.get_method_params("decode") == [320, 1024, 2, 1]
     assert w.get_method_labels("forward")[1] == ["(signal) Reconstructed audio signal (L)",
                                                  "(signal) Reconstructed audio signal (R)"]
-    with pytest.raises(ValueError):
-        NNTildeRAVE(_Cfg(rcfg.v2()), streaming=True)          # offline config cannot stream
-    with pytest.raises(ValueError):
-        NNTildeRAVE(_Cfg(rcfg.discrete()))
+    # a centred config streams too (cached_conv with centred padding, README.md:187-190)
+    assert NNTildeRAVE(_Cfg(rcfg.v2()), streaming=True).streaming is True
+
+
+def test_discrete_method_table():
+    """DiscreteScriptedRAVE (scripts/export.py:503-517): encode's channels are
+    the RVQ indices (16 quantizers), decode takes them back."""
+    w = NNTildeRAVE(_Cfg(rcfg.discrete()))
+    assert w.discrete is True
+    assert w.get_method_params("encode") == [1, 1, 16, 1024]
+    assert w.get_method_params("decode") == [16, 1024, 1, 1]
 
 
 def test_attributes_store_one_tuples():
