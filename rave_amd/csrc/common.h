@@ -107,6 +107,69 @@ __device__ __forceinline__ float sin_squared(float x) {
     return v * v;
 }
 
+// Split-f16 range guard (RAVE_PREC_SPLIT16).  An operand v is carried as
+// hi = f16(v), lo = f16((v - hi) * 2^11), which needs |v| < 2^15.  Kernels
+// convert optimistically and vote per wave on max |v| >= kSplitLimit; a staged
+// operand block that fails is re-converted as v * 2^-s (s = split_shift of its
+// workgroup-wide max, so |v 2^-s| < 2^14) and the GEMM's accumulator (or the
+// epilogue scale) takes the exact 2^s back.  NaN / inf pass through unscaled,
+// as they do in fp32.
+#ifndef RAVE_SPLIT_GUARD
+#define RAVE_SPLIT_GUARD 1          // 0: A/B variant builds only (no range guard)
+#endif
+constexpr float kSplitLimit = 32768.f;
+__device__ __forceinline__ int split_shift(float m) {
+    if (!(m < 3.0e38f)) return 0;
+    int e;
+    (void)frexpf(m, &e);                      // m < 2^e
+    return e > 14 ? e - 14 : 0;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+// per-wave votes: wave w's lane 0 writes byte v[w] (0/1) unconditionally after
+// its conversion; after a barrier any wave reads the NW bytes (masked dwords)
+__device__ __forceinline__ void vote_cast(unsigned char* v, int wave, float m) {
+    if (!RAVE_SPLIT_GUARD) return;
+    const bool over = __builtin_amdgcn_ballot_w64(m >= kSplitLimit) != 0;
+    if ((threadIdx.x & 63) == 0) v[wave] = over ? 1 : 0;
+}
+template <int NW>
+__device__ __forceinline__ bool vote_any(const unsigned char* v) {
+    if (!RAVE_SPLIT_GUARD) return false;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(v);
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < (NW + 3) / 4; ++i) {
+        uint32_t w = p[i];
+        if ((i + 1) * 4 > NW) w &= (1u << (8 * (NW - 4 * i))) - 1u;
+        x |= w;
+    }
+    return __builtin_amdgcn_readfirstlane(x != 0u ? 1 : 0) != 0;
+}
+// workgroup max of per-thread m through `red` (NW floats); one barrier
+template <int NW>
+__device__ __forceinline__ float block_max(float m, float* red) {
+    m = wave_max(m);
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[wave] = m;
+    __syncthreads();
+    float mx = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) mx = fmaxf(mx, red[w]);
+    return mx;
+}
+// max |v_i| of an 8-vector (the optimistic conversion's vote input)
+template <typename V8>
+__device__ __forceinline__ float absmax8(const V8& v) {
+    float m = fabsf(v[0]);
+#pragma unroll
+    for (int i = 1; i < 8; ++i) m = fmaxf(m, fabsf(v[i]));
+    return m;
+}
+
 // Input-activation prologue shared by the conv and noise kernels.
 // LeakyReLU(slope) (rave/blocks.py:91) and Snake (rave/blocks.py:852-853):
 //   x + (alpha + 1e-9)^-1 * sin(alpha * x)^2   -- same operation order as torch.

@@ -183,7 +183,10 @@ struct SGeo {
     // ring + two (hi, lo) plane pairs + Snake alphas + the surplus DMAs' dump piece
     static constexpr int MAIN = NS * STAGE + 2 * 2 * XPLANE + ALPHA + PB;
     static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
-    static constexpr int LDS_ALL = LDS + 16;                 // + the split-K "last arriver" word
+    // + the split-K "last arriver" word, the range guard's per-wave overflow votes
+    // (two plane buffers + the tile vote, x 16 waves, bytes) and wave maxima (16 floats)
+    static constexpr int VOTE = LDS + 16, VRED = LDS + 64;
+    static constexpr int LDS_ALL = LDS + 128;
     static constexpr int G8 = VC / 8;                        // 8-channel groups per row
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;   // convert tasks per thread
     static_assert(XPLANE % 16 == 0 && STAGE % 16 == 0, "16-byte LDS alignment");
@@ -270,6 +273,11 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
     if constexpr (SNAKE) {
         for (int i = tid; i < a.c_in; i += NT) alpha_s[i] = a.alpha[i];
     }
+    // range guard: per-wave overflow votes of the chunk converted into plane
+    // buffer pb at vote[pb * 16 + wave] (unused waves' bytes stay 0), wave maxima
+    unsigned char* vote = reinterpret_cast<unsigned char*>(smem + G::VOTE);
+    float* vred = reinterpret_cast<float*>(smem + G::VRED);
+    if (tid < 12) reinterpret_cast<uint32_t*>(vote)[tid] = 0u;  // ordered by the prologue's first barrier
 
     floatx16 acc[NI][NJ];
 #pragma unroll
@@ -328,12 +336,14 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                 wr[slot][j][pl] = bload16(wrs, wbase + (unsigned)(c * VCX + u) * wcstride +
                                                    (unsigned)(((j * KSC0 + s0) * 2 + pl) * 1024));
     };
-    // raw window of a stage -> activation -> (hi, lo) f16 planes
-    auto convert_task = [&](int c, int stage, int pb, int i) __attribute__((always_inline)) {
+    // raw window of a stage -> activation (* xs) -> (hi, lo) f16 planes; returns
+    // max |act| of the task's values (the range guard's vote input)
+    auto convert_task = [&](int c, int stage, int pb, int i, float xs) __attribute__((always_inline)) {
         const float* raw = reinterpret_cast<const float*>(smem + stage * G::STAGE);
         _Float16* xh = reinterpret_cast<_Float16*>(planes + pb * 2 * G::XPLANE);
         _Float16* xl = reinterpret_cast<_Float16*>(planes + pb * 2 * G::XPLANE + G::XPLANE);
         const int ci0 = c * CPC;
+        float m = 0.f;
         {
             const int e = tid + i * NT;
             const int g = (int)(((unsigned)e * a.xw_magic) >> 24);
@@ -350,18 +360,60 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                     } else {
                         val = val > 0.f ? val : val * slope;
                     }
-                    v8[v] = val;
+                    v8[v] = val * xs;
                 }
+                m = absmax8(v8);
                 const s_h8 hi = __builtin_convertvector(v8, s_h8);
                 const s_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, s_f32x8)) * 2048.0f, s_h8);
                 *reinterpret_cast<s_h8*>(xh + w * PH + g * 8) = hi;
                 *reinterpret_cast<s_h8*>(xl + w * PH + g * 8) = lo;
             }
         }
+        return m;
     };
     auto convert = [&](int c, int stage, int pb) __attribute__((always_inline)) {
+        float m = 0.f;
 #pragma unroll
-        for (int i = 0; i < XT; ++i) convert_task(c, stage, pb, i);
+        for (int i = 0; i < XT; ++i) m = fmaxf(m, convert_task(c, stage, pb, i, 1.0f));
+        return m;
+    };
+    // range guard.  vote: after a chunk's conversion into plane buffer pb, each
+    // wave records whether any of its values reached kSplitLimit.  After the
+    // barrier every wave reads the votes (one 16-byte LDS read); only when one
+    // is set does the workgroup take the rare path: the wave maxima of the
+    // conversion meet in LDS, the chunk is re-converted as act * 2^-s and the
+    // chunk's K-steps run on acc * 2^-s, scaled back by 2^s after them (exact).
+    auto cast_vote = [&](int pb, float m) __attribute__((always_inline)) {
+        if (!RAVE_SPLIT_GUARD) return;
+        const bool over = __builtin_amdgcn_ballot_w64(m >= kSplitLimit) != 0;
+        if (lane == 0) vote[pb * 16 + wave] = over ? 1 : 0;
+    };
+    auto read_vote = [&](int pb) __attribute__((always_inline)) {
+        if (!RAVE_SPLIT_GUARD) return false;
+        const uint32_t* v = reinterpret_cast<const uint32_t*>(vote + pb * 16);
+        return __builtin_amdgcn_readfirstlane((v[0] | v[1] | v[2] | v[3]) != 0u ? 1 : 0) != 0;
+    };
+    auto rescue = [&](int c, int stage, int pb, float m) __attribute__((always_inline)) {
+        m = wave_max(m);
+        if (lane == 0) vred[wave] = m;
+        __syncthreads();
+        float mx = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) mx = fmaxf(mx, vred[w]);
+        const int sh = __builtin_amdgcn_readfirstlane(split_shift(mx));
+        const float xs = ldexpf(1.0f, -sh);
+#pragma nounroll
+        for (int i = 0; i < XT; ++i) (void)convert_task(c, stage, pb, i, xs);
+        __syncthreads();
+        return sh;
+    };
+    auto scale_acc = [&](float f) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] *= f;
     };
 
     // per-lane A-fragment offsets (halves): window row wn*WN + l32 + q*d (+ group shift)
@@ -389,7 +441,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
     // wave issues XI window DMAs, then per own K-step 2*NJ weight loads.  The
     // body is instantiated per K-group (its K-step range fixes the counts);
     // both groups pass the same barriers.
-    auto body = [&](auto gtag) __attribute__((always_inline)) {
+    // guarded: the per-chunk range guard (second attempt only); otherwise the
+    // chunks' overflow votes are just OR-ed into `over` (no LDS traffic)
+    auto body = [&](auto gtag, bool guarded, bool& over) __attribute__((always_inline)) {
         constexpr int GG = decltype(gtag)::value;
         constexpr int KS = G::ks_of(GG);                // own K-steps per chunk
         constexpr int ST0 = G::st_of(GG);               // first own K-step
@@ -400,7 +454,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
         for (int k = 0; k < KS; ++k) load_w(c_begin, k, ST0 + k);
         wait_vm<(NS - 1) * XI + WR>();          // window c_begin landed
         __syncthreads();
-        convert(c_begin, 0, 0);
+        float cmax = convert(c_begin, 0, 0);
+        if (guarded) cast_vote(0, cmax);
+        else over |= cmax >= kSplitLimit;
         wait_vm<(NS - 2) * XI + WR>();          // window c_begin+1 landed
         __syncthreads();
         stamp(1);
@@ -412,9 +468,19 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
         for (int c = c_begin; c < c_end; ++c) {
             const int pb = (c - c_begin) & 1;
             const int s1 = stage + 1 == NS ? 0 : stage + 1;
-            issue(c + NS, stage);
             AFrag f[2];
             read_a(pb, ST0, f[0]);
+            // range guard of chunk c (converted during chunk c-1 or the prologue;
+            // its raw window is still in `stage` until the DMA below): the vote
+            // read rides with the first fragment reads
+            int sh_cur = 0;
+            if (__builtin_expect(guarded && read_vote(pb), 0)) {
+                sh_cur = rescue(c, stage, pb, cmax);
+                read_a(pb, ST0, f[0]);
+            }
+            issue(c + NS, stage);
+            if (__builtin_expect(sh_cur != 0, 0)) scale_acc(ldexpf(1.0f, -sh_cur));
+            cmax = 0.f;
 #pragma unroll
             for (int k = 0; k < KS; ++k) {
                 if (k + 1 < KS) read_a(pb, ST0 + k + 1, f[(k + 1) & 1]);   // next reads in flight
@@ -451,8 +517,13 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                 // split part of window c+1 into the other plane pair (VALU beside the MFMAs)
                 if (c + 1 < c_end) {
 #pragma unroll
-                    for (int i = k; i < XT; i += KS) convert_task(c + 1, s1, pb ^ 1, i);
+                    for (int i = k; i < XT; i += KS) cmax = fmaxf(cmax, convert_task(c + 1, s1, pb ^ 1, i, 1.0f));
                 }
+            }
+            if (__builtin_expect(sh_cur != 0, 0)) scale_acc(ldexpf(1.0f, sh_cur));
+            if (c + 1 < c_end) {
+                if (guarded) cast_vote(pb ^ 1, cmax);
+                else over |= cmax >= kSplitLimit;
             }
             // window c+2 landed: younger are, per chunk since its issue, the
             // weight refills and the next windows
@@ -462,16 +533,39 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
             if (c == c_begin) stamp(2);
         }
     };
-    if (kg == 0) body(IC<0>{});
-    else if constexpr (KG >= 2) {
-        if (kg == 1) body(IC<1>{});
-        else if constexpr (KG == 4) {
-            if (kg == 2) body(IC<2>{});
-            else body(IC<3>{});
+    // Range guard, two attempts over one copy of the K loop: the first runs
+    // with no per-chunk check; only when some chunk of the tile reached
+    // kSplitLimit (one vote per tile) does the loop run again from its
+    // prologue with the per-chunk rescue (rare: activations past 2^15).
+    bool guarded = false;
+#pragma nounroll
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        bool over = false;
+        if (kg == 0) body(IC<0>{}, guarded, over);
+        else if constexpr (KG >= 2) {
+            if (kg == 1) body(IC<1>{}, guarded, over);
+            else if constexpr (KG == 4) {
+                if (kg == 2) body(IC<2>{}, guarded, over);
+                else body(IC<3>{}, guarded, over);
+            }
         }
+        wait_vm<0>();                       // drain the ring (epilogue loads / a second attempt)
+        if (!RAVE_SPLIT_GUARD || guarded) break;
+        const bool wover = __builtin_amdgcn_ballot_w64(over) != 0;
+        if (lane == 0) vote[32 + wave] = wover ? 1 : 0;
+        __syncthreads();
+        const bool tover = vote_any<NW>(vote + 32);
+        if (__builtin_expect(!tover, 1)) break;
+        guarded = true;
+        __syncthreads();                    // every wave read the tile vote
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     }
     stamp(3);
-    wait_vm<0>();                           // drain the ring before the epilogue's own loads
     if constexpr (KG >= 2) {
         // groups 1.. hand their partial tiles to group 0 through LDS (ring and
         // planes are dead); group 0 adds them in group order (fixed: bitwise

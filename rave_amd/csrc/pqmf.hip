@@ -280,17 +280,27 @@ static_assert(kPaFrames == kPsFrames && kPaBlk >= 1, "analysis geometry");
 constexpr int kPsK = 17;                                     // 32-deep K-steps (<= 544 taps / K rows)
 constexpr int kPsKP = 552;                                   // halves per filter row: 1104 B = 20 banks mod 64
 
-// power-of-two scale 2^e with max |v 2^e| in [8, 16) over the workgroup's values
-// (wave max via LDS; `red` holds kPsWaves floats)
+// Power-of-two scales from the workgroup's maxima (wave max via LDS; `red`
+// holds 2 W floats): the filter's 2^e with max |h 2^e| in [8, 16), and the
+// signal's split-f16 range guard 2^-s (common.h split_shift: 1 unless the
+// staged window reaches 2^15).
 template <int W>
-__device__ __forceinline__ float ps_scale(float amax, float* red) {
-    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+__device__ __forceinline__ float ps_scale(float amax, float xmax, float* red, float& xs) {
+    amax = wave_max(amax);
+    xmax = wave_max(xmax);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) red[wave] = amax;
+    if (lane == 0) {
+        red[wave] = amax;
+        red[W + wave] = xmax;
+    }
     __syncthreads();
-    float m = red[0];
+    float m = red[0], mx = red[W];
 #pragma unroll
-    for (int w = 1; w < W; ++w) m = fmaxf(m, red[w]);
+    for (int w = 1; w < W; ++w) {
+        m = fmaxf(m, red[w]);
+        mx = fmaxf(mx, red[W + w]);
+    }
+    xs = ldexpf(1.f, -split_shift(mx));
     if (!(m > 0.f)) return 1.f;
     int e;
     (void)frexpf(m, &e);                  // m in [2^(e-1), 2^e)
@@ -338,14 +348,17 @@ __global__ __launch_bounds__(64 * kPaWaves) void pqmf_analysis_split_kernel(rave
     const int s0 = t0 * 16 - a.pad_left;
     constexpr int XT = ((kPaFrames + 40) * 16 + NT - 1) / NT;
     float xv[XT];
+    float xmax = 0.f;
 #pragma unroll
     for (int it = 0; it < XT; ++it) {
         const int i = tid + it * NT;
         const int t = s0 + i;
         const float v = xb[min(max(t, 0), a.t_in - 1)];
         xv[it] = (i < wframes * 16 && t >= 0 && t < a.t_in) ? v : 0.f;
+        xmax = fmaxf(xmax, fabsf(xv[it]));
     }
-    const float sc = ps_scale<kPaWaves>(amax, red);
+    float xs;
+    const float sc = ps_scale<kPaWaves>(amax, xmax, red, xs);
     for (int i = tid; i < (16 - NBO) * kPsKP; i += NT) {
         fh[NBO * kPsKP + i] = (_Float16)0.f;
         fl[NBO * kPsKP + i] = (_Float16)0.f;
@@ -361,7 +374,7 @@ __global__ __launch_bounds__(64 * kPaWaves) void pqmf_analysis_split_kernel(rave
 #pragma unroll
     for (int it = 0; it < XT; ++it) {
         const int i = tid + it * NT;
-        if (i < wframes * 16) ps_split(xv[it], xh[ps_xi(i)], xl[ps_xi(i)]);
+        if (i < wframes * 16) ps_split(xv[it] * xs, xh[ps_xi(i)], xl[ps_xi(i)]);
     }
     __syncthreads();
     const int g = lane >> 4, col = lane & 15;
@@ -385,7 +398,7 @@ __global__ __launch_bounds__(64 * kPaWaves) void pqmf_analysis_split_kernel(rave
             acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[q], 0, 0, 0);
         }
     }
-    const float unscale = 1.0f / (sc * 2048.0f);              // exact: powers of two
+    const float unscale = 1.0f / (sc * 2048.0f * xs);         // exact: powers of two
     float* yb = a.y + (int64_t)b * a.y_sb;
 #pragma unroll
     for (int q = 0; q < kPaBlk; ++q) {
@@ -453,15 +466,7 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_synthesis_split_kernel(rav
         av[it] = xb[(int64_t)(a.mode == 1 ? cc + 16 : cc) * a.x_sc + ff];
         nv[it] = nzb ? nzb[(int64_t)cc * a.n_sc + ff] : 0.f;
     }
-    const float sc = ps_scale<kPsWaves>(amax, red);
-#pragma unroll
-    for (int it = 0; it < HT; ++it) {
-        const int i = tid + it * NT;
-        if (i < 16 * KW) {
-            const int m = i / KW, k = i - m * KW;
-            ps_split(hv[it] * sc, fh[m * kPsKP + k], fl[m * kPsKP + k]);
-        }
-    }
+    float xmax = 0.f;
 #pragma unroll
     for (int it = 0; it < XT; ++it) {
         const int i = tid + it * NT;
@@ -476,7 +481,25 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_synthesis_split_kernel(rav
             v = tanhf(v);
         }
         if ((c & 1) && !((a.frame0 + f) & 1)) v = -v;   // reverse_half
-        if (i < 16 * xw) ps_split(ok ? v : 0.f, xh[w * kPsXP + c], xl[w * kPsXP + c]);
+        xv[it] = ok ? v : 0.f;
+        xmax = fmaxf(xmax, fabsf(xv[it]));
+    }
+    float xs;
+    const float sc = ps_scale<kPsWaves>(amax, xmax, red, xs);
+#pragma unroll
+    for (int it = 0; it < HT; ++it) {
+        const int i = tid + it * NT;
+        if (i < 16 * KW) {
+            const int m = i / KW, k = i - m * KW;
+            ps_split(hv[it] * sc, fh[m * kPsKP + k], fl[m * kPsKP + k]);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < XT; ++it) {
+        const int i = tid + it * NT;
+        const int c = (int)__umulhi((unsigned)i, a_xw_magic);
+        const int w = i - c * xw;
+        if (i < 16 * xw) ps_split(xv[it] * xs, xh[w * kPsXP + c], xl[w * kPsXP + c]);
     }
     __syncthreads();
     const int g = lane >> 4, col = lane & 15;
@@ -502,7 +525,7 @@ __global__ __launch_bounds__(64 * kPsWaves) void pqmf_synthesis_split_kernel(rav
             acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[q], 0, 0, 0);
         }
     }
-    const float o = 16.f / (sc * 2048.0f);                    // n_band x the exact unscale
+    const float o = 16.f / (sc * 2048.0f * xs);               // n_band x the exact unscale
     float* yb = a.y + (int64_t)b * a.y_sb;
 #pragma unroll
     for (int q = 0; q < kPsBlk; ++q) {
@@ -541,7 +564,7 @@ extern "C" int rave_pqmf_analysis(const rave_pqmf_analysis_args* p, void* stream
     if (a.precision == RAVE_PREC_SPLIT16) {
         const int wframes = kPsFrames + (32 * kPsK + 15) / 16 + 1;
         const int ws = ps_xi(wframes * 16) + 8;
-        const size_t lds = (size_t)(2 * 16 * kPsKP + 2 * ws) * 2 + kPaWaves * 4;
+        const size_t lds = (size_t)(2 * 16 * kPsKP + 2 * ws) * 2 + 2 * kPaWaves * 4;
         dim3 grid(ceil_div(a.t_out, kPaFrames), a.batch);
         if (a.n_out_bands == 6)
             launch(pqmf_analysis_split_kernel<6>, grid, dim3(64 * kPaWaves), lds, as_stream(stream), a, wframes);
@@ -575,7 +598,7 @@ extern "C" int rave_pqmf_synthesis(const rave_pqmf_synthesis_args* p, void* stre
     RAVE_CHECK_ARG(a.precision == RAVE_PREC_F32 || a.precision == RAVE_PREC_SPLIT16,
                    "pqmf_synthesis: precision must be RAVE_PREC_F32 or RAVE_PREC_SPLIT16");
     if (a.precision == RAVE_PREC_SPLIT16) {
-        const size_t lds = (size_t)(2 * 16 * kPsKP + 2 * kPsXW * kPsXP) * 2 + kPsWaves * 4;
+        const size_t lds = (size_t)(2 * 16 * kPsKP + 2 * kPsXW * kPsXP) * 2 + 2 * kPsWaves * 4;
         dim3 grid(ceil_div(a.t_in, kPsFrames), a.batch);
         const unsigned xw_magic = (unsigned)((0x100000000ull + kPsXW - 1) / kPsXW);
         launch(pqmf_synthesis_split_kernel, grid, dim3(64 * kPsWaves), lds, as_stream(stream), a, xw_magic);

@@ -76,7 +76,9 @@ template <int C, int NB, int CB> struct SSGeo {
     static constexpr int G8 = C / 8;
     static constexpr int XT = (XR * G8 + NT - 1) / NT; // window staging tasks per thread
     static constexpr int TAB = kSSUnits * 6 * C;       // per unit: rs1 b1 a2 rs2 b2 a0
-    static constexpr int LDS = 2 * PLANE * 2 + TAB * 4;
+    // + range-guard votes (16 B) and wave maxima (16 floats)
+    static constexpr int VOTE = 2 * PLANE * 2 + TAB * 4, VRED = VOTE + 16;
+    static constexpr int LDS = VRED + 64;
     static_assert(NBX % CB == 0 && ST % R == 0 && NT <= 1024, "geometry");
 };
 
@@ -89,6 +91,8 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
     _Float16* ph = reinterpret_cast<_Float16*>(lds);
     _Float16* pl = ph + G::PLANE;
     float* tab = reinterpret_cast<float*>(lds + 4 * G::PLANE);
+    unsigned char* vote = reinterpret_cast<unsigned char*>(lds + G::VOTE);
+    float* vred = reinterpret_cast<float*>(lds + G::VRED);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -144,7 +148,9 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
     __syncthreads();                                   // tables visible
 
     // ------------------------------------------------------------ unit 0 input window
-    {
+    // (xs: range-guard scale; returns max |act0(x) xs| of the thread's values)
+    auto stage_window = [&](float xs) __attribute__((always_inline)) {
+        float cmax = 0.f;
         float rx[XT][8];
 #pragma unroll
         for (int i = 0; i < XT; ++i) {
@@ -167,8 +173,9 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
                 const float al = SNAKE ? tab[5 * C + min(g * 8 + v, C - 1)] : 0.f;
-                v8[v] = ok ? ss_act<SNAKE>(rx[i][v], slope, al) : 0.f;
+                v8[v] = ok ? ss_act<SNAKE>(rx[i][v], slope, al) * xs : 0.f;
             }
+            cmax = fmaxf(cmax, absmax8(v8));
             const ss_h8 hi = __builtin_convertvector(v8, ss_h8);
             const ss_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, ss_f32x8)) * 2048.0f, ss_h8);
             if (e < XR * G8) {
@@ -176,8 +183,8 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
                 *reinterpret_cast<ss_h8*>(pl + w * PH + g * 8) = lo;
             }
         }
-    }
-
+        return cmax;
+    };
     // running sum y (fp32): lane column col0 + 32j, rows mrow0 + 8(r>>2) + (r&3)
     const int col0 = wn * 32 * CB + l32;               // extended column of this lane
     const int mrow0 = 32 * wm + 4 * hh;
@@ -193,7 +200,37 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
                 xrs, ok ? (unsigned)(m * a.x_sc + t) * 4u : kSSOOB, 0, 0));
         }
     }
-    __syncthreads();
+    // unit 0's act0(x) window, under the range guard: one pass in the common
+    // case, a second one as act0(x) * 2^-sh0 when a wave saw |act0(x)| >= 2^15
+    int sh0 = 0;                                       // range-guard shift of the current unit's act0(y) planes
+    {
+        const float cmax = stage_window(1.0f);
+        vote_cast(vote, wave, cmax);
+        __syncthreads();
+        if (__builtin_expect(vote_any<G::NW>(vote), 0)) {      // rare: a rolled re-staging loop
+            sh0 = __builtin_amdgcn_readfirstlane(split_shift(block_max<G::NW>(cmax, vred)));
+            const float xs = ldexpf(1.0f, -sh0);
+#pragma nounroll
+            for (int e = tid; e < XR * G8; e += NT) {
+                const int g = e / XR, w = e - g * XR;
+                const bool ok = (r0 + w >= 0) && (r0 + w < a.T);
+                const int t = min(max(r0 + w, 0), a.T - 1);
+                ss_f32x8 v8;
+#pragma unroll
+                for (int v = 0; v < 8; ++v) {
+                    const int c = min(g * 8 + v, C - 1);
+                    const float xv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        xrs, (unsigned)(c * a.x_sc + t) * 4u, 0, 0));
+                    v8[v] = ok ? ss_act<SNAKE>(xv, slope, SNAKE ? tab[5 * C + c] : 0.f) * xs : 0.f;
+                }
+                const ss_h8 hi = __builtin_convertvector(v8, ss_h8);
+                const ss_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, ss_f32x8)) * 2048.0f, ss_h8);
+                *reinterpret_cast<ss_h8*>(ph + w * PH + g * 8) = hi;
+                *reinterpret_cast<ss_h8*>(pl + w * PH + g * 8) = lo;
+            }
+            __syncthreads();
+        }
+    }
 
     struct BF {
         ss_h8 h[CB], l[CB];
@@ -214,9 +251,11 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
             for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
     };
     zero_acc();
-    // act(v) -> (hi, lo) planes at extended column col0 + 32j (zero outside [0, T) if mask)
-    auto write_planes = [&](const float (*v)[16], const float* al_tab, bool mask)
+    // act(v) * xs -> (hi, lo) planes at extended column col0 + 32j (zero outside
+    // [0, T) if mask); returns max |act(v) xs| of the thread's values
+    auto write_planes = [&](const float (*v)[16], const float* al_tab, bool mask, float xs)
         __attribute__((always_inline)) {
+        float cmax = 0.f;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int m = mrow0 + 8 * g;
@@ -228,13 +267,31 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
                 const bool ok = !mask || (t >= 0 && t < a.T);
                 ss_f32x4 w4;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) w4[e] = ok ? ss_act<SNAKE>(v[j][4 * g + e], slope, al[e]) : 0.f;
+                for (int e = 0; e < 4; ++e) w4[e] = ok ? ss_act<SNAKE>(v[j][4 * g + e], slope, al[e]) * xs : 0.f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) cmax = fmaxf(cmax, fabsf(w4[e]));
                 const ss_h4 hv = __builtin_convertvector(w4, ss_h4);
                 const ss_h4 lv = __builtin_convertvector((w4 - __builtin_convertvector(hv, ss_f32x4)) * 2048.0f, ss_h4);
                 *reinterpret_cast<ss_h4*>(ph + (OFF + col0 + 32 * j) * PH + m) = hv;
                 *reinterpret_cast<ss_h4*>(pl + (OFF + col0 + 32 * j) * PH + m) = lv;
             }
         }
+        return cmax;
+    };
+    // optimistic planes, then the range guard's vote; on overflow the planes are
+    // rewritten as act(v) 2^-s and the shift s is returned (else 0)
+    auto guarded_planes = [&](const float (*v)[16], const float* al_tab, bool mask)
+        __attribute__((always_inline)) {
+        const float cmax = write_planes(v, al_tab, mask, 1.0f);
+        vote_cast(vote, wave, cmax);
+        __syncthreads();
+        int sh = 0;
+        if (__builtin_expect(vote_any<G::NW>(vote), 0)) {
+            sh = __builtin_amdgcn_readfirstlane(split_shift(block_max<G::NW>(cmax, vred)));
+            (void)write_planes(v, al_tab, mask, ldexpf(1.0f, -sh));
+            __syncthreads();
+        }
+        return sh;
     };
 
 #pragma unroll 1
@@ -270,23 +327,24 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
             }
         }
         __syncthreads();                               // window dead
-        // seam: h = act2(h * rs1 + b1) -> planes
+        // seam: h = act2(h * rs1 * 2^sh0 + b1) -> planes (2^sh0: the range guard of act0(y))
+        int sh2 = 0;
         {
             float hv[CB][16];
+            const float f0 = ldexpf(1.0f, sh0);
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int m = mrow0 + 8 * g;
-                const ss_f32x4 rs = *reinterpret_cast<const ss_f32x4*>(tu + m);
+                const ss_f32x4 rs = *reinterpret_cast<const ss_f32x4*>(tu + m) * f0;
                 const ss_f32x4 bb = *reinterpret_cast<const ss_f32x4*>(tu + C + m);
 #pragma unroll
                 for (int j = 0; j < CB; ++j)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) hv[j][4 * g + e] = acc[j][4 * g + e] * rs[e] + bb[e];
             }
-            write_planes(hv, tu + 2 * C, false);
+            sh2 = guarded_planes(hv, tu + 2 * C, false);
             zero_acc();
         }
-        __syncthreads();
         // phase 2: y += W2 . h
         {
             BF f[2];
@@ -298,10 +356,11 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
                 step(s, f[(s - S1) & 1]);
             }
         }
+        const float f2 = ldexpf(1.0f, sh2);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int m = mrow0 + 8 * g;
-            const ss_f32x4 rs = *reinterpret_cast<const ss_f32x4*>(tu + 3 * C + m);
+            const ss_f32x4 rs = *reinterpret_cast<const ss_f32x4*>(tu + 3 * C + m) * f2;
             const ss_f32x4 bb = *reinterpret_cast<const ss_f32x4*>(tu + 4 * C + m);
 #pragma unroll
             for (int j = 0; j < CB; ++j)
@@ -312,8 +371,7 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
         zero_acc();
         if (u + 1 < kSSUnits) {
             __syncthreads();                           // h dead
-            write_planes(yv, tu + 6 * C + 5 * C, true);    // next unit's act0(y)
-            __syncthreads();
+            sh0 = guarded_planes(yv, tu + 6 * C + 5 * C, true);    // next unit's act0(y)
         }
     }
 

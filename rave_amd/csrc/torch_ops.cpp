@@ -285,6 +285,182 @@ at::Tensor fir_op(at::Tensor x, at::Tensor h, int64_t stride, int64_t pad_left, 
     return y;
 }
 
+// ============================================================== operator seam
+// The cc.* operators the reference's blocks construct (rave/blocks.py:65,97,
+// 182,566; rave/__init__.py:14-27) and CachedPQMF's two convolutions
+// (rave/pqmf.py:234-284), as torch.ops.rave_amd.* -- the kernels behind the
+// rave_amd.cc nn.Modules.  Tensors on the GPU, time contiguous; launches on
+// torch's current HIP stream; every op goes through the C-ABI.
+void seam_tensor(const at::Tensor& t, const char* what) {
+    TORCH_CHECK_VALUE(t.is_cuda() && t.scalar_type() == at::kFloat, what, " must be a float32 GPU tensor");
+    TORCH_CHECK_VALUE(t.dim() == 3 && t.stride(2) == 1, what, " must be (B, C, T) with T contiguous");
+}
+void* cur_stream(const at::Tensor& t) { return c10::hip::getCurrentHIPStream(t.get_device()).stream(); }
+
+// rave_amd::pack_conv1d -- rave_conv1d_pack_weight / rave_conv1d_split_pack_weight
+// on the host (torch layout in: Conv1d (c_out, c_in, k), ConvTranspose1d
+// (c_in, c_out, k)); a CPU float tensor out
+at::Tensor pack_conv1d_op(at::Tensor w, int64_t c_in, int64_t c_out, int64_t kernel, int64_t stride, int64_t dilation,
+                          bool transposed, int64_t out_shift, int64_t precision) {
+    TORCH_CHECK_VALUE(precision == RAVE_PREC_F32 || precision == RAVE_PREC_SPLIT16, "precision: 0 (f32) or 1 (split16)");
+    at::Tensor wc = w.detach().to(at::kCPU, at::kFloat).contiguous();
+    TORCH_CHECK_VALUE(wc.numel() == c_in * c_out * kernel, "weight has ", wc.numel(), " values, expected ",
+                      c_in * c_out * kernel);
+    const bool sp = precision == RAVE_PREC_SPLIT16;
+    const int64_t n = sp ? rave_conv1d_split_packed_size((int)c_in, (int)c_out, (int)kernel, (int)stride, (int)dilation,
+                                                         transposed)
+                         : rave_conv1d_packed_size((int)c_in, (int)c_out, (int)kernel, (int)stride, (int)dilation,
+                                                   transposed);
+    TORCH_CHECK_NOT_IMPLEMENTED(n > 0, "conv1d: unsupported layer shape (c_in ", c_in, ", kernel ", kernel, ", stride ",
+                                stride, ", dilation ", dilation, ")");
+    at::Tensor out = at::zeros({n}, at::kFloat);
+    check(sp ? rave_conv1d_split_pack_weight(wc.data_ptr<float>(), (int)c_in, (int)c_out, (int)kernel, (int)stride,
+                                             (int)dilation, transposed, (int)out_shift, out.data_ptr<float>())
+             : rave_conv1d_pack_weight(wc.data_ptr<float>(), (int)c_in, (int)c_out, (int)kernel, (int)stride,
+                                       (int)dilation, transposed, (int)out_shift, out.data_ptr<float>()),
+          "pack_conv1d");
+    return out;
+}
+
+// rave_amd::conv1d -- rave_conv1d: act(x) conv W (+ bias) (+ residual).
+// transposed: the polyphase ConvTranspose1d (offline: pad_left 0, out_shift
+// stride/2; cached: x starts with one history column, pad_left 1, out_shift 0).
+at::Tensor conv1d_op(at::Tensor x, at::Tensor packed, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> alpha,
+                     c10::optional<at::Tensor> residual, int64_t c_out, int64_t kernel, int64_t stride, int64_t dilation,
+                     int64_t pad_left, int64_t pad_right, bool transposed, int64_t out_shift, int64_t act, double slope,
+                     int64_t precision) {
+    seam_tensor(x, "x");
+    c10::hip::HIPGuard g((c10::DeviceIndex)x.get_device());
+    TORCH_CHECK_VALUE(packed.device() == x.device(), "packed weight must be on x's device");
+    const int64_t B = x.size(0), c_in = x.size(1), T = x.size(2);
+    int64_t t_out;
+    if (transposed) {
+        t_out = (T - pad_left) * stride;
+    } else {
+        const int64_t span = (kernel - 1) * dilation + 1;
+        t_out = (T + pad_left + pad_right - span) / stride + 1;
+    }
+    TORCH_CHECK_VALUE(t_out > 0, "conv1d: input too short");
+    at::Tensor y = at::empty({B, c_out, t_out}, x.options());
+    rave_conv1d_args a{};
+    a.c_in = (int)c_in; a.c_out = (int)c_out; a.kernel = (int)kernel; a.stride = (int)stride; a.dilation = (int)dilation;
+    a.pad_left = (int)pad_left; a.pad_right = transposed ? 0 : (int)pad_right; a.transposed = transposed;
+    a.out_shift = (int)out_shift; a.act = (int)act; a.leaky_slope = (float)slope; a.batch = (int)B;
+    a.t_in = (int)T; a.t_out = (int)t_out; a.precision = (int)precision;
+    a.x = x.data_ptr<float>(); a.x_sb = x.stride(0); a.x_sc = x.stride(1);
+    a.y = y.data_ptr<float>(); a.y_sb = y.stride(0); a.y_sc = y.stride(1);
+    at::Tensor res;
+    if (residual.has_value()) {
+        res = *residual;
+        seam_tensor(res, "residual");
+        TORCH_CHECK_VALUE(res.size(0) == B && res.size(1) == c_out && res.size(2) == t_out, "residual shape");
+        a.residual = res.data_ptr<float>(); a.r_sb = res.stride(0); a.r_sc = res.stride(1);
+    }
+    a.weight = packed.data_ptr<float>();
+    at::Tensor bd, ad;
+    if (bias.has_value()) {
+        bd = bias->to(x.device(), at::kFloat).contiguous();
+        TORCH_CHECK_VALUE(bd.numel() == c_out, "bias must have c_out values");
+        a.bias = bd.data_ptr<float>();
+    }
+    if (act == RAVE_ACT_SNAKE) {
+        TORCH_CHECK_VALUE(alpha.has_value(), "Snake needs alpha");
+        ad = alpha->to(x.device(), at::kFloat).contiguous();
+        TORCH_CHECK_VALUE(ad.numel() == c_in, "alpha must have c_in values");
+        a.alpha = ad.data_ptr<float>();
+    }
+    const int64_t nws = rave_conv1d_workspace(&a);
+    if (nws < 0) check((int)nws, "conv1d workspace");
+    at::Tensor ws;
+    if (nws > 0) {
+        ws = at::zeros({nws}, x.options());      // split-K arrival counters start (and end) zero
+        a.partial = ws.data_ptr<float>();
+    }
+    check(rave_conv1d(&a, cur_stream(x)), "conv1d");
+    return y;
+}
+
+// rave_amd::pqmf_analysis -- CachedPQMF.forward (rave/pqmf.py:269-273): x (B, 1, T)
+// -> (B, n_out_bands, T / n_band); hkf (n_band, taps) on x's device
+at::Tensor pqmf_analysis_op(at::Tensor x, at::Tensor hkf, int64_t n_out_bands, int64_t pad_left, int64_t precision) {
+    seam_tensor(x, "x");
+    c10::hip::HIPGuard g((c10::DeviceIndex)x.get_device());
+    TORCH_CHECK_VALUE(x.size(1) == 1, "x must be (B, 1, T)");
+    at::Tensor h = hkf.to(x.device(), at::kFloat).contiguous();
+    const int64_t nb = h.size(0), B = x.size(0), T = x.size(2);
+    TORCH_CHECK_VALUE(T % nb == 0, "T must be a multiple of n_band");
+    at::Tensor y = at::empty({B, n_out_bands, T / nb}, x.options());
+    rave_pqmf_analysis_args a{};
+    a.n_band = (int)nb; a.taps = (int)h.size(1); a.n_out_bands = (int)n_out_bands; a.batch = (int)B;
+    a.t_in = (int)T; a.pad_left = (int)pad_left; a.t_out = (int)(T / nb); a.precision = (int)precision;
+    a.x = x.data_ptr<float>(); a.x_sb = x.stride(0);
+    a.y = y.data_ptr<float>(); a.y_sb = y.stride(0); a.y_sc = y.stride(1);
+    a.hkf = h.data_ptr<float>();
+    check(rave_pqmf_analysis(&a, cur_stream(x)), "pqmf_analysis");
+    return y;
+}
+
+// rave_amd::pqmf_synthesis -- CachedPQMF.inverse (rave/pqmf.py:275-284): x (B, n_band, F)
+// -> (B, 1, F * n_band); hki (n_band, n_band, taps).  x_len > F: x carries
+// cached history columns before the F frames (streaming, pad_left 0).
+at::Tensor pqmf_synthesis_op(at::Tensor x, at::Tensor hki, int64_t pad_left, int64_t frames, int64_t frame0,
+                             int64_t precision) {
+    seam_tensor(x, "x");
+    c10::hip::HIPGuard g((c10::DeviceIndex)x.get_device());
+    at::Tensor h = hki.to(x.device(), at::kFloat).contiguous();
+    const int64_t nb = h.size(0), B = x.size(0), XL = x.size(2);
+    TORCH_CHECK_VALUE(x.size(1) == nb, "x must have n_band channels");
+    const int64_t F = frames > 0 ? frames : XL;
+    at::Tensor y = at::empty({B, 1, F * nb}, x.options());
+    rave_pqmf_synthesis_args a{};
+    a.n_band = (int)nb; a.taps = (int)h.size(2); a.batch = (int)B; a.t_in = (int)F; a.pad_left = (int)pad_left;
+    a.mode = 0; a.frame0 = (int)frame0; a.x_len = (int)XL;
+    a.x = x.data_ptr<float>(); a.x_sb = x.stride(0); a.x_sc = x.stride(1);
+    a.y = y.data_ptr<float>(); a.y_sb = y.stride(0);
+    a.hki = h.data_ptr<float>(); a.precision = (int)precision;
+    check(rave_pqmf_synthesis(&a, cur_stream(x)), "pqmf_synthesis");
+    return y;
+}
+
+// rave_amd::rvq_encode / rvq_decode -- ResidualVectorQuantization.encode / decode
+// (rave/quantization.py:302-318): z (B, D, T), codebooks (n_q, K, D) -> idx (B, n_q, T) int64
+at::Tensor rvq_encode_op(at::Tensor z, at::Tensor codebooks) {
+    seam_tensor(z, "z");
+    c10::hip::HIPGuard g((c10::DeviceIndex)z.get_device());
+    at::Tensor cb = codebooks.to(z.device(), at::kFloat).contiguous();
+    TORCH_CHECK_VALUE(cb.dim() == 3 && cb.size(2) == z.size(1), "codebooks must be (n_q, K, D)");
+    const int64_t B = z.size(0), D = z.size(1), T = z.size(2), nq = cb.size(0);
+    at::Tensor idx = at::empty({B, nq, T}, z.options().dtype(at::kLong));
+    rave_rvq_args a{};
+    a.n_q = (int)nq; a.codebook_size = (int)cb.size(1); a.dim = (int)D; a.batch = (int)B; a.t_len = (int)T;
+    a.codebooks = cb.data_ptr<float>();
+    a.z = z.data_ptr<float>(); a.z_sb = z.stride(0); a.z_sc = z.stride(1);
+    a.idx = idx.data_ptr<int64_t>(); a.i_sb = nq * T; a.i_sq = T;
+    const int64_t nw = rave_rvq_workspace(&a);
+    if (nw < 0) check((int)nw, "rvq_workspace");
+    at::Tensor work = at::empty({std::max<int64_t>(nw, 1)}, z.options());
+    a.work = work.data_ptr<float>();
+    check(rave_rvq_encode(&a, cur_stream(z)), "rvq_encode");
+    return idx;
+}
+
+at::Tensor rvq_decode_op(at::Tensor idx, at::Tensor codebooks) {
+    TORCH_CHECK_VALUE(idx.is_cuda() && idx.scalar_type() == at::kLong && idx.dim() == 3, "idx must be (B, n_q, T) int64");
+    c10::hip::HIPGuard g((c10::DeviceIndex)idx.get_device());
+    at::Tensor ic = idx.contiguous();
+    at::Tensor cb = codebooks.to(idx.device(), at::kFloat).contiguous();
+    TORCH_CHECK_VALUE(cb.dim() == 3 && cb.size(0) == idx.size(1), "codebooks must be (n_q, K, D)");
+    const int64_t B = idx.size(0), nq = idx.size(1), T = idx.size(2), D = cb.size(2);
+    at::Tensor y = at::empty({B, D, T}, idx.options().dtype(at::kFloat));
+    rave_rvq_args a{};
+    a.n_q = (int)nq; a.codebook_size = (int)cb.size(1); a.dim = (int)D; a.batch = (int)B; a.t_len = (int)T;
+    a.codebooks = cb.data_ptr<float>();
+    a.idx = ic.data_ptr<int64_t>(); a.i_sb = nq * T; a.i_sq = T;
+    a.y = y.data_ptr<float>(); a.y_sb = D * T; a.y_sc = T;
+    check(rave_rvq_decode(&a, cur_stream(idx)), "rvq_decode");
+    return y;
+}
+
 using State = std::tuple<std::vector<int64_t>, double, std::vector<std::string>, std::vector<at::Tensor>, at::Tensor,
                          int64_t, int64_t>;
 
@@ -292,6 +468,17 @@ using State = std::tuple<std::vector<int64_t>, double, std::vector<std::string>,
 
 TORCH_LIBRARY(rave_amd, lib) {
     lib.def("fir(Tensor x, Tensor h, int stride, int pad_left, int pad_right, Tensor? hist) -> Tensor", &fir_op);
+    lib.def("pack_conv1d(Tensor w, int c_in, int c_out, int kernel, int stride, int dilation, bool transposed, "
+            "int out_shift, int precision) -> Tensor", &pack_conv1d_op);
+    lib.def("conv1d(Tensor x, Tensor packed, Tensor? bias, Tensor? alpha, Tensor? residual, int c_out, int kernel, "
+            "int stride, int dilation, int pad_left, int pad_right, bool transposed, int out_shift, int act, "
+            "float slope, int precision) -> Tensor", &conv1d_op);
+    lib.def("pqmf_analysis(Tensor x, Tensor hkf, int n_out_bands, int pad_left, int precision) -> Tensor",
+            &pqmf_analysis_op);
+    lib.def("pqmf_synthesis(Tensor x, Tensor hki, int pad_left, int frames, int frame0, int precision) -> Tensor",
+            &pqmf_synthesis_op);
+    lib.def("rvq_encode(Tensor z, Tensor codebooks) -> Tensor", &rvq_encode_op);
+    lib.def("rvq_decode(Tensor idx, Tensor codebooks) -> Tensor", &rvq_decode_op);
     lib.class_<Engine>("Engine")
         .def(torch::init<std::vector<int64_t>, double, std::vector<std::string>, std::vector<at::Tensor>, at::Tensor,
                          int64_t, int64_t>())

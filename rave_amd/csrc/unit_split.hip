@@ -97,7 +97,9 @@ template <int C, int WGN, int MI, int KG = 1, int CB = 2> struct USGeo {
     static constexpr int XPLANE = XW_MAX * PH * 2;    // bytes per f16 plane
     static constexpr int HPLANE = BN * PH * 2;
     static constexpr int PLANES = 2 * (XPLANE > HPLANE ? XPLANE : HPLANE);
-    static constexpr int LDS = PLANES + 6 * C * 4;    // + per-row table: rs1 b1 a2 | rs2 b2 a0
+    // + per-row table: rs1 b1 a2 | rs2 b2 a0, + range-guard votes (16 B) and wave maxima (16 floats)
+    static constexpr int TAB = PLANES, VOTE = PLANES + 6 * C * 4, VRED = VOTE + 16;
+    static constexpr int LDS = VRED + 64;
     static constexpr int G8 = C / 8;                  // 8-channel groups per window row
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;
     static constexpr int R = 3;                       // weight ring depth (K-steps)
@@ -115,7 +117,9 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     extern __shared__ __attribute__((aligned(16))) char lds[];
     _Float16* ph = reinterpret_cast<_Float16*>(lds);
     _Float16* pl = reinterpret_cast<_Float16*>(lds + G::PLANES / 2);
-    float* tab = reinterpret_cast<float*>(lds + G::PLANES);   // [6][C]
+    float* tab = reinterpret_cast<float*>(lds + G::TAB);      // [6][C]
+    unsigned char* vote = reinterpret_cast<unsigned char*>(lds + G::VOTE);
+    float* vred = reinterpret_cast<float*>(lds + G::VRED);
 
     US_STAMP(0);
     const int tid = threadIdx.x;
@@ -135,6 +139,7 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
 
     const auto xrs = us_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);
     const auto wrs = us_rsrc(a.w, a.w_bytes);
+    int sh0 = 0, sh2 = 0;                            // range-guard shifts of the two GEMMs' B operands
 
     // ------------------------------------------------------------ weight ring
     // this wave's m-blocks MI*wm .. MI*wm+MI-1; fragment (mb, s, plane) at ((mb*ST + s)*2 + plane) KB
@@ -161,7 +166,10 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     }
 
     // ------------------------------------------------------------ prologue: act0(x) window
-    {
+    // (xs: the range guard's power-of-two scale; returns max |act0(x) xs| of the
+    // thread's values)
+    auto stage_window = [&](float xs) __attribute__((always_inline)) {
+        float cmax = 0.f;
         float rx[XT][8];
 #pragma unroll
         for (int i = 0; i < XT; ++i) {
@@ -186,8 +194,9 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
                 const float al = SNAKE ? a.a0[min(g * 8 + v, C - 1)] : 0.f;   // L1-hot
-                v8[v] = ok ? us_act<SNAKE>(rx[i][v], slope, al) : 0.f;
+                v8[v] = ok ? us_act<SNAKE>(rx[i][v], slope, al) * xs : 0.f;
             }
+            cmax = fmaxf(cmax, absmax8(v8));
             const us_h8 hi = __builtin_convertvector(v8, us_h8);
             const us_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, us_f32x8)) * 2048.0f, us_h8);
             if (e < ntask) {
@@ -195,8 +204,39 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
                 *reinterpret_cast<us_h8*>(pl + w * PH + g * 8) = lo;
             }
         }
+        return cmax;
+    };
+    // range guard: when a wave saw |act0(x)| >= 2^15 the window is staged again
+    // as act0(x) * 2^-sh0 by a rolled loop (small code, few registers: rare)
+    {
+        const float cmax = stage_window(1.0f);
+        vote_cast(vote, wave, cmax);
+        __syncthreads();
+        if (__builtin_expect(vote_any<G::NW>(vote), 0)) {
+            sh0 = __builtin_amdgcn_readfirstlane(split_shift(block_max<G::NW>(cmax, vred)));
+            const float xs = ldexpf(1.0f, -sh0);
+#pragma nounroll
+            for (int e = tid; e < ntask; e += NT) {
+                const int g = (int)(((unsigned)e * a.xw_magic) >> 24);
+                const int w = e - g * XW;
+                const bool ok = (t0 + w >= 0) && (t0 + w < a.T);
+                const int t = min(max(t0 + w, 0), a.T - 1);
+                us_f32x8 v8;
+#pragma unroll
+                for (int v = 0; v < 8; ++v) {
+                    const int c = min(g * 8 + v, C - 1);
+                    const float xv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        xrs, (unsigned)(c * a.x_sc + t) * 4u, 0, 0));
+                    v8[v] = ok ? us_act<SNAKE>(xv, slope, SNAKE ? a.a0[c] : 0.f) * xs : 0.f;
+                }
+                const us_h8 hi = __builtin_convertvector(v8, us_h8);
+                const us_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, us_f32x8)) * 2048.0f, us_h8);
+                *reinterpret_cast<us_h8*>(ph + w * PH + g * 8) = hi;
+                *reinterpret_cast<us_h8*>(pl + w * PH + g * 8) = lo;
+            }
+            __syncthreads();
+        }
     }
-    __syncthreads();
     US_STAMP(1);
 
     // ------------------------------------------------------------ K loop (both phases)
@@ -300,27 +340,47 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     US_STAMP(2);
 
     // ------------------------------------------------------------ seam: h = act2(h*rs1 + b1) -> planes
-    if (KG == 1 || kg == 0) {
+    // (phase 1 ran on act0(x) 2^-sh0: its scale 2^sh0 rides on rs1; xs = the
+    // range guard's scale of h; returns max |h xs| of the thread's values)
+    const float f0 = ldexpf(1.0f, sh0);
+    auto seam = [&](float xs) __attribute__((always_inline)) {
+        float cmax = 0.f;
+        if (KG == 1 || kg == 0) {
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
+            for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int m = mrow0 + 32 * i + 8 * g;
-                const us_f32x4 rs = *reinterpret_cast<const us_f32x4*>(tab + m);
-                const us_f32x4 bb = *reinterpret_cast<const us_f32x4*>(tab + C + m);
-                us_f32x4 al = {0.f, 0.f, 0.f, 0.f};
-                if constexpr (SNAKE) al = *reinterpret_cast<const us_f32x4*>(tab + 2 * C + m);
+                for (int g = 0; g < 4; ++g) {
+                    const int m = mrow0 + 32 * i + 8 * g;
+                    const us_f32x4 rs = *reinterpret_cast<const us_f32x4*>(tab + m) * f0;
+                    const us_f32x4 bb = *reinterpret_cast<const us_f32x4*>(tab + C + m);
+                    us_f32x4 al = {0.f, 0.f, 0.f, 0.f};
+                    if constexpr (SNAKE) al = *reinterpret_cast<const us_f32x4*>(tab + 2 * C + m);
 #pragma unroll
-                for (int j = 0; j < CB; ++j) {
-                    us_f32x4 v;
+                    for (int j = 0; j < CB; ++j) {
+                        us_f32x4 v;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = us_act<SNAKE>(acc[i][j][4 * g + e] * rs[e] + bb[e], slope, al[e]);
-                    const us_h4 hv = __builtin_convertvector(v, us_h4);
-                    const us_h4 lv = __builtin_convertvector((v - __builtin_convertvector(hv, us_f32x4)) * 2048.0f, us_h4);
-                    *reinterpret_cast<us_h4*>(ph + (col0 + 32 * j) * PH + m) = hv;
-                    *reinterpret_cast<us_h4*>(pl + (col0 + 32 * j) * PH + m) = lv;
+                        for (int e = 0; e < 4; ++e)
+                            v[e] = us_act<SNAKE>(acc[i][j][4 * g + e] * rs[e] + bb[e], slope, al[e]) * xs;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) cmax = fmaxf(cmax, fabsf(v[e]));
+                        const us_h4 hv = __builtin_convertvector(v, us_h4);
+                        const us_h4 lv = __builtin_convertvector((v - __builtin_convertvector(hv, us_f32x4)) * 2048.0f, us_h4);
+                        *reinterpret_cast<us_h4*>(ph + (col0 + 32 * j) * PH + m) = hv;
+                        *reinterpret_cast<us_h4*>(pl + (col0 + 32 * j) * PH + m) = lv;
+                    }
                 }
-            }
+        }
+        return cmax;
+    };
+    {                                            // range guard of h (rare path: h * 2^-sh2)
+        const float cmax = seam(1.0f);
+        vote_cast(vote, wave, cmax);
+        __syncthreads();
+        if (__builtin_expect(vote_any<G::NW>(vote), 0)) {
+            sh2 = __builtin_amdgcn_readfirstlane(split_shift(block_max<G::NW>(cmax, vred)));
+            (void)seam(ldexpf(1.0f, -sh2));
+            __syncthreads();
+        }
     }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -328,7 +388,6 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
         for (int j = 0; j < CB; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    __syncthreads();
     US_STAMP(3);
 
     if (KG == 1 || kg == 0) kloop(IC<0>{}, IC<S1 / KG>{}, IC<ST / KG>{});
@@ -340,6 +399,7 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     // ------------------------------------------------------------ epilogue: y*rs2 + b2 + x
     // every residual load issued before the first store (one exposed latency)
     {
+        const float f2 = ldexpf(1.0f, sh2);
         const auto yrs = us_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
         float res[MI][CB][16];
 #pragma unroll
@@ -360,7 +420,7 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int m = mrow0 + 32 * i + 8 * g;
-                const us_f32x4 rs = *reinterpret_cast<const us_f32x4*>(tab + 3 * C + m);
+                const us_f32x4 rs = *reinterpret_cast<const us_f32x4*>(tab + 3 * C + m) * f2;
                 const us_f32x4 bb = *reinterpret_cast<const us_f32x4*>(tab + 4 * C + m);
 #pragma unroll
                 for (int j = 0; j < CB; ++j) {

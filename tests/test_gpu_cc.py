@@ -1,0 +1,145 @@
+"""The operator-level seam (rave_amd.cc + rave_amd.modules): the reference's
+module tree written against ``cc.Conv1d`` / ``cc.ConvTranspose1d`` /
+``CachedPQMF`` runs on the HIP kernels through torch.ops.rave_amd.* and
+reproduces the reference's fixtures -- per layer (offline), block for block
+(cached_conv streaming, causal and centred), and RVQ indices.  Runs on an
+MI355X only (``-m gpu``)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def maxabs(a, b):
+    return float(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)).max())
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _tree(cfg, g, golden, dev, cached=False, precision="f32"):
+    from rave_amd import cc
+    from rave_amd.modules import RAVEModules, load_reference_state
+    from rave_amd.weights import init_params
+    cc.use_cached_conv(cached)
+    cc.set_precision(precision)
+    try:
+        m = RAVEModules(cfg, g["speaker"], hk=golden("pqmf")["hk"])
+    finally:
+        cc.use_cached_conv(False)
+        cc.set_precision("f32")
+    load_reference_state(m, init_params(cfg, seed=int(g["seed"])))
+    return m.to(dev).eval()
+
+
+@pytest.mark.parametrize("precision", ["f32", "split16"])
+def test_cc_tree_per_layer_golden(dev, golden, precision):
+    """Every conv of the v2 tree (capacity 8) against the reference's per-layer
+    outputs (tests/golden/v2_small_layers.npz, forward hooks on the reference
+    modules of the same names); z and y within 1e-4; the scripted tree equal."""
+    from rave_amd import cc
+    from rave_amd import config as rcfg
+    cfg = rcfg.v2(capacity=8)
+    g = golden("v2_small_layers")
+    m = _tree(cfg, g, golden, dev, precision=precision)
+    got = {}
+    hooks = [mod.register_forward_hook(lambda mod, i, o, n=n: got.__setitem__(n, o.detach().cpu().numpy()))
+             for n, mod in m.named_modules() if isinstance(mod, (cc.Conv1d, cc.ConvTranspose1d))]
+    with torch.no_grad():
+        z = m.encode(torch.from_numpy(g["x"]).to(dev))
+        y = m.decode(torch.from_numpy(g["z"]).to(dev))
+    for h in hooks:
+        h.remove()
+    layers = [k[len("layer/"):] for k in g if k.startswith("layer/")]
+    assert layers and set(layers) <= set(got), sorted(set(layers) - set(got))[:5]
+    worst = 0.0
+    for name in layers:
+        ref = g["layer/" + name]
+        err = maxabs(got[name], ref)
+        worst = max(worst, err / max(1.0, float(np.abs(ref).max())))
+        assert err <= 2e-5 * max(1.0, float(np.abs(ref).max())), (name, err)
+    ez = maxabs(z.cpu().numpy()[:, :cfg.latent_size], g["z"][:, :cfg.latent_size])
+    ey = maxabs(y.cpu().numpy(), g["y"])
+    print(f"\n[cc] v2 cap 8 {precision}: {len(layers)} layers, worst rel {worst:.2e}; z {ez:.2e} y {ey:.2e}")
+    assert ez < TOL and ey < TOL
+    ts = torch.jit.script(m)
+    with torch.no_grad():
+        ys = ts.decode(torch.from_numpy(g["z"]).to(dev))
+    assert maxabs(ys.cpu().numpy(), y.cpu().numpy()) == 0.0
+
+
+@pytest.mark.parametrize("name,fixture", [("causal", "causal_stream"), ("v2", "v2_stream")])
+def test_cc_cached_tree_streams_reference(dev, golden, name, fixture):
+    """cc.use_cached_conv(True) before construction: the tree streams 2048-sample
+    blocks and matches the reference's cached_conv run block for block
+    (causal, and the reference's default centred model)."""
+    from rave_amd import config as rcfg
+    cfg = rcfg.get_config(name)
+    g = golden(fixture)
+    m = _tree(cfg, g, golden, dev, cached=True)
+    blk = int(g["block"])
+    Fz = blk // cfg.hop
+    x = torch.from_numpy(g["x"]).to(dev)
+    z = torch.from_numpy(g["z"]).to(dev)
+    nb = x.shape[-1] // blk
+    with torch.no_grad():
+        zs = torch.cat([m.encode(x[..., i * blk:(i + 1) * blk]) for i in range(nb)], -1)
+        ys = torch.cat([m.decode(z[..., i * Fz:(i + 1) * Fz]) for i in range(nb)], -1)
+    ez, ey = maxabs(zs.cpu().numpy(), g["z_stream"]), maxabs(ys.cpu().numpy(), g["y_stream"])
+    print(f"\n[cc] cached {name} tree vs reference streaming: z {ez:.2e} y {ey:.2e}")
+    assert ez < TOL and ey < TOL
+
+
+def test_cc_rvq_ops_golden(dev, golden):
+    """cc.rvq_encode / rvq_decode against the reference's RVQ fixture (indices
+    exact outside the tie margin)."""
+    from rave_amd import cc
+    from rave_amd import config as rcfg
+    from rave_amd.weights import init_params
+    g = golden("rvq")
+    cfg = rcfg.discrete()
+    params = init_params(cfg, seed=int(g["seed"]))
+    cbs = torch.from_numpy(np.stack([params[f"encoder.rvq.layers.{i}._codebook.embed"] for i in range(16)])).to(dev)
+    z = torch.from_numpy(g["z"]).to(dev)
+    idx = cc.rvq_encode(z, cbs)
+    zq = cc.rvq_decode(torch.from_numpy(g["idx"]).to(dev), cbs)
+    torch.cuda.synchronize()
+    got, ref = idx.cpu().numpy(), g["idx"]
+    B, _, T = z.shape
+    gap = g["gap"].reshape(16, B, T).transpose(1, 0, 2)
+    mism = got != ref
+    assert (gap[mism] < 1e-3).all()
+    assert maxabs(zq.cpu().numpy(), g["zq"]) < 1e-5
+
+
+def test_cc_conv_module_contract(dev):
+    """cc.Conv1d / ConvTranspose1d keep torch's parameter layout (weight_norm
+    applies; a changed weight is re-packed) and refuse shapes the kernels do
+    not take."""
+    from rave_amd import cc
+    from oracle.rave_oracle import conv1d, conv_transpose1d
+    conv = cc.Conv1d(16, 32, 3, padding=cc.get_padding(3, dilation=2), dilation=2).to(dev)
+    assert tuple(conv.weight.shape) == (32, 16, 3)
+    x = torch.randn(2, 16, 100, device=dev)
+    ref = conv1d(x.cpu().double().numpy(), conv.weight.detach().cpu().numpy(), conv.bias.detach().cpu().numpy(),
+                 1, 2, (2, 2))
+    assert maxabs(conv(x).detach().cpu().numpy(), ref) < 1e-5
+    with torch.no_grad():
+        conv.weight.mul_(2.0)                          # in-place change: re-packed on the next call
+    assert maxabs(conv(x).detach().cpu().numpy(), conv1d(x.cpu().double().numpy(),
+                  conv.weight.detach().cpu().numpy(), conv.bias.detach().cpu().numpy(), 1, 2, (2, 2))) < 1e-5
+    wn = torch.nn.utils.weight_norm(cc.Conv1d(16, 8, 1).to(dev))
+    assert hasattr(wn, "weight_g") and tuple(wn(x).shape) == (2, 8, 100)
+    ct = cc.ConvTranspose1d(16, 8, 8, stride=4, padding=2).to(dev)
+    refc = conv_transpose1d(x.cpu().double().numpy(), ct.weight.detach().cpu().numpy(), 4, 2, None)
+    assert maxabs(ct(x).detach().cpu().numpy(), refc) < 1e-5
+    with pytest.raises(NotImplementedError):
+        cc.ConvTranspose1d(16, 8, 5, stride=2, padding=1)
