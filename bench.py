@@ -441,7 +441,7 @@ def main():
     exact = None
     if a.precision not in ("f32", "f32_tuned") and not a.no_f32:
         # exact fp32 on every op, with the same launch-configuration autotuning as the headline
-        exact, y_f32 = run_mode(a, cfg, params, spk, "f32_tuned", x, dev, world, rank, False)
+        exact, y_f32 = run_mode(a, cfg, params, spk, "f32_tuned", x, dev, world, rank, rank == 0)
         # the same input through both arithmetic modes (north star: <= 1e-4 max-abs)
         exact["headline_vs_f32_max_abs"] = float((y_head - y_f32).abs().max())
         del y_f32

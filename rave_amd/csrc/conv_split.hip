@@ -441,10 +441,11 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
     // wave issues XI window DMAs, then per own K-step 2*NJ weight loads.  The
     // body is instantiated per K-group (its K-step range fixes the counts);
     // both groups pass the same barriers.
-    // guarded: the per-chunk range guard (second attempt only); otherwise the
-    // chunks' overflow votes are just OR-ed into `over` (no LDS traffic)
-    auto body = [&](auto gtag, bool guarded, bool& over) __attribute__((always_inline)) {
+    // GUARDED (compile time): the per-chunk range guard of the rare second
+    // attempt; the first attempt's loop carries no guard code at all
+    auto body = [&](auto gtag, auto guardtag) __attribute__((always_inline)) {
         constexpr int GG = decltype(gtag)::value;
+        constexpr bool guarded = decltype(guardtag)::value != 0;
         constexpr int KS = G::ks_of(GG);                // own K-steps per chunk
         constexpr int ST0 = G::st_of(GG);               // first own K-step
         constexpr int WR = KS * NJ * 2, XI = G::XI;
@@ -455,8 +456,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
         wait_vm<(NS - 1) * XI + WR>();          // window c_begin landed
         __syncthreads();
         float cmax = convert(c_begin, 0, 0);
-        if (guarded) cast_vote(0, cmax);
-        else over |= cmax >= kSplitLimit;
+        if constexpr (guarded) cast_vote(0, cmax);
         wait_vm<(NS - 2) * XI + WR>();          // window c_begin+1 landed
         __syncthreads();
         stamp(1);
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
             // its raw window is still in `stage` until the DMA below): the vote
             // read rides with the first fragment reads
             int sh_cur = 0;
-            if (__builtin_expect(guarded && read_vote(pb), 0)) {
+            if (guarded && __builtin_expect(read_vote(pb), 0)) {
                 sh_cur = rescue(c, stage, pb, cmax);
                 read_a(pb, ST0, f[0]);
             }
@@ -521,9 +521,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                 }
             }
             if (__builtin_expect(sh_cur != 0, 0)) scale_acc(ldexpf(1.0f, sh_cur));
-            if (c + 1 < c_end) {
-                if (guarded) cast_vote(pb ^ 1, cmax);
-                else over |= cmax >= kSplitLimit;
+            if constexpr (guarded) {
+                if (c + 1 < c_end) cast_vote(pb ^ 1, cmax);
             }
             // window c+2 landed: younger are, per chunk since its issue, the
             // weight refills and the next windows
@@ -533,37 +532,45 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
             if (c == c_begin) stamp(2);
         }
     };
-    // Range guard, two attempts over one copy of the K loop: the first runs
-    // with no per-chunk check; only when some chunk of the tile reached
-    // kSplitLimit (one vote per tile) does the loop run again from its
-    // prologue with the per-chunk rescue (rare: activations past 2^15).
-    bool guarded = false;
-#pragma nounroll
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        bool over = false;
-        if (kg == 0) body(IC<0>{}, guarded, over);
+    // Range guard, two attempts: the first runs the plain K loop (no guard
+    // code); an operand past the f16 range became inf in its hi half, so it
+    // shows as a non-finite partial sum.  Only when some wave of the tile holds
+    // one (one vote per tile) does the loop run again from its prologue with
+    // the per-chunk rescue (rare: activations past 2^15; a genuine inf / NaN
+    // input takes the second attempt too and passes through, as in fp32).
+    auto run_k = [&](auto guardtag) __attribute__((always_inline)) {
+        if (kg == 0) body(IC<0>{}, guardtag);
         else if constexpr (KG >= 2) {
-            if (kg == 1) body(IC<1>{}, guarded, over);
+            if (kg == 1) body(IC<1>{}, guardtag);
             else if constexpr (KG == 4) {
-                if (kg == 2) body(IC<2>{}, guarded, over);
-                else body(IC<3>{}, guarded, over);
+                if (kg == 2) body(IC<2>{}, guardtag);
+                else body(IC<3>{}, guardtag);
             }
         }
         wait_vm<0>();                       // drain the ring (epilogue loads / a second attempt)
-        if (!RAVE_SPLIT_GUARD || guarded) break;
-        const bool wover = __builtin_amdgcn_ballot_w64(over) != 0;
-        if (lane == 0) vote[32 + wave] = wover ? 1 : 0;
-        __syncthreads();
-        const bool tover = vote_any<NW>(vote + 32);
-        if (__builtin_expect(!tover, 1)) break;
-        guarded = true;
-        __syncthreads();                    // every wave read the tile vote
+    };
+    run_k(IC<0>{});
+    if (RAVE_SPLIT_GUARD) {
+        bool bad = false;
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+                for (int r = 0; r < 16; ++r) bad |= !__builtin_isfinite(acc[i][j][r]);
+        const bool wover = __builtin_amdgcn_ballot_w64(bad) != 0;
+        if (lane == 0) vote[32 + wave] = wover ? 1 : 0;
+        __syncthreads();
+        if (__builtin_expect(vote_any<NW>(vote + 32), 0)) {
+            __syncthreads();                // every wave read the tile vote
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            run_k(IC<1>{});
+        }
     }
     stamp(3);
     if constexpr (KG >= 2) {

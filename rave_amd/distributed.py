@@ -38,10 +38,12 @@ def shard_bounds(n: int, rank: int, size: int) -> Tuple[int, int]:
 
 def gather_latents(z_local: torch.Tensor, out: Optional[torch.Tensor] = None,
                    group=None) -> torch.Tensor:
-    """All-gather equally sized per-rank latent shards along dim 0."""
-    rank, size = world()
-    if size == 1:
+    """All-gather equally sized per-rank latent shards along dim 0.  Without a
+    process group this is the identity; with one (any size, world size 1
+    included) the shards always go through the backend's collective."""
+    if not (dist.is_available() and dist.is_initialized()):
         return z_local
+    size = dist.get_world_size(group)
     z_local = z_local.contiguous()
     if out is None:
         out = torch.empty((size * z_local.shape[0],) + tuple(z_local.shape[1:]),
@@ -103,7 +105,7 @@ class ShardedRunner:
 
     def _gather(self, t: torch.Tensor, sizes: List[int]) -> torch.Tensor:
         rank, size = world()
-        if size == 1:
+        if not (dist.is_available() and dist.is_initialized()):
             return t
         narrow = self._narrow_codes()
         # codes travel as int16 (1024-entry codebooks), viewed as bytes: every

@@ -151,3 +151,19 @@ def test_adain_style_transfer(golden, name, cfg):
             assert rel(st[b], g[f"final/{n}.{b}"]) < 1e-4, (n, b)
         assert st["num_update_x"] == float(g[f"final/{n}.num_update_x"][0])
         assert st["num_update_y"] == float(g[f"final/{n}.num_update_y"][0])
+
+
+def test_manifest_covers_every_fixture():
+    """Provenance: every committed fixture is listed in MANIFEST.json with the
+    sha256 prefix make_golden.py recorded when the reference produced it."""
+    import hashlib
+    import json
+    import os
+    d = os.path.join(os.path.dirname(__file__), "golden")
+    with open(os.path.join(d, "MANIFEST.json")) as fh:
+        files = json.load(fh)["files"]
+    npz = sorted(f for f in os.listdir(d) if f.endswith(".npz"))
+    assert sorted(files) == npz
+    for f in npz:
+        with open(os.path.join(d, f), "rb") as fh:
+            assert hashlib.sha256(fh.read()).hexdigest()[:16] == files[f], f
