@@ -49,7 +49,7 @@ SR = 48000
 # GEMM-shaped kernel families of a step: name -> (kernels, peak in fp32-op TFLOP/s).
 # The names match tools/rocprof_summary.py's grouping of rocprofv3 kernel rows.
 FAMILIES = {
-    "conv_f32": ("conv1d_mfma_kernel + conv1d_splitk_reduce_kernel, fp32 MFMA 32x32x2",
+    "conv_f32": ("conv1d_mfma_kernel / conv1d_ring_f32_kernel (+ split-K reduce), exact fp32 MFMA 32x32x2",
                  PEAK_FP32_TFLOPS),
     "conv_split16": ("conv1d_split_kernel + split_reduce_kernel, split-f16 MFMA 32x32x16 (3 per fp32 MAC)",
                      PEAK_SPLIT16_TFLOPS),
@@ -63,6 +63,10 @@ FAMILIES = {
                               PEAK_SPLIT16_TFLOPS),
     "pqmf_synthesis_split16": ("pqmf_synthesis_split_kernel, split-f16 MFMA 16x16x32 (3 per fp32 MAC)",
                                PEAK_SPLIT16_TFLOPS),
+    "head_split16": ("encoder_head_kernel: PQMF analysis (phase-packed) + EncoderV2's first conv, split-f16 "
+                     "MFMA 16x16x32 / 32x32x16", PEAK_SPLIT16_TFLOPS),
+    "tail_split16": ("decoder_tail_kernel: GeneratorV2's last conv + epilogue + PQMF synthesis, split-f16 "
+                     "MFMA 32x32x16 / 16x16x32", PEAK_SPLIT16_TFLOPS),
 }
 
 
@@ -79,6 +83,10 @@ def op_family(kind: int, precision: int) -> str:
         return "pqmf_analysis_" + prec
     if kind == N.OP_PQMF_SYNTHESIS:
         return "pqmf_synthesis_" + prec
+    if kind == N.OP_HEAD:
+        return "head_split16"
+    if kind == N.OP_TAIL:
+        return "tail_split16"
     return "other"
 
 
@@ -139,8 +147,9 @@ def cpu_baseline(cfg, params, spk, B: int, T: int, seconds: float, threads: int)
 
 
 DTYPE = {"f32": "fp32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32)",
-         "f32_tuned": "fp32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32; launch configurations and fused/unfused "
-                      "units autotuned)",
+         "f32_tuned": "fp32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32 on every op; per conv the faster of the "
+                      "register-staged kernel and the LDS-DMA ring kernel, launch configurations and "
+                      "fused/unfused units autotuned)",
          "split16": "fp32 I/O, split-f16 GEMMs (3 f16 MFMA passes hi*hi+hi*lo+lo*hi on ~22-bit operands, "
                     "fp32 accumulate)",
          "auto": "fp32 I/O; per op the faster of exact-fp32 MFMA and split-f16 GEMMs (3 f16 MFMA passes on "

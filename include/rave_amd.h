@@ -27,6 +27,10 @@
  *                        rave/model.py:618-620.
  *   rave_rvq_encode /    ResidualVectorQuantization.encode / decode
  *   rave_rvq_decode      rave/quantization.py:302-318.
+ *   rave_encoder_head    rave_pqmf_analysis + EncoderV2's first conv (+ the speaker
+ *                        concat) in one launch (split-f16): RAVE.encode's head.
+ *   rave_decoder_tail    GeneratorV2's last act + conv + epilogue +
+ *                        rave_pqmf_synthesis in one launch (split-f16).
  *   rave_plan_*          RAVE.encode / decode / forward rave/model.py:594-634 as
  *                        one pre-built launch sequence (the module graph).
  */
@@ -40,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 11
+#define RAVE_ABI_VERSION 12
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 
@@ -69,6 +73,12 @@ enum { RAVE_ACT_NONE = 0, RAVE_ACT_LEAKY = 1, RAVE_ACT_SNAKE = 2 };
  *                      5.3x the fp32 MFMA rate.  Weights must be packed with the
  *                      *_split_* packers. */
 enum { RAVE_PREC_F32 = 0, RAVE_PREC_SPLIT16 = 1 };
+/*   RAVE_PREC_F32_RING exact fp32 (v_mfma_f32_32x32x2_f32) on the split16 kernels'
+ *                      staging machinery (LDS-DMA window ring, register weight ring,
+ *                      K-groups, the same tiles and launch configurations); weights
+ *                      packed with rave_conv1d_ring_pack_weight (sizes as the split
+ *                      image).  Value 4: 2 and 3 are model-level modes below. */
+#define RAVE_PREC_F32_RING 4
 
 const char* rave_last_error(void);
 int rave_abi_version(void);
@@ -149,6 +159,10 @@ int64_t rave_conv1d_split_packed_size(int c_in, int c_out, int kernel, int strid
                                       int transposed);
 int rave_conv1d_split_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
                                   int dilation, int transposed, int out_shift, float* packed);
+/* RAVE_PREC_F32_RING weight image: the split image's layout with 8 fp32 values
+ * per lane and K-step (4 in each 1 KB slot) and row scales 1 */
+int rave_conv1d_ring_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
+                                 int dilation, int transposed, int out_shift, float* packed);
 int rave_conv1d(const rave_conv1d_args* a, void* stream);
 
 /* ---------------------------------------------------------------- PQMF
@@ -339,6 +353,48 @@ typedef struct rave_stack_args {
 int rave_stack_supported(int channels);
 int rave_residual_stack(const rave_stack_args* a, void* stream);
 
+/* ---------------------------------------------------------------- path edges (split-f16)
+ * The PQMF end of each half of the path fused with the conv next to it; one
+ * launch each, split-f16 arithmetic (RAVE_PREC_SPLIT16: every operand block is
+ * scaled by a power of two from its workgroup maximum, so any finite input is
+ * in range).  The intermediate never reaches HBM.
+ *
+ * rave_encoder_head: CachedPQMF.forward + band slice (rave/pqmf.py:269-273,
+ * rave/model.py:613) then EncoderV2's first conv (rave/blocks.py:533-536):
+ *   bands = rave_pqmf_analysis(x, n_out_bands = conv_c_in, pad pqmf_pad_left)
+ *   y[b, m, t] = bias[m] + sum_{c, j} W[m, c, j] * bands[b, c, t + j - conv_pad_left]
+ *   x: audio (B, 1, 16 * frames), x_sb; y: (B, conv_c_out, frames).
+ *   filter: hkf (16, 513); conv_c_in <= 8 bands, conv_c_out <= 64, conv_kernel 7.
+ *   fill_channels > 0: also fill_y[b, c, t] = fill_values[c], t < fill_t (the
+ *   speaker concat of RAVE.encode, rave/model.py:618-620).
+ * rave_decoder_tail: GeneratorV2's act + conv (rave/blocks.py:691-696), its
+ * epilogue (:699-707) and CachedPQMF.inverse (rave/pqmf.py:275-284):
+ *   w = bias + conv_k(act(x))          conv_c_in 64 -> conv_c_out 32 (mode 1) / 16 (mode 2)
+ *   y = rave_pqmf_synthesis(w, mode, noise, pad pqmf_pad_left)
+ *   x: (B, 64, frames); y: (B, 1, 16 * frames), 16-byte aligned.  filter: hki
+ *   (16, 16, 33); act RAVE_ACT_LEAKY / RAVE_ACT_SNAKE (alpha: 64 floats).
+ * weight: the conv's rave_conv1d_split_pack_weight image (7 taps, stride 1).
+ */
+typedef struct rave_edge_args {
+    int32_t batch, frames;          /* PQMF frames (audio samples / 16)                    */
+    int32_t conv_c_in, conv_c_out, conv_kernel, conv_pad_left;
+    int32_t pqmf_taps, pqmf_pad_left;
+    int32_t mode, act;              /* tail: synthesis mode 1 / 2; the conv input act      */
+    float leaky_slope;
+    int32_t fill_channels, fill_t, _pad0;
+    const float* x;     int64_t x_sb, x_sc;
+    float* y;           int64_t y_sb, y_sc;
+    const float* weight;
+    const float* bias;  /* conv_c_out floats or NULL                                       */
+    const float* alpha; /* Snake alphas of the conv input (tail)                           */
+    const float* filter;
+    const float* noise; int64_t n_sb, n_sc;   /* tail: (B, 16, frames) or NULL             */
+    float* fill_y;      int64_t f_sb, f_sc;
+    const float* fill_values;
+} rave_edge_args;
+int rave_encoder_head(const rave_edge_args* a, void* stream);
+int rave_decoder_tail(const rave_edge_args* a, void* stream);
+
 /* ---------------------------------------------------------------- plans
  * A plan is a recorded sequence of the ops above (the module graph of
  * RAVE.encode/decode).  Pointer fields inside an op's args may be relocated at
@@ -358,7 +414,9 @@ enum {
     RAVE_OP_NOISE = 9,
     RAVE_OP_ADAIN = 10,
     RAVE_OP_UNIT = 11,
-    RAVE_OP_STACK = 12
+    RAVE_OP_STACK = 12,
+    RAVE_OP_HEAD = 13,
+    RAVE_OP_TAIL = 14
 };
 
 #define RAVE_OP_PAYLOAD 240
@@ -376,6 +434,7 @@ typedef struct rave_plan_op {
         rave_adain_args adain;
         rave_unit_args unit;
         rave_stack_args stack;
+        rave_edge_args edge;
         unsigned char raw[RAVE_OP_PAYLOAD];
     } u;
 } rave_plan_op;

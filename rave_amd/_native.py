@@ -39,7 +39,9 @@ OP_NOISE = 9
 OP_ADAIN = 10
 OP_UNIT = 11
 OP_STACK = 12
-ABI_VERSION = 11
+OP_HEAD = 13
+OP_TAIL = 14
+ABI_VERSION = 12
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 
 # GEMM arithmetic of conv / unit ops (include/rave_amd.h RAVE_PREC_*)
@@ -47,7 +49,8 @@ PREC_F32 = 0
 PREC_SPLIT16 = 1
 PREC_AUTO = 2
 PREC_F32_TUNED = 3      # exact fp32, launch choices autotuned (RAVE_PREC_F32_TUNED)
-PRECISION = {"f32": PREC_F32, "split16": PREC_SPLIT16}
+PREC_F32_RING = 4       # exact fp32 on the split16 kernels' staging machinery (RAVE_PREC_F32_RING)
+PRECISION = {"f32": PREC_F32, "split16": PREC_SPLIT16, "f32_ring": PREC_F32_RING}
 STREAM_GRAPH = 1
 STREAM_ENCODE_ONLY = 2
 STREAM_DECODE_ONLY = 4
@@ -176,6 +179,16 @@ class MaxPoolArgs(C.Structure):
                 ("x", vp), ("x_sb", i64), ("x_sc", i64), ("y", vp), ("y_sb", i64), ("y_sc", i64)]
 
 
+class EdgeArgs(C.Structure):
+    _fields_ = [("batch", i32), ("frames", i32), ("conv_c_in", i32), ("conv_c_out", i32), ("conv_kernel", i32),
+                ("conv_pad_left", i32), ("pqmf_taps", i32), ("pqmf_pad_left", i32), ("mode", i32), ("act", i32),
+                ("leaky_slope", f32), ("fill_channels", i32), ("fill_t", i32), ("_pad0", i32),
+                ("x", vp), ("x_sb", i64), ("x_sc", i64), ("y", vp), ("y_sb", i64), ("y_sc", i64),
+                ("weight", vp), ("bias", vp), ("alpha", vp), ("filter", vp),
+                ("noise", vp), ("n_sb", i64), ("n_sc", i64),
+                ("fill_y", vp), ("f_sb", i64), ("f_sc", i64), ("fill_values", vp)]
+
+
 MAX_RATIOS = 8
 MAX_DILATIONS = 8
 
@@ -215,13 +228,14 @@ class Reloc(C.Structure):
 
 STRUCTS = [ConvArgs, AnalysisArgs, SynthesisArgs, FillArgs, RvqArgs, ShiftArgs, PlanOp, Reloc,
            CopyArgs, NoiseArgs, AdainArgs, UnitArgs, StackArgs, ModelConfig, Param, OpInfo,
-           FirArgs, RowStatsArgs, AttnPoolArgs, LinearArgs, MaxPoolArgs]
+           FirArgs, RowStatsArgs, AttnPoolArgs, LinearArgs, MaxPoolArgs, EdgeArgs]
 
 # every exported symbol of include/rave_amd.h
 EXPORTS = [
     "rave_last_error", "rave_abi_version", "rave_struct_sizes",
     "rave_conv1d_chunk", "rave_conv1d_packed_size", "rave_conv1d_pack_weight", "rave_conv1d",
     "rave_conv1d_workspace", "rave_conv1d_configs", "rave_conv1d_split_packed_size", "rave_conv1d_split_pack_weight",
+    "rave_conv1d_ring_pack_weight",
     "rave_pqmf_analysis", "rave_pqmf_synthesis", "rave_fill_channels", "rave_copy",
     "rave_rvq_workspace", "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
     "rave_unit_packed_size", "rave_unit_pack_weight", "rave_residual_unit",
@@ -239,6 +253,7 @@ EXPORTS = [
     "rave_stream_encode", "rave_stream_decode", "rave_stream_encode_codes", "rave_stream_decode_codes",
     "rave_stream_delay",
     "rave_fir", "rave_row_stats", "rave_attn_pool", "rave_linear", "rave_maxpool",
+    "rave_encoder_head", "rave_decoder_tail",
 ]
 
 
@@ -264,6 +279,7 @@ def _load():
     lib.rave_conv1d_split_packed_size.argtypes = [C.c_int] * 6
     lib.rave_conv1d_split_packed_size.restype = i64
     lib.rave_conv1d_split_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
+    lib.rave_conv1d_ring_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
     lib.rave_unit_packed_size.argtypes = [C.c_int]
     lib.rave_unit_packed_size.restype = i64
     lib.rave_unit_pack_weight.argtypes = [vp, vp, C.c_int, vp]
@@ -281,7 +297,8 @@ def _load():
                      ("rave_noise_synth", NoiseArgs), ("rave_adain", AdainArgs),
                      ("rave_residual_unit", UnitArgs), ("rave_residual_stack", StackArgs),
                      ("rave_fir", FirArgs), ("rave_row_stats", RowStatsArgs), ("rave_attn_pool", AttnPoolArgs),
-                     ("rave_linear", LinearArgs), ("rave_maxpool", MaxPoolArgs)]:
+                     ("rave_linear", LinearArgs), ("rave_maxpool", MaxPoolArgs),
+                     ("rave_encoder_head", EdgeArgs), ("rave_decoder_tail", EdgeArgs)]:
         getattr(lib, name).argtypes = [C.POINTER(st), vp]
     lib.rave_plan_create.argtypes = [C.POINTER(PlanOp), C.c_int, C.POINTER(Reloc), C.c_int,
                                      C.POINTER(vp)]
@@ -410,6 +427,8 @@ def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed, out_s
     w = np.ascontiguousarray(w, dtype=np.float32)
     size_fn, pack_fn = ((lib.rave_conv1d_packed_size, lib.rave_conv1d_pack_weight)
                         if precision == PREC_F32 else
+                        (lib.rave_conv1d_split_packed_size, lib.rave_conv1d_ring_pack_weight)
+                        if precision == PREC_F32_RING else
                         (lib.rave_conv1d_split_packed_size, lib.rave_conv1d_split_pack_weight))
     n = int(size_fn(c_in, c_out, kernel, stride, dilation, int(transposed)))
     if n <= 0:

@@ -40,7 +40,7 @@ extern "C" int rave_struct_sizes(int64_t* out, int n) {
         (int64_t)sizeof(rave_param),             (int64_t)sizeof(rave_op_info),
         (int64_t)sizeof(rave_fir_args),          (int64_t)sizeof(rave_row_stats_args),
         (int64_t)sizeof(rave_attn_pool_args),    (int64_t)sizeof(rave_linear_args),
-        (int64_t)sizeof(rave_maxpool_args),
+        (int64_t)sizeof(rave_maxpool_args),      (int64_t)sizeof(rave_edge_args),
     };
     const int cnt = (int)(sizeof(sizes) / sizeof(sizes[0]));
     if (!out) return cnt;
@@ -198,6 +198,8 @@ extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, v
             case RAVE_OP_ADAIN: rc = rave_adain(&op.u.adain, stream); break;
             case RAVE_OP_UNIT: rc = rave_residual_unit(&op.u.unit, stream); break;
             case RAVE_OP_STACK: rc = rave_residual_stack(&op.u.stack, stream); break;
+            case RAVE_OP_HEAD: rc = rave_encoder_head(&op.u.edge, stream); break;
+            case RAVE_OP_TAIL: rc = rave_decoder_tail(&op.u.edge, stream); break;
             default:
                 rave::set_error("plan_run: unknown op kind " + std::to_string(op.kind));
                 return RAVE_ERR_STATE;

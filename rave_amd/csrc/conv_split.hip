@@ -202,8 +202,13 @@ template <int V> struct IC {
     static constexpr int value = V;
 };
 
-template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX, int NS>
-__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split_kernel(ConvKArgs a) {
+// F32: the same machinery with exact fp32 operands (RAVE_PREC_F32_RING): one
+// fp32 plane per staged buffer (row pitch PH floats, the bytes of the hi / lo
+// pair), weight fragments of 8 floats per lane in the split image's slots, and
+// eight v_mfma_f32_32x32x2_f32 per 16-deep K-step (K-slot (s, half h) =
+// channel 8h + s of the step's 16); no range guard, row scales 1.
+template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX, int NS, bool F32>
+__device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
     using G = SGeo<KT, BM, BN, WM, XV, KG, WN_, VCX, NS>;
     constexpr int S = G::S, CPC = G::CPC, PH = G::PH;
     constexpr int NT = G::NT, NW = G::NW, NWT = G::NWT, WGM = G::WGM, G8 = G::G8, XT = G::XT;
@@ -362,11 +367,17 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                     }
                     v8[v] = val * xs;
                 }
-                m = absmax8(v8);
-                const s_h8 hi = __builtin_convertvector(v8, s_h8);
-                const s_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, s_f32x8)) * 2048.0f, s_h8);
-                *reinterpret_cast<s_h8*>(xh + w * PH + g * 8) = hi;
-                *reinterpret_cast<s_h8*>(xl + w * PH + g * 8) = lo;
+                if constexpr (F32) {
+                    float* xf = reinterpret_cast<float*>(planes + pb * 2 * G::XPLANE);
+                    *reinterpret_cast<s_f32x4*>(xf + w * PH + g * 8) = s_f32x4{v8[0], v8[1], v8[2], v8[3]};
+                    *reinterpret_cast<s_f32x4*>(xf + w * PH + g * 8 + 4) = s_f32x4{v8[4], v8[5], v8[6], v8[7]};
+                } else {
+                    m = absmax8(v8);
+                    const s_h8 hi = __builtin_convertvector(v8, s_h8);
+                    const s_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, s_f32x8)) * 2048.0f, s_h8);
+                    *reinterpret_cast<s_h8*>(xh + w * PH + g * 8) = hi;
+                    *reinterpret_cast<s_h8*>(xl + w * PH + g * 8) = lo;
+                }
             }
         }
         return m;
@@ -431,8 +442,15 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
         const _Float16* xl = reinterpret_cast<const _Float16*>(planes + pb * 2 * G::XPLANE + G::XPLANE);
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            f.h[i] = *reinterpret_cast<const s_h8*>(xh + xoff[q] + i * 32 * PH + hv * 16);
-            f.l[i] = *reinterpret_cast<const s_h8*>(xl + xoff[q] + i * 32 * PH + hv * 16);
+            if constexpr (F32) {   // 8 floats: channels 8h..8h+7 of the step's 16 (xoff counts floats)
+                const float* xf = reinterpret_cast<const float*>(planes + pb * 2 * G::XPLANE) + xoff[q] + i * 32 * PH +
+                                  hv * 16;
+                f.h[i] = *reinterpret_cast<const s_h8*>(xf);
+                f.l[i] = *reinterpret_cast<const s_h8*>(xf + 4);
+            } else {
+                f.h[i] = *reinterpret_cast<const s_h8*>(xh + xoff[q] + i * 32 * PH + hv * 16);
+                f.l[i] = *reinterpret_cast<const s_h8*>(xl + xoff[q] + i * 32 * PH + hv * 16);
+            }
         }
     };
 
@@ -490,28 +508,43 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
                 for (int j = 0; j < NJ; ++j) wait_vm_regs<2 * (WR / 2 - NJ) + XI>(wr[k][j][0], wr[k][j][1]);
                 __builtin_amdgcn_sched_barrier(0);
                 const AFrag& g = f[k & 1];
-                s_h8 bh[NJ], bl[NJ], b2[NJ];
+                if constexpr (F32) {
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    bh[j] = __builtin_bit_cast(s_h8, wr[k][j][0]);
-                    bl[j] = __builtin_bit_cast(s_h8, wr[k][j][1]);
-                    b2[j] = bh[j] * (_Float16)2048.0f;
+                    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+#pragma unroll
+                            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                                for (int j = 0; j < NJ; ++j) {
+                                    const s_f32x4 av = __builtin_bit_cast(s_f32x4, hf ? g.l[i] : g.h[i]);
+                                    const s_f32x4 bv = __builtin_bit_cast(s_f32x4, wr[k][j][hf]);
+                                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bv[e], acc[i][j], 0, 0, 0);
+                                }
+                } else {
+                    s_h8 bh[NJ], bl[NJ], b2[NJ];
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        bh[j] = __builtin_bit_cast(s_h8, wr[k][j][0]);
+                        bl[j] = __builtin_bit_cast(s_h8, wr[k][j][1]);
+                        b2[j] = bh[j] * (_Float16)2048.0f;
+                    }
+#pragma unroll
+                    for (int i = 0; i < NI; ++i)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.h[i], b2[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < NI; ++i)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.l[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < NI; ++i)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.h[i], bl[j], acc[i][j], 0, 0, 0);
                 }
-#pragma unroll
-                for (int i = 0; i < NI; ++i)
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.h[i], b2[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-                for (int i = 0; i < NI; ++i)
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.l[i], bh[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-                for (int i = 0; i < NI; ++i)
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(g.h[i], bl[j], acc[i][j], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
                 load_w(c + 1, k, ST0 + k);      // refill the slot one chunk ahead
                 // split part of window c+1 into the other plane pair (VALU beside the MFMAs)
@@ -550,7 +583,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
         wait_vm<0>();                       // drain the ring (epilogue loads / a second attempt)
     };
     run_k(IC<0>{});
-    if (RAVE_SPLIT_GUARD) {
+    if (RAVE_SPLIT_GUARD && !F32) {
         bool bad = false;
 #pragma unroll
         for (int i = 0; i < NI; ++i)
@@ -820,6 +853,15 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split
     }
 }
 
+template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX, int NS>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split_kernel(ConvKArgs a) {
+    conv1d_split_body<KT, BM, BN, WM, SNAKE, XV, KG, WN_, VCX, NS, false>(a);
+}
+template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX, int NS>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_ring_f32_kernel(ConvKArgs a) {
+    conv1d_split_body<KT, BM, BN, WM, SNAKE, XV, KG, WN_, VCX, NS, true>(a);
+}
+
 // --------------------------------------------------------------------- tiles
 struct SplitCfg {
     int tile, S, sep;     // kSplitTiles index, K-splits, separate reduce launch
@@ -879,11 +921,11 @@ static inline auto with_tile(int ti, Fn&& f) {
 // instantiations are spread over separate translation units (the Makefile
 // compiles this file once per (KT, SNAKE, XV) with -DRAVE_SPLIT_KT / _SNAKE / _XV,
 // and once without them for the host side) so the build runs in parallel.
-template <int KT, bool SNAKE, bool XV>
+template <int KT, bool SNAKE, bool XV, bool F32>
 int split_launch_inst(ConvKArgs k, int tile, hipStream_t st);
 
 #ifdef RAVE_SPLIT_KT
-template <int KT, int BM, int BN, int WM, int KG, int WN, int VCX, int NS, bool SNAKE, bool XV>
+template <int KT, int BM, int BN, int WM, int KG, int WN, int VCX, int NS, bool SNAKE, bool XV, bool F32>
 static int split_launch_xv(ConvKArgs k, hipStream_t st) {
     using G = SGeo<KT, BM, BN, WM, XV, KG, WN, VCX, NS>;
     if constexpr (!G::VALID) {
@@ -897,7 +939,10 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
         constexpr size_t lds = (size_t)G::LDS_ALL;
         static_assert(lds <= 160 * 1024, "LDS budget");
         dim3 grid(k.gx * k.gy * k.B * k.S);
-        auto kern = conv1d_split_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN, VCX, NS>;
+        auto kern = [] {
+            if constexpr (F32) return conv1d_ring_f32_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN, VCX, NS>;
+            else return conv1d_split_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN, VCX, NS>;
+        }();
         if (lds > 64 * 1024) {
             static bool done = false;
             if (!done) {
@@ -907,21 +952,24 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
             }
         }
         launch(kern, grid, dim3(G::NT), (uint32_t)lds, st, k);
-        return launch_status("conv1d_split_kernel");
+        return launch_status(F32 ? "conv1d_ring_f32_kernel" : "conv1d_split_kernel");
     }
 }
 
-template <int KT, bool SNAKE, bool XV>
+template <int KT, bool SNAKE, bool XV, bool F32>
 int split_launch_inst(ConvKArgs k, int tile, hipStream_t st) {
     return with_tile(tile, [&](auto bm, auto bn, auto wm, auto kg, auto wn, auto vcx, auto ns) {
         constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
                       KG = decltype(kg)::value, WN = decltype(wn)::value, VCX = decltype(vcx)::value,
                       NS = decltype(ns)::value;
-        return split_launch_xv<KT, BM, BN, WM, KG, WN, VCX, NS, SNAKE, XV>(k, st);
+        return split_launch_xv<KT, BM, BN, WM, KG, WN, VCX, NS, SNAKE, XV, F32>(k, st);
     });
 }
-template int split_launch_inst<RAVE_SPLIT_KT, (RAVE_SPLIT_SNAKE != 0), (RAVE_SPLIT_XV != 0)>(ConvKArgs, int,
-                                                                                              hipStream_t);
+#ifndef RAVE_SPLIT_F32
+#define RAVE_SPLIT_F32 0
+#endif
+template int split_launch_inst<RAVE_SPLIT_KT, (RAVE_SPLIT_SNAKE != 0), (RAVE_SPLIT_XV != 0), (RAVE_SPLIT_F32 != 0)>(
+    ConvKArgs, int, hipStream_t);
 
 }  // namespace rave
 #else   // ------------------------------------------------------- host side
@@ -1026,15 +1074,17 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
 }
 
 template <int KT>
-static int split_launch_family(ConvKArgs k, const SplitCfg& c, hipStream_t st) {
+static int split_launch_family(ConvKArgs k, const SplitCfg& c, bool f32, hipStream_t st) {
     const int* t = kSplitTiles[c.tile];
     k.XW = t[1] + (SFam<KT>::Q - 1) * k.d + (k.transposed ? 1 : 0);
     k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
     const unsigned rl = (unsigned)(k.XW * SFam<KT>::S);
     k.rl_magic = (unsigned)((0x100000000ull + rl - 1) / rl);
     const bool snake = k.act == RAVE_ACT_SNAKE;
-    auto fn = snake ? (k.x_vec ? split_launch_inst<KT, true, true> : split_launch_inst<KT, true, false>)
-                    : (k.x_vec ? split_launch_inst<KT, false, true> : split_launch_inst<KT, false, false>);
+    auto fn = f32 ? (snake ? (k.x_vec ? split_launch_inst<KT, true, true, true> : split_launch_inst<KT, true, false, true>)
+                           : (k.x_vec ? split_launch_inst<KT, false, true, true> : split_launch_inst<KT, false, false, true>))
+                  : (snake ? (k.x_vec ? split_launch_inst<KT, true, true, false> : split_launch_inst<KT, true, false, false>)
+                           : (k.x_vec ? split_launch_inst<KT, false, true, false> : split_launch_inst<KT, false, false, false>));
     return fn(k, c.tile, st);
 }
 
@@ -1141,13 +1191,14 @@ int conv1d_split(const rave_conv1d_args& a, void* stream) {
     k.stamps = a.stamps;
 #endif
     hipStream_t st = as_stream(stream);
+    const bool f32 = a.precision == RAVE_PREC_F32_RING;
     switch (taps) {
-        case 1: rc = split_launch_family<1>(k, c, st); break;
-        case 2: rc = split_launch_family<2>(k, c, st); break;
-        case 3: rc = split_launch_family<3>(k, c, st); break;
-        case 4: rc = split_launch_family<4>(k, c, st); break;
-        case 7: rc = split_launch_family<7>(k, c, st); break;
-        case 8: rc = split_launch_family<8>(k, c, st); break;
+        case 1: rc = split_launch_family<1>(k, c, f32, st); break;
+        case 2: rc = split_launch_family<2>(k, c, f32, st); break;
+        case 3: rc = split_launch_family<3>(k, c, f32, st); break;
+        case 4: rc = split_launch_family<4>(k, c, f32, st); break;
+        case 7: rc = split_launch_family<7>(k, c, f32, st); break;
+        case 8: rc = split_launch_family<8>(k, c, f32, st); break;
         default: set_error("conv1d: unsupported kernel size"); return RAVE_ERR_UNSUPPORTED;
     }
     if (rc != RAVE_OK || k.S <= 1 || k.inlaunch) return rc;
@@ -1209,8 +1260,8 @@ extern "C" int64_t rave_conv1d_split_packed_size(int c_in, int c_out, int kernel
     return best;
 }
 
-extern "C" int rave_conv1d_split_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
-                                             int dilation, int transposed, int out_shift, float* packed) {
+static int split_pack(const float* w, int c_in, int c_out, int kernel, int stride, int dilation, int transposed,
+                      int out_shift, float* packed, bool f32) {
     RAVE_CHECK_ARG(w && packed, "split_pack_weight: null pointer");
     RAVE_CHECK_ARG(c_in > 0 && c_out > 0 && kernel > 0 && stride > 0 && dilation > 0,
                    "split_pack_weight: bad shape");
@@ -1247,7 +1298,7 @@ extern "C" int rave_conv1d_split_pack_weight(const float* w, int c_in, int c_out
     };
     const int KT_orig = transposed ? 2 : kernel;
     std::vector<int> ex(Mpad, 0);
-    for (int m = 0; m < Mpad; ++m) {
+    for (int m = 0; m < Mpad && !f32; ++m) {
         double amax = 0.0;
         for (int ci = 0; ci < c_in; ++ci)
             for (int j = 0; j < KT_orig; ++j) amax = std::max(amax, (double)std::fabs(wval(m, ci, j)));
@@ -1258,14 +1309,20 @@ extern "C" int rave_conv1d_split_pack_weight(const float* w, int c_in, int c_out
         for (int mb = 0; mb < MB; ++mb)
             for (int st = 0; st < KSC; ++st) {
                 const int q = st / HPS, hv = st % HPS;
-                _Float16* hi = out + (((int64_t)(c * MB + mb) * KSC + st) * 2) * 512;
+                const int64_t blk = ((int64_t)(c * MB + mb) * KSC + st) * 2;   // 1 KB slots
+                _Float16* hi = out + blk * 512;
                 _Float16* lo = hi + 512;
+                float* f32s = packed + blk * 256;      // fp32: floats 0-3 of a lane in slot 0, 4-7 in slot 1
                 for (int l = 0; l < 64; ++l)
                     for (int e = 0; e < 8; ++e) {
                         const int m = mb * 32 + (l & 31);
                         const int vc = hv * 16 + 8 * (l >> 5) + e;
                         int ci, j;
                         kmap(c, q, vc, ci, j);
+                        if (f32) {
+                            f32s[(e >> 2) * 256 + l * 4 + (e & 3)] = wval(m, ci, j);
+                            continue;
+                        }
                         const float v = std::ldexp(wval(m, ci, j), ex[m]);
                         const _Float16 vh = (_Float16)v;
                         const _Float16 vl = (_Float16)((v - (float)vh) * 2048.0f);
@@ -1274,7 +1331,17 @@ extern "C" int rave_conv1d_split_pack_weight(const float* w, int c_in, int c_out
                     }
             }
     float* rs = packed + (int64_t)nchunks * MB * KSC * 2 * 256;
-    for (int m = 0; m < Mpad; ++m) rs[m] = (float)std::ldexp(1.0, -(ex[m] + 11));
+    for (int m = 0; m < Mpad; ++m) rs[m] = f32 ? 1.0f : (float)std::ldexp(1.0, -(ex[m] + 11));
     return RAVE_OK;
+}
+
+extern "C" int rave_conv1d_split_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
+                                             int dilation, int transposed, int out_shift, float* packed) {
+    return split_pack(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift, packed, false);
+}
+
+extern "C" int rave_conv1d_ring_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
+                                            int dilation, int transposed, int out_shift, float* packed) {
+    return split_pack(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift, packed, true);
 }
 #endif  // RAVE_SPLIT_KT

@@ -402,6 +402,13 @@ struct Model {
     void synthesis_op(Plan& p, int B, int F, const View& x, const View& y, const View* noise, int pad, int frame0,
                       int x_len);
     void fill_speaker(Plan& p, int B, int Fz, const View& z);
+    // PQMF + edge-conv fusions (csrc/edge_split.hip), split-f16 only
+    rave_edge_args head_desc(int B, int F) const;
+    bool use_head(int B, int T);
+    void head_op(Plan& p, int B, int T, const View& x, const View& y, const View* fill_z);
+    rave_edge_args tail_desc(int B, int F) const;
+    bool use_tail(int B, int F);
+    void tail_op(Plan& p, int B, int F, const View& x, const View& y, const View* noise);
     void rvq_encode_op(Plan& p, int B, int Fz, const View& lat, const View& idx);
     void rvq_decode_op(Plan& p, int B, int Fz, const View& idx, const View& z);
     Plan& encode_plan(int B, int T, bool codes);
@@ -1072,6 +1079,217 @@ void Model::fill_speaker(Plan& p, int B, int Fz, const View& z) {
     p.bind(o, A, A.values, &s);
 }
 
+// ------------------------------------------------------------------ path edges
+// The PQMF op and the conv next to it as one split-f16 launch: the encoder head
+// (analysis -> EncoderV2's first conv, + the speaker fill) and the decoder tail
+// (GeneratorV2's last conv + epilogue -> synthesis).  Used where split-f16 is
+// one of the model's arithmetics, the shapes are the kernels', and (with
+// autotuning) the fused launch beats the two separate ops at their best.
+rave_edge_args Model::head_desc(int B, int F) const {
+    const Node& n = g.encoder.front();
+    rave_edge_args a{};
+    a.batch = B;
+    a.frames = F;
+    a.conv_c_in = n.c_in;
+    a.conv_c_out = n.c_out;
+    a.conv_kernel = n.kernel;
+    a.conv_pad_left = n.pad_l;
+    a.pqmf_taps = taps_a;
+    a.pqmf_pad_left = get_padding(taps_a, 1, cfg.causal).first;
+    a.act = n.act;
+    a.leaky_slope = cfg.leaky_slope;
+    return a;
+}
+
+rave_edge_args Model::tail_desc(int B, int F) const {
+    const Node& n = g.decoder.back();
+    rave_edge_args a{};
+    a.batch = B;
+    a.frames = F;
+    a.conv_c_in = n.c_in;
+    a.conv_c_out = n.c_out;
+    a.conv_kernel = n.kernel;
+    a.conv_pad_left = n.pad_l;
+    a.pqmf_taps = taps_s;
+    a.pqmf_pad_left = get_padding(taps_s, 1, cfg.causal).first;
+    a.mode = cfg.amplitude_modulation ? 1 : 2;
+    a.act = n.act;
+    a.leaky_slope = cfg.leaky_slope;
+    return a;
+}
+
+bool Model::use_head(int B, int T) {
+    const Node& n = g.encoder.front();
+    const int F = T / cfg.n_band;
+    if (std::find(precs.begin(), precs.end(), RAVE_PREC_SPLIT16) == precs.end()) return false;
+    if (cfg.n_band != 16 || n.kernel != 7 || n.stride != 1 || n.dilation != 1 || n.act != RAVE_ACT_NONE ||
+        n.transposed || n.c_in > 8 || n.c_out > 64 || !n.adain.empty() || F * cfg.n_band != T)
+        return false;
+    const std::string key = key_of({"head", std::to_string(B), std::to_string(T)});
+    if (!tuned.count(key)) {
+        rave_edge_args a = head_desc(B, F);
+        const int64_t nx = (int64_t)B * T, ny = (int64_t)B * n.c_out * F, nb = (int64_t)B * n.c_in * F;
+        float* sc = scratch_buf(nx + ny + nb + 256);
+        a.x = sc;
+        a.x_sb = T;
+        a.y = sc + nx + 64;
+        a.y_sb = (int64_t)n.c_out * F;
+        a.y_sc = F;
+        a.weight = aptr(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
+        a.bias = n.bias ? aptr(bias_off.at(n.name)) : nullptr;
+        a.filter = aptr(hkf_off);
+        const double fused = time_native([&](hipStream_t st) { return rave_encoder_head(&a, st); });
+        double split = 1e30;
+        if (precs.size() == 1) {
+            split = fused >= 0 ? 1e30 : -1.0;
+        } else {
+            // the two ops at their best: analysis in either arithmetic, the conv's tuned launch
+            rave_pqmf_analysis_args q{};
+            q.n_band = cfg.n_band;
+            q.taps = taps_a;
+            q.n_out_bands = n.c_in;
+            q.batch = B;
+            q.t_in = T;
+            q.pad_left = a.pqmf_pad_left;
+            q.t_out = F;
+            q.x = sc;
+            q.x_sb = T;
+            q.y = sc + nx + ny + 128;
+            q.y_sb = (int64_t)n.c_in * F;
+            q.y_sc = F;
+            q.hkf = aptr(hkf_off);
+            double ta = 1e30;
+            for (int pr : {RAVE_PREC_F32, RAVE_PREC_SPLIT16}) {
+                q.precision = pr;
+                const double ms = time_native([&](hipStream_t st) { return rave_pqmf_analysis(&q, st); });
+                if (ms >= 0) ta = std::min(ta, ms);
+            }
+            View dummy;
+            int t_out;
+            const rave_conv1d_args cd = conv_desc(n, B, F, dummy, dummy, nullptr, t_out);
+            (void)conv_launch(n, cd, false, true);
+            const auto it = tuned.find(key_of({"conv", n.name, "0", std::to_string(B), std::to_string(F)}));
+            split = ta + (it != tuned.end() ? it->second.second : 1e30);
+        }
+        tuned[key] = {fused >= 0 && fused < split ? 1 : 0, fused};
+    }
+    return tuned.at(key).first == 1;
+}
+
+void Model::head_op(Plan& p, int B, int T, const View& x, const View& y, const View* fill_z) {
+    const Node& n = g.encoder.front();
+    const int F = T / cfg.n_band;
+    rave_edge_args a = head_desc(B, F);
+    a.x_sb = x.sb;
+    a.y_sb = y.sb;
+    a.y_sc = y.sc;
+    if (fill_z && cfg.speaker_size > 0) {
+        a.fill_channels = cfg.speaker_size;
+        a.fill_t = T / hop;
+        a.f_sb = fill_z->sb;
+        a.f_sc = fill_z->sc;
+    }
+    PlanOp& o = p.add(RAVE_OP_HEAD, a, "encoder_head:pqmf_analysis+" + n.name);
+    rave_edge_args& A = *reinterpret_cast<rave_edge_args*>(o.op.u.raw);
+    View wv = arena_view(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
+    View bv = n.bias ? arena_view(bias_off.at(n.name)) : View{};
+    View hv = arena_view(hkf_off);
+    View sv = arena_view(spk_off);
+    p.bind(o, A, A.x, &x);
+    p.bind(o, A, A.y, &y);
+    p.bind(o, A, A.weight, &wv);
+    p.bind(o, A, A.bias, n.bias ? &bv : nullptr);
+    p.bind(o, A, A.filter, &hv);
+    p.bind(o, A, A.fill_y, a.fill_channels ? fill_z : nullptr);
+    p.bind(o, A, A.fill_values, a.fill_channels ? &sv : nullptr);
+    o.prec = RAVE_PREC_SPLIT16;
+    o.flops = 2.0 * B * F * ((double)n.c_in * taps_a + (double)n.c_out * n.c_in * n.kernel);
+    o.bytes = 4.0 * ((double)B * T + (double)B * n.c_out * F);
+}
+
+bool Model::use_tail(int B, int F) {
+    const Node& n = g.decoder.back();
+    if (std::find(precs.begin(), precs.end(), RAVE_PREC_SPLIT16) == precs.end()) return false;
+    const int c_want = cfg.amplitude_modulation ? 2 * cfg.n_band : cfg.n_band;
+    if (cfg.n_band != 16 || n.kernel != 7 || n.stride != 1 || n.dilation != 1 || n.transposed || n.c_in != 64 ||
+        n.c_out != c_want || (n.act != RAVE_ACT_LEAKY && n.act != RAVE_ACT_SNAKE) || !n.adain.empty())
+        return false;
+    const std::string key = key_of({"tail", std::to_string(B), std::to_string(F)});
+    if (!tuned.count(key)) {
+        rave_edge_args a = tail_desc(B, F);
+        const int64_t nx = (int64_t)B * n.c_in * F, nw = (int64_t)B * n.c_out * F, ny = (int64_t)B * F * cfg.n_band;
+        float* sc = scratch_buf(nx + nw + ny + 256);
+        a.x = sc;
+        a.x_sb = (int64_t)n.c_in * F;
+        a.x_sc = F;
+        a.y = sc + ((nx + nw + 63) / 64 + 1) * 64;     // 16-byte aligned
+        a.y_sb = (int64_t)F * cfg.n_band;
+        a.weight = aptr(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
+        a.bias = n.bias ? aptr(bias_off.at(n.name)) : nullptr;
+        a.alpha = n.act == RAVE_ACT_SNAKE ? aptr(alpha_off.at(n.alpha)) : nullptr;
+        a.filter = aptr(hki_off);
+        const double fused = time_native([&](hipStream_t st) { return rave_decoder_tail(&a, st); });
+        double split = 1e30;
+        if (precs.size() == 1) {
+            split = fused >= 0 ? 1e30 : -1.0;
+        } else {
+            rave_pqmf_synthesis_args q{};
+            q.n_band = cfg.n_band;
+            q.taps = taps_s;
+            q.batch = B;
+            q.t_in = F;
+            q.pad_left = a.pqmf_pad_left;
+            q.mode = a.mode;
+            q.x = sc + nx + 64;
+            q.x_sb = (int64_t)n.c_out * F;
+            q.x_sc = F;
+            q.y = a.y;
+            q.y_sb = a.y_sb;
+            q.hki = aptr(hki_off);
+            double ts = 1e30;
+            for (int pr : {RAVE_PREC_F32, RAVE_PREC_SPLIT16}) {
+                q.precision = pr;
+                const double ms = time_native([&](hipStream_t st) { return rave_pqmf_synthesis(&q, st); });
+                if (ms >= 0) ts = std::min(ts, ms);
+            }
+            View dummy;
+            int t_out;
+            const rave_conv1d_args cd = conv_desc(n, B, F, dummy, dummy, nullptr, t_out);
+            (void)conv_launch(n, cd, false, true);
+            const auto it = tuned.find(key_of({"conv", n.name, "0", std::to_string(B), std::to_string(F)}));
+            split = ts + (it != tuned.end() ? it->second.second : 1e30);
+        }
+        tuned[key] = {fused >= 0 && fused < split ? 1 : 0, fused};
+    }
+    return tuned.at(key).first == 1;
+}
+
+void Model::tail_op(Plan& p, int B, int F, const View& x, const View& y, const View* noise) {
+    const Node& n = g.decoder.back();
+    rave_edge_args a = tail_desc(B, F);
+    a.x_sb = x.sb;
+    a.x_sc = x.sc;
+    a.y_sb = y.sb;
+    a.n_sb = noise ? noise->sb : 0;
+    a.n_sc = noise ? noise->sc : 0;
+    PlanOp& o = p.add(RAVE_OP_TAIL, a, "decoder_tail:" + n.name + "+pqmf_synthesis");
+    rave_edge_args& A = *reinterpret_cast<rave_edge_args*>(o.op.u.raw);
+    View wv = arena_view(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
+    View bv = n.bias ? arena_view(bias_off.at(n.name)) : View{};
+    View av = n.act == RAVE_ACT_SNAKE ? arena_view(alpha_off.at(n.alpha)) : View{};
+    View hv = arena_view(hki_off);
+    p.bind(o, A, A.x, &x);
+    p.bind(o, A, A.y, &y);
+    p.bind(o, A, A.weight, &wv);
+    p.bind(o, A, A.bias, n.bias ? &bv : nullptr);
+    p.bind(o, A, A.alpha, n.act == RAVE_ACT_SNAKE ? &av : nullptr);
+    p.bind(o, A, A.filter, &hv);
+    p.bind(o, A, A.noise, noise);
+    o.prec = RAVE_PREC_SPLIT16;
+    o.flops = 2.0 * B * F * ((double)n.c_out * n.c_in * n.kernel + (double)cfg.n_band * cfg.n_band * taps_s);
+    o.bytes = 4.0 * ((double)B * n.c_in * F + (double)B * F * cfg.n_band + (noise ? (double)B * cfg.n_band * F : 0.0));
+}
+
 // ResidualVectorQuantization.encode (rave/quantization.py:302-310): latents
 // (B, latent, Fz) at `lat` -> indices (B, n_q, Fz) int64 at `idx`
 void Model::rvq_encode_op(Plan& p, int B, int Fz, const View& lat, const View& idx) {
@@ -1137,16 +1355,25 @@ Plan& Model::encode_plan(int B, int T, bool codes) {
     auto plan = std::make_unique<Plan>();
     Plan& p = *plan;
     const int F = T / cfg.n_band, Fz = T / hop;
-    View bands = ws_view(p.ws.alloc((int64_t)B * cfg.enc_bands * F), (int64_t)cfg.enc_bands * F, F);
-    analysis_op(p, B, T, io_view(0, T, T), bands, cfg.enc_bands, get_padding(taps_a, 1, cfg.causal).first, T);
     View lat;
     if (codes) lat = ws_view(p.ws.alloc((int64_t)B * cfg.latent_size * Fz), (int64_t)cfg.latent_size * Fz, Fz);
     else lat = io_view(1, (int64_t)(cfg.latent_size + cfg.speaker_size) * Fz, Fz);
-    run_stack(p, ptrs_of(g.encoder), B, {{"enc_in", {bands, F}}}, {{"latent", lat}});
-    if (codes) {
-        rvq_encode_op(p, B, Fz, lat, io_view(1, 0, 0));
+    const View spk_z = lat.at((int64_t)cfg.latent_size * Fz);
+    std::vector<const Node*> nodes = ptrs_of(g.encoder);
+    if (use_head(B, T)) {
+        // analysis + the first conv (+ the speaker fill) in one launch
+        const Node& n0 = *nodes.front();
+        View h0 = ws_view(p.ws.alloc((int64_t)B * n0.c_out * F), (int64_t)n0.c_out * F, F);
+        head_op(p, B, T, io_view(0, T, T), h0, codes ? nullptr : &spk_z);
+        nodes.erase(nodes.begin());
+        run_stack(p, nodes, B, {{n0.dst, {h0, F}}}, {{"latent", lat}});
+        if (codes) rvq_encode_op(p, B, Fz, lat, io_view(1, 0, 0));
     } else {
-        fill_speaker(p, B, Fz, lat.at((int64_t)cfg.latent_size * Fz));
+        View bands = ws_view(p.ws.alloc((int64_t)B * cfg.enc_bands * F), (int64_t)cfg.enc_bands * F, F);
+        analysis_op(p, B, T, io_view(0, T, T), bands, cfg.enc_bands, get_padding(taps_a, 1, cfg.causal).first, T);
+        run_stack(p, nodes, B, {{"enc_in", {bands, F}}}, {{"latent", lat}});
+        if (codes) rvq_encode_op(p, B, Fz, lat, io_view(1, 0, 0));
+        else fill_speaker(p, B, Fz, spk_z);
     }
     p.finalize(arena);
     return *(plans[key] = std::move(plan));
@@ -1168,8 +1395,18 @@ Plan& Model::decode_plan(int B, int Fz, bool codes) {
         z = io_view(0, (int64_t)dec_in * Fz, Fz);
     }
     const int F = Fz * hop / cfg.n_band;
-    View wave = ws_view(p.ws.alloc((int64_t)B * dec_out * F), (int64_t)dec_out * F, F);
-    std::map<std::string, View> outputs{{"wave", wave}};
+    const bool tail = use_tail(B, F);
+    const Node& wnode = g.decoder.back();
+    std::map<std::string, View> outputs;
+    View wave, feat;
+    if (tail) {
+        // the waveform conv runs inside the fused tail: its input is the stack's output
+        feat = ws_view(p.ws.alloc((int64_t)B * wnode.c_in * F), (int64_t)wnode.c_in * F, F);
+        outputs[wnode.src] = feat;
+    } else {
+        wave = ws_view(p.ws.alloc((int64_t)B * dec_out * F), (int64_t)dec_out * F, F);
+        outputs["wave"] = wave;
+    }
     int Fn = 0, na = 0;
     if (cfg.noise) {
         Fn = F / noise_target;
@@ -1177,6 +1414,7 @@ Plan& Model::decode_plan(int B, int Fz, bool codes) {
         outputs["noise_amp"] = ws_view(p.ws.alloc((int64_t)B * na * Fn), (int64_t)na * Fn, Fn);
     }
     std::vector<const Node*> nodes = ptrs_of(g.decoder);
+    if (tail) nodes.pop_back();
     for (const Node& n : g.noise) nodes.push_back(&n);
     run_stack(p, nodes, B, {{"dec_in", {z, Fz}}}, outputs);
     View noise_v;
@@ -1203,8 +1441,11 @@ Plan& Model::decode_plan(int B, int Fz, bool codes) {
         p.bind(o, N, N.y, &noise_v);
     }
     const int T = F * cfg.n_band;
-    synthesis_op(p, B, F, wave, io_view(1, T, T), cfg.noise ? &noise_v : nullptr,
-                 get_padding(taps_s, 1, cfg.causal).first, 0, 0);
+    if (tail)
+        tail_op(p, B, F, feat, io_view(1, T, T), cfg.noise ? &noise_v : nullptr);
+    else
+        synthesis_op(p, B, F, wave, io_view(1, T, T), cfg.noise ? &noise_v : nullptr,
+                     get_padding(taps_s, 1, cfg.causal).first, 0, 0);
     p.finalize(arena);
     return *(plans[key] = std::move(plan));
 }
@@ -1262,7 +1503,7 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
     build_graph(cfg, m->g);
     if (precision == RAVE_PREC_AUTO) m->precs = {RAVE_PREC_F32, RAVE_PREC_SPLIT16};
     else if (precision == RAVE_PREC_F32 || precision == RAVE_PREC_SPLIT16) m->precs = {precision};
-    else if (precision == RAVE_PREC_F32_TUNED) m->precs = {RAVE_PREC_F32};
+    else if (precision == RAVE_PREC_F32_TUNED) m->precs = {RAVE_PREC_F32, RAVE_PREC_F32_RING};
     else fail(RAVE_ERR_ARG, "precision must be RAVE_PREC_F32, RAVE_PREC_SPLIT16, RAVE_PREC_AUTO or RAVE_PREC_F32_TUNED");
     m->autotune = precision == RAVE_PREC_AUTO || precision == RAVE_PREC_F32_TUNED;
     m->hop = cfg.n_band;
@@ -1302,17 +1543,23 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
         for (int pr : m->precs) {
             for (int form = 0; form < (n->transposed ? 2 : 1); ++form) {
                 const int os = n->transposed ? (form == 0 ? n->stride / 2 : 0) : 0;
-                const bool sp = pr == RAVE_PREC_SPLIT16;
+                // split16 and the fp32 ring path share the fragment image layout
+                const bool sp = pr == RAVE_PREC_SPLIT16 || pr == RAVE_PREC_F32_RING;
                 const int64_t sz = sp ? rave_conv1d_split_packed_size(n->c_in, n->c_out, n->kernel, n->stride,
                                                                       n->dilation, n->transposed)
                                       : rave_conv1d_packed_size(n->c_in, n->c_out, n->kernel, n->stride, n->dilation,
                                                                 n->transposed);
                 if (sz <= 0) fail(RAVE_ERR_UNSUPPORTED, "conv " + n->name + ": unsupported layer shape");
                 std::vector<float> packed((size_t)sz, 0.f);
-                const int rc = sp ? rave_conv1d_split_pack_weight(w.data(), n->c_in, n->c_out, n->kernel, n->stride,
-                                                                  n->dilation, n->transposed, os, packed.data())
-                                  : rave_conv1d_pack_weight(w.data(), n->c_in, n->c_out, n->kernel, n->stride,
-                                                            n->dilation, n->transposed, os, packed.data());
+                const int rc =
+                    pr == RAVE_PREC_SPLIT16
+                        ? rave_conv1d_split_pack_weight(w.data(), n->c_in, n->c_out, n->kernel, n->stride, n->dilation,
+                                                        n->transposed, os, packed.data())
+                    : pr == RAVE_PREC_F32_RING
+                        ? rave_conv1d_ring_pack_weight(w.data(), n->c_in, n->c_out, n->kernel, n->stride, n->dilation,
+                                                       n->transposed, os, packed.data())
+                        : rave_conv1d_pack_weight(w.data(), n->c_in, n->c_out, n->kernel, n->stride, n->dilation,
+                                                  n->transposed, os, packed.data());
                 check_rc(rc, "pack " + n->name);
                 (form == 0 ? m->w_pack : m->w_pack_stream)[{n->name, pr}] = m->add(packed);
             }
@@ -1331,6 +1578,7 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
             std::vector<float> w1 = fold_wn(get(k3.name + ".weight_g"), get(k3.name + ".weight_v"), C_, (int64_t)C_ * 3);
             std::vector<float> w2 = fold_wn(get(k1.name + ".weight_g"), get(k1.name + ".weight_v"), C_, C_);
             for (int p : m->precs) {
+                if (p == RAVE_PREC_F32_RING) continue;   // fused units: the fp32 and split16 kernels
                 const bool sp = p == RAVE_PREC_SPLIT16;
                 const int64_t sz = sp ? rave_unit_split_packed_size(C_) : rave_unit_packed_size(C_);
                 if (sz <= 0) continue;

@@ -149,7 +149,7 @@ def conv_case(case):
     return x, w, b, alpha.reshape(-1) if alpha is not None else None, res, pad, ref
 
 
-@pytest.mark.parametrize("precision", ["f32", "split16"])
+@pytest.mark.parametrize("precision", ["f32", "split16", "f32_ring"])
 @pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("case", CONV_CASES, ids=[str(c[:8]) for c in CONV_CASES])
 def test_conv_layer(N, dev, case, split, precision):
@@ -164,7 +164,7 @@ def test_conv_layer(N, dev, case, split, precision):
 CONFIG_CASES = [CONV_CASES[i] for i in (1, 2, 4, 5, 8, 9, 11, 12, 14)] + CONV_CASES[-2:]
 
 
-@pytest.mark.parametrize("precision", ["f32", "split16"])
+@pytest.mark.parametrize("precision", ["f32", "split16", "f32_ring"])
 @pytest.mark.parametrize("case", CONFIG_CASES, ids=[str(c[:8]) for c in CONFIG_CASES])
 def test_conv_every_config(N, dev, case, precision):
     """Every launch configuration rave_conv1d_configs() offers the autotuner

@@ -24,23 +24,35 @@ import json
 import re
 from collections import defaultdict
 
-# family -> (main kernel, helper kernels launched by the same op)
+# family -> (main kernels, helper kernels launched by the same op)
 FAMILIES = {
-    "conv_f32": ("conv1d_mfma_kernel", ("conv1d_splitk_reduce_kernel",)),
-    "conv_split16": ("conv1d_split_kernel", ("split_reduce_kernel",)),
-    "unit_f32": ("residual_unit_kernel", ()),
-    "unit_split16": ("unit_split_kernel", ()),
-    "stack_split16": ("stack_split_kernel", ()),
-    "pqmf_analysis_f32": ("pqmf_analysis_kernel", ()),
-    "pqmf_synthesis_f32": ("pqmf_synthesis_kernel", ()),
-    "pqmf_analysis_split16": ("pqmf_analysis_split_kernel", ()),
-    "pqmf_synthesis_split16": ("pqmf_synthesis_split_kernel", ()),
+    "conv_f32": (("conv1d_mfma_kernel", "conv1d_ring_f32_kernel"), ("conv1d_splitk_reduce_kernel",)),
+    "conv_split16": (("conv1d_split_kernel",), ("split_reduce_kernel",)),
+    "unit_f32": (("residual_unit_kernel",), ()),
+    "unit_split16": (("unit_split_kernel",), ()),
+    "stack_split16": (("stack_split_kernel",), ()),
+    "pqmf_analysis_f32": (("pqmf_analysis_kernel",), ()),
+    "pqmf_synthesis_f32": (("pqmf_synthesis_kernel",), ()),
+    "pqmf_analysis_split16": (("pqmf_analysis_split_kernel",), ()),
+    "pqmf_synthesis_split16": (("pqmf_synthesis_split_kernel",), ()),
+    "head_split16": (("encoder_head_kernel",), ()),
+    "tail_split16": (("decoder_tail_kernel",), ()),
 }
 _KERNEL_FAMILY = {}
-for _fam, (_main, _helpers) in FAMILIES.items():
-    _KERNEL_FAMILY[_main] = (_fam, True)
+for _fam, (_mains, _helpers) in FAMILIES.items():
+    for _m in _mains:
+        _KERNEL_FAMILY[_m] = (_fam, True)
     for _h in _helpers:
         _KERNEL_FAMILY[_h] = (_fam, False)
+
+
+def set_precision(precision: str) -> None:
+    """Exact-fp32 runs: the split kernels' separate K-split reduce belongs to
+    the fp32 ring convs (conv1d_ring_f32_kernel), not to a split16 family."""
+    if precision in ("f32", "f32_tuned"):
+        _KERNEL_FAMILY["split_reduce_kernel"] = ("conv_f32", False)
+
+
 _NAME = re.compile(r"(?:^|[\s:])([A-Za-z_][A-Za-z0-9_]*)\s*[<(]")
 
 
@@ -110,6 +122,7 @@ def main():
     ap.add_argument("--workload", default="v2,16,65536", help="config,batch,samples of the passes")
     ap.add_argument("--precision", default="auto", help="bench.py --precision of the passes")
     a = ap.parse_args()
+    set_precision(a.precision)
     s = trace_summary(a.trace)
     if a.fetch and a.write:
         fe = counter_by_family(a.fetch, "FETCH_SIZE")
