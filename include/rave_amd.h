@@ -364,15 +364,17 @@ int rave_residual_stack(const rave_stack_args* a, void* stream);
  *   bands = rave_pqmf_analysis(x, n_out_bands = conv_c_in, pad pqmf_pad_left)
  *   y[b, m, t] = bias[m] + sum_{c, j} W[m, c, j] * bands[b, c, t + j - conv_pad_left]
  *   x: audio (B, 1, 16 * frames), x_sb; y: (B, conv_c_out, frames).
- *   filter: hkf (16, 513); conv_c_in <= 8 bands, conv_c_out <= 64, conv_kernel 7.
+ *   filter: rave_encoder_head_pack_filter image; conv_c_in <= 8 bands, conv_c_out <= 64,
+ *   conv_kernel 7.
  *   fill_channels > 0: also fill_y[b, c, t] = fill_values[c], t < fill_t (the
  *   speaker concat of RAVE.encode, rave/model.py:618-620).
  * rave_decoder_tail: GeneratorV2's act + conv (rave/blocks.py:691-696), its
  * epilogue (:699-707) and CachedPQMF.inverse (rave/pqmf.py:275-284):
  *   w = bias + conv_k(act(x))          conv_c_in 64 -> conv_c_out 32 (mode 1) / 16 (mode 2)
  *   y = rave_pqmf_synthesis(w, mode, noise, pad pqmf_pad_left)
- *   x: (B, 64, frames); y: (B, 1, 16 * frames), 16-byte aligned.  filter: hki
- *   (16, 16, 33); act RAVE_ACT_LEAKY / RAVE_ACT_SNAKE (alpha: 64 floats).
+ *   x: (B, 64, frames); y: (B, 1, 16 * frames), 16-byte aligned.  filter:
+ *   rave_decoder_tail_pack_filter image; act RAVE_ACT_LEAKY / RAVE_ACT_SNAKE
+ *   (alpha: 64 floats).
  * weight: the conv's rave_conv1d_split_pack_weight image (7 taps, stride 1).
  */
 typedef struct rave_edge_args {
@@ -394,6 +396,14 @@ typedef struct rave_edge_args {
 } rave_edge_args;
 int rave_encoder_head(const rave_edge_args* a, void* stream);
 int rave_decoder_tail(const rave_edge_args* a, void* stream);
+/* `filter` of both: a pre-split image of the PQMF filter (the kernels' LDS
+ * layout: f16 hi / lo planes of 16 rows x 552, scaled by 2^e with max |h 2^e|
+ * in [8, 16), then the float 2^-(e+11)), RAVE_EDGE_FILTER_FLOATS floats.
+ * Head: phase-packed analysis rows (8p + k) of hkf (n_band, taps) for the
+ * first n_out_bands bands; tail: hki (n_band, n_band, taps) as K = tap*16 + c. */
+#define RAVE_EDGE_FILTER_FLOATS 8836
+int rave_encoder_head_pack_filter(const float* hkf, int n_band, int taps, int n_out_bands, float* image);
+int rave_decoder_tail_pack_filter(const float* hki, int n_band, int taps, float* image);
 
 /* ---------------------------------------------------------------- plans
  * A plan is a recorded sequence of the ops above (the module graph of

@@ -253,8 +253,9 @@ EXPORTS = [
     "rave_stream_encode", "rave_stream_decode", "rave_stream_encode_codes", "rave_stream_decode_codes",
     "rave_stream_delay",
     "rave_fir", "rave_row_stats", "rave_attn_pool", "rave_linear", "rave_maxpool",
-    "rave_encoder_head", "rave_decoder_tail",
+    "rave_encoder_head", "rave_decoder_tail", "rave_encoder_head_pack_filter", "rave_decoder_tail_pack_filter",
 ]
+EDGE_FILTER_FLOATS = 8836   # RAVE_EDGE_FILTER_FLOATS
 
 
 class NativeError(RuntimeError):
@@ -280,6 +281,8 @@ def _load():
     lib.rave_conv1d_split_packed_size.restype = i64
     lib.rave_conv1d_split_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
     lib.rave_conv1d_ring_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
+    lib.rave_encoder_head_pack_filter.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp]
+    lib.rave_decoder_tail_pack_filter.argtypes = [vp, C.c_int, C.c_int, vp]
     lib.rave_unit_packed_size.argtypes = [C.c_int]
     lib.rave_unit_packed_size.restype = i64
     lib.rave_unit_pack_weight.argtypes = [vp, vp, C.c_int, vp]
@@ -436,6 +439,21 @@ def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed, out_s
     out = np.zeros(n, np.float32)
     check(pack_fn(w.ctypes.data, c_in, c_out, kernel, stride, dilation,
                   int(transposed), int(out_shift), out.ctypes.data), "pack_weight")
+    return out
+
+
+def pack_edge_filter(filt, head: bool, n_out_bands: int = 6):
+    """PQMF filter -> the fused edges' pre-split image (numpy float32):
+    head: hkf (16, taps) analysis rows; tail: hki (16, 16, taps)."""
+    import numpy as np
+    f = np.ascontiguousarray(filt, dtype=np.float32)
+    out = np.zeros(EDGE_FILTER_FLOATS, np.float32)
+    if head:
+        check(lib.rave_encoder_head_pack_filter(f.ctypes.data, f.shape[0], f.shape[-1], int(n_out_bands),
+                                                out.ctypes.data), "encoder_head_pack_filter")
+    else:
+        check(lib.rave_decoder_tail_pack_filter(f.ctypes.data, f.shape[0], f.shape[-1], out.ctypes.data),
+              "decoder_tail_pack_filter")
     return out
 
 

@@ -32,6 +32,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cmath>
 
 namespace rave {
 
@@ -47,6 +48,14 @@ constexpr int kEdgeKW = 544;                       // PQMF K extent (17 steps of
 constexpr int kEdgeFP = 552;                       // halves per filter row (conflict-free b128)
 constexpr int kSynTapsE = 33;
 constexpr int kAnaTapsE = 513;
+
+// Host-split PQMF filter image (rave_encoder_head_pack_filter /
+// rave_decoder_tail_pack_filter): the kernel's LDS layout verbatim -- hi plane
+// [16 rows][kEdgeFP halves] then lo plane -- with the filter scaled by 2^e
+// (max |h 2^e| in [8, 16)), followed by one float 2^-(e + 11).  A workgroup
+// copies it with 16-byte loads instead of converting the fp32 filter.
+constexpr int kEdgeFilterHalves = 2 * 16 * kEdgeFP;
+constexpr int kEdgeFilterFloats = kEdgeFilterHalves / 2 + 4;
 
 // launch geometry the host derives from the args
 struct EdgeGeo {
@@ -72,34 +81,6 @@ __device__ __forceinline__ void e_split(float v, _Float16& hi, _Float16& lo) {
     lo = (_Float16)((v - (float)hi) * 2048.0f);
 }
 
-// 2^e with max |h 2^e| in [8, 16) for a filter maximum m (1 if m == 0)
-__device__ __forceinline__ float e_filter_scale(float m) {
-    if (!(m > 0.f)) return 1.f;
-    int e;
-    (void)frexpf(m, &e);
-    return ldexpf(1.f, 4 - e);
-}
-
-// workgroup maxima of two per-thread values through `red` (2 * kEdgeWaves floats)
-__device__ __forceinline__ void e_block_max2(float& a, float& b, float* red) {
-    a = wave_max(a);
-    b = wave_max(b);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) {
-        red[wave] = a;
-        red[kEdgeWaves + wave] = b;
-    }
-    __syncthreads();
-    float ma = red[0], mb = red[kEdgeWaves];
-#pragma unroll
-    for (int w = 1; w < kEdgeWaves; ++w) {
-        ma = fmaxf(ma, red[w]);
-        mb = fmaxf(mb, red[kEdgeWaves + w]);
-    }
-    a = ma;
-    b = mb;
-}
-
 // split-f16 conv weight image (rave_conv1d_split_pack_weight, 7 taps, stride 1):
 // [chunk of 16 in-channels][32-row block mb][tap][hi|lo][64 lanes][8 halves],
 // then one float row scale 2^-(e_m + 11) per padded row
@@ -113,6 +94,19 @@ struct EdgeW {
         return __builtin_bit_cast(e_h8, __builtin_amdgcn_raw_buffer_load_b128(rs, off(chunk, mb, tap, plane, lane), 0, 0));
     }
 };
+
+// Diagnostic stage cut (tools/probes/edge_probe.hip builds with -DRAVE_EDGE_STOP=n;
+// off in the product): end the kernel after stage n, sinking one value so the
+// work before it stays live.
+#ifdef RAVE_EDGE_STOP
+#define EDGE_STOP(n, v)                                                   \
+    if (RAVE_EDGE_STOP == (n)) {                                          \
+        if (threadIdx.x == 0) a.y[(int64_t)blockIdx.x] = (float)(v);      \
+        return;                                                           \
+    }
+#else
+#define EDGE_STOP(n, v)
+#endif
 
 template <int V> struct EdgeN {
     static constexpr int value = V;
@@ -129,7 +123,7 @@ constexpr int kHBP = 24;                            // halves per band-plane row
 constexpr int kHXS = 512 * (kHAB - 1) + 32 * 15 + kEdgeKW;   // window samples (5120 + 32)
 __host__ __device__ constexpr int e_xi(int i) { return i + 8 * (i >> 7); }   // 8 halves of pad per 128
 constexpr int kHXP = e_xi(kHXS) + 8;                // halves per window plane
-constexpr int kHeadLds = (2 * 16 * kEdgeFP + 2 * kHXP + 2 * kHBR * kHBP) * 2 + 4 * kEdgeWaves * 4;
+constexpr int kHeadLds = (2 * 16 * kEdgeFP + 2 * kHXP + 2 * kHBR * kHBP) * 2 + 4 * kEdgeWaves * 4 + 16;
 
 __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a, EdgeGeo geo) {
     const int tiles = geo.tiles;
@@ -145,41 +139,33 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nmain = tiles * a.batch;
 
-    if ((int)blockIdx.x >= nmain) {
-        // the speaker concat of RAVE.encode: one workgroup per batch item
-        const int b = blockIdx.x - nmain;
+    const int lg = __builtin_amdgcn_readfirstlane(xcd_major(blockIdx.x, nmain));
+    const int b = lg / tiles;
+    const int tile = lg - b * tiles;
+    const int n0 = tile * kHF;
+    if (a.fill_channels > 0) {
+        // the speaker concat of RAVE.encode: the batch item's tiles share its rows
         float* z = a.fill_y + (int64_t)b * a.f_sb;
         const int n = a.fill_channels * a.fill_t;
-        for (int i = tid; i < n; i += kEdgeNT) {
+        for (int i = tile * kEdgeNT + tid; i < n; i += tiles * kEdgeNT) {
             const int c = i / a.fill_t, t = i - c * a.fill_t;
             z[(int64_t)c * a.f_sc + t] = a.fill_values[c];
         }
-        return;
     }
-    const int lg = __builtin_amdgcn_readfirstlane(xcd_major(blockIdx.x, nmain));
-    const int b = lg / tiles;
-    const int n0 = (lg - b * tiles) * kHF;
     const int F = a.frames;
     const int T = F * 16;
-    const int NB = a.conv_c_in;                     // bands the encoder reads (<= 8)
     const int g0 = n0 - a.conv_pad_left;            // band frame of band-plane row 0
     const int s0 = 16 * g0 - a.pqmf_pad_left;       // audio sample of window sample 0
 
-    // ---- operands into registers: phase-packed filter rows, audio window
-    // filter row 8p + k, K index j: h_k[j - 16 p] (zero outside [0, 513), k >= NB)
-    constexpr int HT = (16 * kEdgeKW + kEdgeNT - 1) / kEdgeNT;    // 17
-    float hv[HT];
-    float amax = 0.f;
-#pragma unroll
-    for (int it = 0; it < HT; ++it) {
-        const int i = tid + it * kEdgeNT;
-        const int r = i / kEdgeKW, j = i - r * kEdgeKW;
-        const int p = r >> 3, k = r & 7, jj = j - 16 * p;
-        const bool ok = k < NB && jj >= 0 && jj < kAnaTapsE;
-        const float v = a.filter[(int64_t)min(k, NB - 1) * kAnaTapsE + min(max(jj, 0), kAnaTapsE - 1)];
-        hv[it] = ok ? v : 0.f;
-        amax = fmaxf(amax, fabsf(hv[it]));
+    unsigned char* vote = reinterpret_cast<unsigned char*>(red + 4 * kEdgeWaves);
+    // ---- phase-packed filter image -> LDS (16-byte copies); audio window,
+    // split optimistically (no scale) with a per-wave range vote
+    {
+        const e_h8* src = reinterpret_cast<const e_h8*>(a.filter);
+        e_h8* dst = reinterpret_cast<e_h8*>(fh);
+        for (int i = tid; i < kEdgeFilterHalves / 8; i += kEdgeNT) dst[i] = src[i];
     }
+    const float f_unscale = a.filter[kEdgeFilterHalves / 2];        // 2^-(e + 11)
     constexpr int XT = (kHXS + kEdgeNT - 1) / kEdgeNT;             // 11
     const float* xb = a.x + (int64_t)b * a.x_sb;
     float xv[XT];
@@ -192,31 +178,36 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
         xv[it] = (i < kHXS && t >= 0 && t < T) ? v : 0.f;
         xmax = fmaxf(xmax, fabsf(xv[it]));
     }
-    e_block_max2(amax, xmax, red);
-    const float sc = e_filter_scale(amax);
-    const float xs = ldexpf(1.f, -split_shift(xmax));
-#pragma unroll
-    for (int it = 0; it < HT; ++it) {
-        const int i = tid + it * kEdgeNT;
-        const int r = i / kEdgeKW, j = i - r * kEdgeKW;
-        e_split(hv[it] * sc, fh[r * kEdgeFP + j], fl[r * kEdgeFP + j]);
-    }
 #pragma unroll
     for (int it = 0; it < XT; ++it) {
         const int i = tid + it * kEdgeNT;
-        if (i < kHXS) e_split(xv[it] * xs, xh[e_xi(i)], xl[e_xi(i)]);
+        if (i < kHXS) e_split(xv[it], xh[e_xi(i)], xl[e_xi(i)]);
     }
+    vote_cast(vote, wave, xmax);
     // band-plane channels 8..15 stay zero (the conv chunk is 16 channels wide)
     for (int i = tid; i < kHBR; i += kEdgeNT) {
         *reinterpret_cast<e_h8*>(bh + i * kHBP + 8) = e_h8{0, 0, 0, 0, 0, 0, 0, 0};
         *reinterpret_cast<e_h8*>(bl + i * kHBP + 8) = e_h8{0, 0, 0, 0, 0, 0, 0, 0};
     }
     __syncthreads();
+    float xs = 1.f;
+    if (__builtin_expect(vote_any<kEdgeWaves>(vote), 0)) {
+        // rare: audio at 2^15 or beyond -- the window again as x 2^-s
+        xs = ldexpf(1.f, -__builtin_amdgcn_readfirstlane(split_shift(block_max<kEdgeWaves>(xmax, red))));
+#pragma unroll
+        for (int it = 0; it < XT; ++it) {
+            const int i = tid + it * kEdgeNT;
+            if (i < kHXS) e_split(xv[it] * xs, xh[e_xi(i)], xl[e_xi(i)]);
+        }
+        __syncthreads();
+    }
+    EDGE_STOP(1, xh[tid] + fh[tid])
 
     // ---- analysis: block blk, column n = frame pair (frames 32 blk + 2n + p)
     const int g = lane >> 4, col = lane & 15;
+    // three independent accumulator chains (one per product), summed at the end
     auto analysis_block = [&](int blk, e_f32x4& acc) __attribute__((always_inline)) {
-        acc = e_f32x4{0.f, 0.f, 0.f, 0.f};
+        e_f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0;
 #pragma unroll
         for (int s = 0; s < kEdgeKW / 32; ++s) {
             const int ka = col * kEdgeFP + 32 * s + 8 * g;
@@ -226,14 +217,15 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
             const int xi = e_xi(512 * blk + 32 * col + 32 * s + 8 * g);
             const e_h8 xh8 = *reinterpret_cast<const e_h8*>(xh + xi);
             const e_h8 xl8 = *reinterpret_cast<const e_h8*>(xl + xi);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, xh8, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, xl8, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, xh8, acc, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, xh8, c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, xl8, c1, 0, 0, 0);
+            c2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, xh8, c2, 0, 0, 0);
         }
+        acc = (c0 + c1) + c2;
     };
     // acc rows 4g + r = (p = g >> 1, k = 4 (g & 1) + r); value = band k of frame
     // g0 + 32 blk + 2 col + p (reverse_half, zero outside [0, F))
-    const float unscale = 1.0f / (sc * 2048.0f * xs);
+    const float unscale = f_unscale / xs;
     auto band_values = [&](int blk, const e_f32x4& acc, e_f32x4& v, float& m) __attribute__((always_inline)) {
         const int p = g >> 1;
         const int f = g0 + 32 * blk + 2 * col + p;
@@ -256,10 +248,7 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
         analysis_block(wave + kEdgeWaves, acc1);
         band_values(wave + kEdgeWaves, acc1, v1, bmax);
     }
-    float dummy = 0.f;
-    e_block_max2(bmax, dummy, red + 2 * kEdgeWaves);
-    const float bs = ldexpf(1.f, -split_shift(bmax));             // band planes' range scale
-    auto put_bands = [&](int blk, const e_f32x4& v) __attribute__((always_inline)) {
+    auto put_bands = [&](int blk, const e_f32x4& v, float bs) __attribute__((always_inline)) {
         const int row = 32 * blk + 2 * col + (g >> 1);
         e_h4 hv4, lv4;
 #pragma unroll
@@ -272,19 +261,9 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
         *reinterpret_cast<e_h4*>(bh + row * kHBP + 4 * (g & 1)) = hv4;
         *reinterpret_cast<e_h4*>(bl + row * kHBP + 4 * (g & 1)) = lv4;
     };
-    put_bands(wave, v0);
-    if (extra) put_bands(wave + kEdgeWaves, v1);
-    __syncthreads();
-
-    // ---- conv (7 taps, 16-channel chunk, rows 0..63): wave = 32 output columns
+    // the conv's weight fragments (no data dependence): in flight across the band barrier
     const EdgeW W{e_rsrc(a.weight, (int64_t)geo.w_bytes), geo.w_mb};
-    const int h = lane >> 5, l32 = lane & 31;
     const int MB = (a.conv_c_out + 31) / 32;        // 1 or 2 row blocks
-    e_f32x16 acc[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
     e_h8 wr[kEdgeK7][2][2];
 #pragma unroll
     for (int q = 0; q < kEdgeK7; ++q)
@@ -292,6 +271,27 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int pl = 0; pl < 2; ++pl) wr[q][j][pl] = j < MB ? W.frag(0, j, q, pl, lane) : e_h8{};
+    // band planes split optimistically, with a range vote (rare: a rescale by 2^-s)
+    put_bands(wave, v0, 1.f);
+    if (extra) put_bands(wave + kEdgeWaves, v1, 1.f);
+    vote_cast(vote + 8, wave, bmax);
+    __syncthreads();
+    float bs = 1.f;
+    if (__builtin_expect(vote_any<kEdgeWaves>(vote + 8), 0)) {
+        bs = ldexpf(1.f, -__builtin_amdgcn_readfirstlane(split_shift(block_max<kEdgeWaves>(bmax, red))));
+        put_bands(wave, v0, bs);
+        if (extra) put_bands(wave + kEdgeWaves, v1, bs);
+        __syncthreads();
+    }
+    EDGE_STOP(2, bh[tid] + bl[tid])
+
+    // ---- conv (7 taps, 16-channel chunk, rows 0..63): wave = 32 output columns
+    const int h = lane >> 5, l32 = lane & 31;
+    e_f32x16 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 #pragma unroll
     for (int q = 0; q < kEdgeK7; ++q) {
         const int row = 32 * wave + l32 + q;
@@ -306,6 +306,7 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
             acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh8, wr[q][j][1], acc[j], 0, 0, 0);
         }
     }
+    EDGE_STOP(3, acc[0][0] + acc[1][7])
     // epilogue: lane = output channel m, registers 4c..4c+3 = 4 consecutive frames
     const float* rsc = a.weight + geo.w_frag_floats;
     const float inv_bs = 1.0f / bs;
@@ -349,7 +350,7 @@ constexpr int kTSW = kTF + kSynTapsE + 1;           // synthesis window rows (29
 constexpr int kTSP = 24;                            // halves per synthesis row
 constexpr int kTPlane = 2 * kTXR * kTXP;            // halves of the two act(x) planes
 static_assert(2 * kTSW * kTSP <= kTPlane, "synthesis planes reuse the act(x) planes");
-constexpr int kTailLds = (2 * 16 * kEdgeFP + kTPlane) * 2 + 2 * kEdgeWaves * 4;
+constexpr int kTailLds = (2 * 16 * kEdgeFP + kTPlane) * 2 + 2 * kEdgeWaves * 4 + 16;
 
 template <bool SNAKE, bool AM>
 __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a, EdgeGeo geo) {
@@ -373,77 +374,9 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
     const int x0 = f0 - a.conv_pad_left;             // input frame of act(x) row 0
     const float slope = a.leaky_slope;
 
-    // ---- operands into registers: synthesis filter (K = tap * 16 + c), act(x)
-    constexpr int KD = 16 * kSynTapsE;               // 528
-    constexpr int HT = (16 * KD + kEdgeNT - 1) / kEdgeNT;   // 17 (coalesced reads of hki rows)
-    float hv[HT];
-    float amax = 0.f;
-#pragma unroll
-    for (int it = 0; it < HT; ++it) {
-        const int i = min(tid + it * kEdgeNT, 16 * KD - 1);
-        hv[it] = a.filter[i];                        // hki[m][c][tap], i = m*528 + c*33 + tap
-        amax = fmaxf(amax, fabsf(hv[it]));
-    }
-    constexpr int XT = (kTC * kTXR + kEdgeNT - 1) / kEdgeNT;   // 41
-    const float* xb = a.x + (int64_t)b * a.x_sb;
-    float xv[XT];
-    float xmax = 0.f;
-#pragma unroll
-    for (int it = 0; it < XT; ++it) {
-        const int i = tid + it * kEdgeNT;
-        const int c = i / kTXR, w = i - c * kTXR;
-        const int t = x0 + w;
-        const bool ok = i < kTC * kTXR && t >= 0 && t < F;
-        const int cc = min(c, kTC - 1);
-        const float v = xb[(int64_t)cc * a.x_sc + min(max(t, 0), F - 1)];
-        float r = v;
-        if constexpr (SNAKE) {
-            const float al = a.alpha[cc];
-            r = v + (1.0f / (al + 1e-9f)) * sin_squared(al * v);
-        } else {
-            r = v > 0.f ? v : v * slope;
-        }
-        xv[it] = ok ? r : 0.f;
-        xmax = fmaxf(xmax, fabsf(xv[it]));
-    }
-    e_block_max2(amax, xmax, red);
-    const float sc = e_filter_scale(amax);
-    const float xs = ldexpf(1.f, -split_shift(xmax));
-#pragma unroll
-    for (int it = 0; it < HT; ++it) {
-        const int i = tid + it * kEdgeNT;
-        if (i < 16 * KD) {
-            const int m = i / KD, rem = i - m * KD;
-            const int c = rem / kSynTapsE, tap = rem - c * kSynTapsE;
-            const int k = tap * 16 + c;
-            e_split(hv[it] * sc, fh[m * kEdgeFP + k], fl[m * kEdgeFP + k]);
-        }
-    }
-    for (int i = tid; i < 16 * (kEdgeKW - KD); i += kEdgeNT) {     // K rows 528..543
-        const int m = i / (kEdgeKW - KD), k = KD + i % (kEdgeKW - KD);
-        fh[m * kEdgeFP + k] = (_Float16)0.f;
-        fl[m * kEdgeFP + k] = (_Float16)0.f;
-    }
-#pragma unroll
-    for (int it = 0; it < XT; ++it) {
-        const int i = tid + it * kEdgeNT;
-        if (i < kTC * kTXR) {
-            const int c = i / kTXR, w = i - c * kTXR;
-            e_split(xv[it] * xs, xh[w * kTXP + c], xl[w * kTXP + c]);
-        }
-    }
-    __syncthreads();
-
-    // ---- conv: 32 rows (16 wave + 16 amplitude channels, or 16 + padding),
-    // K = 4 chunks x 7 taps; wave w owns column blocks w (and w + 8)
+    unsigned char* vote = reinterpret_cast<unsigned char*>(red + 2 * kEdgeWaves);
+    // ---- the conv's first weight fragments (no data dependence): issued first
     const EdgeW W{e_rsrc(a.weight, (int64_t)geo.w_bytes), geo.w_mb};
-    const int h = lane >> 5, l32 = lane & 31;
-    e_f32x16 acc[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-    const bool two = wave + kEdgeWaves < kTB;
     constexpr int KS = (kTC / 16) * kEdgeK7;          // 28 K-steps
     constexpr int RING = 4;
     e_h8 wr[RING][2];
@@ -451,8 +384,88 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
     for (int s = 0; s < RING; ++s)
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl) wr[s][pl] = W.frag(s / kEdgeK7, 0, s % kEdgeK7, pl, lane);
-    auto kstep = [&](int s, auto nblk) __attribute__((always_inline)) {
-        constexpr int NBK = decltype(nblk)::value;
+    // ---- synthesis filter image -> LDS (16-byte copies); act(x) in 4-channel
+    // groups (coalesced along time), split optimistically with a range vote
+    {
+        const e_h8* src = reinterpret_cast<const e_h8*>(a.filter);
+        e_h8* dst = reinterpret_cast<e_h8*>(fh);
+        for (int i = tid; i < kEdgeFilterHalves / 8; i += kEdgeNT) dst[i] = src[i];
+    }
+    const float f_unscale = a.filter[kEdgeFilterHalves / 2];        // 2^-(e + 11)
+    constexpr int NG = kTC / 4;                                      // 4-channel groups
+    constexpr int XT = (NG * kTXR + kEdgeNT - 1) / kEdgeNT;          // 11
+    const float* xb = a.x + (int64_t)b * a.x_sb;
+    e_f32x4 xv[XT];
+    float xmax = 0.f;
+#pragma unroll
+    for (int it = 0; it < XT; ++it) {
+        const int i = tid + it * kEdgeNT;
+        const int cg = i / kTXR, w = i - cg * kTXR;
+        const int t = x0 + w;
+        const bool ok = i < NG * kTXR && t >= 0 && t < F;
+        const int tt = min(max(t, 0), F - 1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int cc = min(4 * cg + e, kTC - 1);
+            const float v = xb[(int64_t)cc * a.x_sc + tt];
+            float r;
+            if constexpr (SNAKE) {
+                const float al = a.alpha[cc];
+                r = v + (1.0f / (al + 1e-9f)) * sin_squared(al * v);
+            } else {
+                r = v > 0.f ? v : v * slope;
+            }
+            xv[it][e] = ok ? r : 0.f;
+            xmax = fmaxf(xmax, fabsf(xv[it][e]));
+        }
+    }
+    auto put_x = [&](float xs) __attribute__((always_inline)) {
+#pragma unroll
+        for (int it = 0; it < XT; ++it) {
+            const int i = tid + it * kEdgeNT;
+            if (i < NG * kTXR) {
+                const int cg = i / kTXR, w = i - cg * kTXR;
+                const e_f32x4 v = xv[it] * xs;
+                const e_h4 hi = __builtin_convertvector(v, e_h4);
+                const e_h4 lo = __builtin_convertvector((v - __builtin_convertvector(hi, e_f32x4)) * 2048.0f, e_h4);
+                *reinterpret_cast<e_h4*>(xh + w * kTXP + 4 * cg) = hi;
+                *reinterpret_cast<e_h4*>(xl + w * kTXP + 4 * cg) = lo;
+            }
+        }
+    };
+    put_x(1.f);
+    vote_cast(vote, wave, xmax);
+    __syncthreads();
+    float xs = 1.f;
+    if (__builtin_expect(vote_any<kEdgeWaves>(vote), 0)) {
+        // rare: act(x) at 2^15 or beyond -- the window again as act(x) 2^-s
+        xs = ldexpf(1.f, -__builtin_amdgcn_readfirstlane(split_shift(block_max<kEdgeWaves>(xmax, red))));
+        put_x(xs);
+        __syncthreads();
+    }
+    EDGE_STOP(1, xh[tid] + fh[tid])
+
+    // ---- conv: 32 rows (16 wave + 16 amplitude channels, or 16 + padding),
+    // K = 4 chunks x 7 taps.  Wave w owns column block w; the last two blocks
+    // (8, 9) are split by K: wave w also takes block 8 + (w >> 2) over chunk w & 3
+    // (its 7 K-steps share the main block's weight fragments), and the four
+    // partial tiles of each meet in LDS in chunk order.
+    static_assert(kTB == kEdgeWaves + 2 && KS == 4 * kEdgeK7, "tail conv balance");
+    const int h = lane >> 5, l32 = lane & 31;
+    e_f32x16 acc, acl, acc_x, acl_x;                  // main block, K-split block; hi x hi / lo-term chains
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = acl[r] = acc_x[r] = acl_x[r] = 0.f;
+    const int xblk = kEdgeWaves + (wave >> 2), xchunk = wave & 3;
+    auto mfma3 = [&](int row, int ch, const e_h8& b2, const e_h8& bh8, const e_h8& bl8, e_f32x16& c0,
+                     e_f32x16& c1) __attribute__((always_inline)) {
+        const e_h8 xh8 = *reinterpret_cast<const e_h8*>(xh + row * kTXP + 16 * ch + 8 * h);
+        const e_h8 xl8 = *reinterpret_cast<const e_h8*>(xl + row * kTXP + 16 * ch + 8 * h);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh8, b2, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl8, bh8, c1, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh8, bl8, c1, 0, 0, 0);
+    };
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
         const int ch = s / kEdgeK7, q = s - ch * kEdgeK7;
         const e_h8 bh8 = wr[s % RING][0], bl8 = wr[s % RING][1];
         if (s + RING < KS) {
@@ -461,73 +474,77 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
             for (int pl = 0; pl < 2; ++pl) wr[s % RING][pl] = W.frag(s2 / kEdgeK7, 0, s2 % kEdgeK7, pl, lane);
         }
         const e_h8 b2 = bh8 * (_Float16)2048.0f;
-#pragma unroll
-        for (int j = 0; j < NBK; ++j) {
-            const int row = 32 * (wave + kEdgeWaves * j) + l32 + q;
-            const e_h8 xh8 = *reinterpret_cast<const e_h8*>(xh + row * kTXP + 16 * ch + 8 * h);
-            const e_h8 xl8 = *reinterpret_cast<const e_h8*>(xl + row * kTXP + 16 * ch + 8 * h);
-            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh8, b2, acc[j], 0, 0, 0);
-            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl8, bh8, acc[j], 0, 0, 0);
-            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh8, bl8, acc[j], 0, 0, 0);
-        }
-    };
-    if (two) {
-#pragma unroll
-        for (int s = 0; s < KS; ++s) kstep(s, EdgeN<2>{});
-    } else {
-#pragma unroll
-        for (int s = 0; s < KS; ++s) kstep(s, EdgeN<1>{});
+        mfma3(32 * wave + l32 + q, ch, b2, bh8, bl8, acc, acl);
+        if (ch == xchunk) mfma3(32 * xblk + l32 + q, ch, b2, bh8, bl8, acc_x, acl_x);
     }
+    acc += acl;
+    acc_x += acl_x;
+    __syncthreads();                                 // act(x) planes dead
+    // the K-split blocks' partial tiles -> LDS (past the synthesis planes), summed
+    // in chunk order by waves 0 (block 8) and 4 (block 9)
+    float* part = reinterpret_cast<float*>(xh + 2 * kTSW * kTSP);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) part[(wave * 16 + r) * 64 + lane] = acc_x[r];
+    __syncthreads();
+    const bool has_x = (wave & 3) == 0;
+    if (has_x) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float v = part[((wave + 0) * 16 + r) * 64 + lane];
+#pragma unroll
+            for (int c = 1; c < 4; ++c) v += part[((wave + c) * 16 + r) * 64 + lane];
+            acc_x[r] = v;
+        }
+    }
+    EDGE_STOP(2, acc[0] + acc_x[5])
     // ---- epilogue: wave/amplitude pairs -> x * sigmoid(a) (+ noise) -> tanh ->
     // reverse_half -> synthesis planes (zero outside [0, F))
     const float* rsc = a.weight + geo.w_frag_floats;
-    const float rs = rsc[l32] / xs;
+    const float rs = rsc[l32] / xs;                   // the conv's row scale and the act(x) range scale
     const float bias = (a.bias && l32 < a.conv_c_out) ? a.bias[l32] : 0.f;
     const float* nz = a.noise ? a.noise + (int64_t)b * a.n_sb : nullptr;
-    float sv[2][16];
+    // Lanes pair up across the 16-row halves (l32 and l32 ^ 16 hold the same
+    // frames): the low lane finishes positions r < 8 of channel c = l32 & 15, the
+    // high lane positions r >= 8, each taking the other half of the (wave,
+    // amplitude) pair by one xor-shuffle -- every lane works, 8 outputs each.
+    const int c_out = l32 & 15;
+    const bool lo_half = l32 < 16;
+    const float* nzc = nz ? nz + (int64_t)c_out * a.n_sc : nullptr;
+    auto put_block = [&](int blk, const e_f32x16& c) __attribute__((always_inline)) {
+        float v[16];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        if (j == 1 && !two) break;
-        const int blk = wave + kEdgeWaves * j;
+        for (int r = 0; r < 16; ++r) v[r] = c[r] * rs + bias;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float v = acc[j][r] * rs + bias;
-            float out = v;
+        for (int k = 0; k < 8; ++k) {
+            const float recv = __shfl_xor(lo_half ? v[k + 8] : v[k], 16);
+            const int r = lo_half ? k : k + 8;
+            float out = lo_half ? v[k] : recv;              // the wave channel's value
             if constexpr (AM) {
-                const float amp = __shfl(v, (lane + 16) & 63);   // lane l32 + 16: channel + 16, same frames
-                out = v * (1.0f / (1.0f + __expf(-amp)));
+                const float amp = lo_half ? recv : v[k + 8];  // its amplitude channel (+16)
+                out = out * __builtin_amdgcn_rcpf(1.0f + __expf(-amp));
             }
             const int w = 32 * blk + 8 * (r >> 2) + 4 * h + (r & 3);
             const int f = f0 + w;
-            const bool ok = f >= 0 && f < F && l32 < 16;
-            if (nz && ok) out = out + nz[(int64_t)l32 * a.n_sc + f];
-            out = tanhf(out);
-            if ((l32 & 1) && !(f & 1)) out = -out;
-            sv[j][r] = ok ? out : 0.f;
+            const bool ok = f >= 0 && f < F;
+            if (nzc && ok) out = out + nzc[f];
+            // tanh(x) = 1 - 2 / (e^2x + 1): saturates to +-1 through inf / 0
+            out = 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * out) + 1.0f);
+            if ((c_out & 1) && !(f & 1)) out = -out;
+            if (w < kTSW) e_split(ok ? out : 0.f, sh[w * kTSP + c_out], sl[w * kTSP + c_out]);
         }
-    }
-    __syncthreads();                                 // act(x) planes dead: the synthesis planes reuse them
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        if (j == 1 && !two) break;
-        const int blk = wave + kEdgeWaves * j;
-        if (l32 < 16) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int w = 32 * blk + 8 * (r >> 2) + 4 * h + (r & 3);
-                if (w < kTSW) e_split(sv[j][r], sh[w * kTSP + l32], sl[w * kTSP + l32]);
-            }
-        }
-    }
+    };
+    put_block(wave, acc);
+    if (has_x) put_block(xblk, acc_x);
     __syncthreads();
+    EDGE_STOP(3, sh[tid] + fl[tid])
 
     // ---- synthesis (as pqmf_synthesis_split_kernel): wave = 2 blocks of 16 frames
     const int g = lane >> 4, col = lane & 15;
     constexpr int BLK = kTF / (16 * kEdgeWaves);     // 2
     const int fb = wave * BLK * 16;
-    e_f32x4 sacc[BLK];
+    e_f32x4 sacc[BLK], sac1[BLK], sac2[BLK];
 #pragma unroll
-    for (int q = 0; q < BLK; ++q) sacc[q] = e_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < BLK; ++q) sacc[q] = sac1[q] = sac2[q] = e_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < kEdgeKW / 32; ++s) {
         const int ka = col * kEdgeFP + 32 * s + 8 * g;
@@ -541,11 +558,13 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
             const e_h8 b_h = *reinterpret_cast<const e_h8*>(sh + xi);
             const e_h8 b_l = *reinterpret_cast<const e_h8*>(sl + xi);
             sacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, b_h, sacc[q], 0, 0, 0);
-            sacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, b_l, sacc[q], 0, 0, 0);
-            sacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, b_h, sacc[q], 0, 0, 0);
+            sac1[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, b_l, sac1[q], 0, 0, 0);
+            sac2[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, b_h, sac2[q], 0, 0, 0);
         }
     }
-    const float o = 16.f / (sc * 2048.0f);
+#pragma unroll
+    for (int q = 0; q < BLK; ++q) sacc[q] = (sacc[q] + sac1[q]) + sac2[q];
+    const float o = 16.f * f_unscale;
     float* yb = a.y + (int64_t)b * a.y_sb;
 #pragma unroll
     for (int q = 0; q < BLK; ++q) {
@@ -584,6 +603,63 @@ static int edge_lds_attr(K kern, int lds, bool& done) {
     return RAVE_OK;
 }
 
+// ------------------------------------------------------------ filter images
+static int edge_row_exponent(double amax) {   // max |h 2^e| in [8, 16)
+    if (!(amax > 0.0)) return 0;
+    int e = (int)std::floor(std::log2(16.0 / amax));
+    while (std::ldexp(amax, e) >= 16.0) --e;
+    while (std::ldexp(amax, e) < 8.0) ++e;
+    return e;
+}
+
+// A[r][k] (16 rows x kEdgeKW, zero beyond) -> hi / lo planes + 2^-(e + 11)
+template <typename Fn>
+static void edge_filter_image(Fn&& A, float* image) {
+    double amax = 0.0;
+    for (int r = 0; r < 16; ++r)
+        for (int k = 0; k < kEdgeKW; ++k) amax = std::max(amax, std::fabs((double)A(r, k)));
+    const int e = edge_row_exponent(amax);
+    _Float16* hi = reinterpret_cast<_Float16*>(image);
+    _Float16* lo = hi + 16 * kEdgeFP;
+    for (int r = 0; r < 16; ++r)
+        for (int k = 0; k < kEdgeFP; ++k) {
+            const float v = k < kEdgeKW ? (float)std::ldexp((double)A(r, k), e) : 0.f;
+            const _Float16 vh = (_Float16)v;
+            hi[r * kEdgeFP + k] = vh;
+            lo[r * kEdgeFP + k] = (_Float16)((v - (float)vh) * 2048.0f);
+        }
+    image[kEdgeFilterHalves / 2] = (float)std::ldexp(1.0, -(e + 11));
+    for (int i = kEdgeFilterHalves / 2 + 1; i < kEdgeFilterFloats; ++i) image[i] = 0.f;
+}
+
+extern "C" int rave_encoder_head_pack_filter(const float* hkf, int n_band, int taps, int n_out_bands, float* image) {
+    RAVE_CHECK_ARG(hkf && image, "encoder_head_pack_filter: null pointer");
+    if (n_band != 16 || taps != kAnaTapsE || n_out_bands < 1 || n_out_bands > 8) {
+        set_error("encoder_head_pack_filter: built for 16 bands, 513 taps, <= 8 output bands");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    // row 8p + k, K index j: h_k[j - 16 p] (phase p = 0, 1)
+    edge_filter_image([&](int r, int j) -> float {
+        const int p = r >> 3, k = r & 7, jj = j - 16 * p;
+        return (k < n_out_bands && jj >= 0 && jj < taps) ? hkf[(int64_t)k * taps + jj] : 0.f;
+    }, image);
+    return RAVE_OK;
+}
+
+extern "C" int rave_decoder_tail_pack_filter(const float* hki, int n_band, int taps, float* image) {
+    RAVE_CHECK_ARG(hki && image, "decoder_tail_pack_filter: null pointer");
+    if (n_band != 16 || taps != kSynTapsE) {
+        set_error("decoder_tail_pack_filter: built for 16 bands, 33 taps");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    // row m, K index tap * 16 + c: hki[m][c][tap]
+    edge_filter_image([&](int m, int k) -> float {
+        const int tap = k >> 4, c = k & 15;
+        return tap < taps ? hki[((int64_t)m * n_band + c) * taps + tap] : 0.f;
+    }, image);
+    return RAVE_OK;
+}
+
 extern "C" int rave_encoder_head(const rave_edge_args* p, void* stream) {
     RAVE_CHECK_ARG(p && p->x && p->y && p->weight && p->filter, "encoder_head: null pointer");
     const rave_edge_args& a = *p;
@@ -599,7 +675,7 @@ extern "C" int rave_encoder_head(const rave_edge_args* p, void* stream) {
     static bool attr = false;
     const int rc = edge_lds_attr(encoder_head_kernel, kHeadLds, attr);
     if (rc != RAVE_OK) return rc;
-    const int grid = g.tiles * a.batch + (a.fill_channels > 0 ? a.batch : 0);
+    const int grid = g.tiles * a.batch;
     launch(encoder_head_kernel, dim3(grid), dim3(kEdgeNT), (uint32_t)kHeadLds, as_stream(stream), a, g);
     return launch_status("encoder_head_kernel");
 }

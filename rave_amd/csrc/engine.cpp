@@ -16,6 +16,8 @@
 //                   two convs, every stack against its units; the fastest wins.
 #include "engine.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -329,6 +331,7 @@ struct Model {
     std::map<std::string, int64_t> bias_off, alpha_off;
     std::set<std::string> unit_ok;     // k=3 names of units with a fused pack in some arithmetic
     int64_t hkf_off = 0, hki_off = 0, spk_off = 0, cb_off = -1;
+    int64_t head_filt_off = -1, tail_filt_off = -1;   // rave_*_pack_filter images (-1: shape unsupported)
     int taps_a = 0, taps_s = 0;
     // AdaIN buffers (rave/blocks.py:858-868), device
     int max_batch = 64;
@@ -397,7 +400,8 @@ struct Model {
         const std::vector<const Node*>& nodes) const;
     std::map<std::string, std::pair<View, int>> run_stack(Plan& p, const std::vector<const Node*>& nodes, int B,
                                                           const std::map<std::string, std::pair<View, int>>& inputs,
-                                                          const std::map<std::string, View>& outputs);
+                                                          const std::map<std::string, View>& outputs,
+                                                          const std::map<std::string, int64_t>& owned = {});
     void analysis_op(Plan& p, int B, int T, const View& x, const View& y, int n_out, int pad, int t_in);
     void synthesis_op(Plan& p, int B, int F, const View& x, const View& y, const View* noise, int pad, int frame0,
                       int x_len);
@@ -876,9 +880,11 @@ void Model::adain_op(Plan& p, const std::string& name, int B, int C, int T, cons
 
 // Lay a conv sequence into the plan, allocating workspace tensors with
 // liveness-based reuse.  inputs: tensor -> (view, T); outputs: fixed views.
+// owned: inputs that live in the plan's workspace (floats), released after their last use
 std::map<std::string, std::pair<View, int>> Model::run_stack(Plan& p, const std::vector<const Node*>& nodes, int B,
                                                              const std::map<std::string, std::pair<View, int>>& inputs,
-                                                             const std::map<std::string, View>& outputs) {
+                                                             const std::map<std::string, View>& outputs,
+                                                             const std::map<std::string, int64_t>& owned) {
     std::map<std::string, int> last_use;
     for (size_t i = 0; i < nodes.size(); ++i) {
         last_use[nodes[i]->src] = (int)i;
@@ -890,7 +896,10 @@ std::map<std::string, std::pair<View, int>> Model::run_stack(Plan& p, const std:
         int64_t size;   // floats owned in the workspace (-1: not owned)
     };
     std::map<std::string, T_> ts;
-    for (auto& kv : inputs) ts[kv.first] = {kv.second.first, kv.second.second, -1};
+    for (auto& kv : inputs) {
+        auto ow = owned.find(kv.first);
+        ts[kv.first] = {kv.second.first, kv.second.second, ow != owned.end() ? ow->second : -1};
+    }
     std::map<std::string, const Node*> fused;
     if (cfg.fuse_units)
         for (auto& pr : unit_pairs(nodes))
@@ -1118,7 +1127,14 @@ rave_edge_args Model::tail_desc(int B, int F) const {
     return a;
 }
 
+// RAVE_EDGES=0 in the environment keeps both edges unfused (same-box A/B runs)
+static bool edges_enabled() {
+    const char* e = std::getenv("RAVE_EDGES");
+    return !(e && e[0] == '0');
+}
+
 bool Model::use_head(int B, int T) {
+    if (!edges_enabled() || head_filt_off < 0) return false;
     const Node& n = g.encoder.front();
     const int F = T / cfg.n_band;
     if (std::find(precs.begin(), precs.end(), RAVE_PREC_SPLIT16) == precs.end()) return false;
@@ -1137,7 +1153,7 @@ bool Model::use_head(int B, int T) {
         a.y_sc = F;
         a.weight = aptr(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
         a.bias = n.bias ? aptr(bias_off.at(n.name)) : nullptr;
-        a.filter = aptr(hkf_off);
+        a.filter = aptr(head_filt_off);
         const double fused = time_native([&](hipStream_t st) { return rave_encoder_head(&a, st); });
         double split = 1e30;
         if (precs.size() == 1) {
@@ -1193,7 +1209,7 @@ void Model::head_op(Plan& p, int B, int T, const View& x, const View& y, const V
     rave_edge_args& A = *reinterpret_cast<rave_edge_args*>(o.op.u.raw);
     View wv = arena_view(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
     View bv = n.bias ? arena_view(bias_off.at(n.name)) : View{};
-    View hv = arena_view(hkf_off);
+    View hv = arena_view(head_filt_off);
     View sv = arena_view(spk_off);
     p.bind(o, A, A.x, &x);
     p.bind(o, A, A.y, &y);
@@ -1208,6 +1224,7 @@ void Model::head_op(Plan& p, int B, int T, const View& x, const View& y, const V
 }
 
 bool Model::use_tail(int B, int F) {
+    if (!edges_enabled() || tail_filt_off < 0) return false;
     const Node& n = g.decoder.back();
     if (std::find(precs.begin(), precs.end(), RAVE_PREC_SPLIT16) == precs.end()) return false;
     const int c_want = cfg.amplitude_modulation ? 2 * cfg.n_band : cfg.n_band;
@@ -1227,7 +1244,7 @@ bool Model::use_tail(int B, int F) {
         a.weight = aptr(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
         a.bias = n.bias ? aptr(bias_off.at(n.name)) : nullptr;
         a.alpha = n.act == RAVE_ACT_SNAKE ? aptr(alpha_off.at(n.alpha)) : nullptr;
-        a.filter = aptr(hki_off);
+        a.filter = aptr(tail_filt_off);
         const double fused = time_native([&](hipStream_t st) { return rave_decoder_tail(&a, st); });
         double split = 1e30;
         if (precs.size() == 1) {
@@ -1277,7 +1294,7 @@ void Model::tail_op(Plan& p, int B, int F, const View& x, const View& y, const V
     View wv = arena_view(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
     View bv = n.bias ? arena_view(bias_off.at(n.name)) : View{};
     View av = n.act == RAVE_ACT_SNAKE ? arena_view(alpha_off.at(n.alpha)) : View{};
-    View hv = arena_view(hki_off);
+    View hv = arena_view(tail_filt_off);
     p.bind(o, A, A.x, &x);
     p.bind(o, A, A.y, &y);
     p.bind(o, A, A.weight, &wv);
@@ -1363,10 +1380,15 @@ Plan& Model::encode_plan(int B, int T, bool codes) {
     if (use_head(B, T)) {
         // analysis + the first conv (+ the speaker fill) in one launch
         const Node& n0 = *nodes.front();
-        View h0 = ws_view(p.ws.alloc((int64_t)B * n0.c_out * F), (int64_t)n0.c_out * F, F);
+        // workspace laid out as the two-op path lays it (the bands tensor's slot,
+        // then the conv's output, freed after its last use), so every later tensor
+        // lands at the same offset with or without the fusion
+        const int64_t n_bands = (int64_t)B * cfg.enc_bands * F, n_h0 = (int64_t)B * n0.c_out * F;
+        (void)p.ws.alloc(n_bands);
+        View h0 = ws_view(p.ws.alloc(n_h0), (int64_t)n0.c_out * F, F);
         head_op(p, B, T, io_view(0, T, T), h0, codes ? nullptr : &spk_z);
         nodes.erase(nodes.begin());
-        run_stack(p, nodes, B, {{n0.dst, {h0, F}}}, {{"latent", lat}});
+        run_stack(p, nodes, B, {{n0.dst, {h0, F}}}, {{"latent", lat}}, {{n0.dst, n_h0}});
         if (codes) rvq_encode_op(p, B, Fz, lat, io_view(1, 0, 0));
     } else {
         View bands = ws_view(p.ws.alloc((int64_t)B * cfg.enc_bands * F), (int64_t)cfg.enc_bands * F, F);
@@ -1612,6 +1634,12 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
                     hki[((size_t)mm * nb + c) * m->taps_s + t] = hk.first[(size_t)c * L + (L - 1 - (t * nb + mm))];
         m->hkf_off = m->add(hkf);
         m->hki_off = m->add(hki);
+        // the fused edges' pre-split filter images (split16 models; shapes the kernels build)
+        std::vector<float> img(RAVE_EDGE_FILTER_FLOATS, 0.f);
+        if (rave_encoder_head_pack_filter(hkf.data(), nb, m->taps_a, cfg.enc_bands, img.data()) == RAVE_OK)
+            m->head_filt_off = m->add(img);
+        if (rave_decoder_tail_pack_filter(hki.data(), nb, m->taps_s, img.data()) == RAVE_OK)
+            m->tail_filt_off = m->add(img);
     }
     m->spk_off = cfg.speaker_size > 0 ? m->add(speaker, cfg.speaker_size) : 0;
     if (cfg.rvq_quantizers > 0) {

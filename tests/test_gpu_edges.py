@@ -68,7 +68,8 @@ def test_encoder_head(N, dev, golden, causal, F, B, scale):
     spk = torch.from_numpy(rng.standard_normal(256).astype(np.float32)).to(dev)
     Fz = max(1, F // 64)
     z = torch.full((B, 320, Fz), float("nan"), device=dev)
-    hd, bd = torch.from_numpy(hkf).to(dev), torch.from_numpy(b).to(dev)
+    hd = torch.from_numpy(N.pack_edge_filter(hkf, head=True, n_out_bands=nb)).to(dev)
+    bd = torch.from_numpy(b).to(dev)
     a = N.EdgeArgs(batch=B, frames=F, conv_c_in=nb, conv_c_out=co, conv_kernel=k, conv_pad_left=cpad[0],
                    pqmf_taps=hkf.shape[-1], pqmf_pad_left=get_padding(hkf.shape[-1], causal=causal)[0],
                    x=xd.data_ptr(), x_sb=T, y=y.data_ptr(), y_sb=co * F, y_sc=F,
@@ -113,7 +114,8 @@ def test_decoder_tail(N, dev, golden, causal, am, act, noise, F, B):
     packed = torch.from_numpy(N.pack_conv_weight(w, ci, co, k, 1, 1, 0, precision=N.PREC_SPLIT16)).to(dev)
     xd = torch.from_numpy(x).to(dev)
     y = torch.full((B, 1, 16 * F), float("nan"), device=dev)
-    bd, ad, hd = (torch.from_numpy(v).to(dev) for v in (b, alpha, hki))
+    bd, ad = (torch.from_numpy(v).to(dev) for v in (b, alpha))
+    hd = torch.from_numpy(N.pack_edge_filter(hki, head=False)).to(dev)
     nd = torch.from_numpy(nz).to(dev) if noise else None
     a = N.EdgeArgs(batch=B, frames=F, conv_c_in=ci, conv_c_out=co, conv_kernel=k, conv_pad_left=cpad[0],
                    pqmf_taps=hki.shape[-1], pqmf_pad_left=spad[0], mode=1 if am else 2, act=N.ACT[act],
