@@ -35,7 +35,7 @@ timeout -k 10 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --ker
 echo "mfma pass done"
 MF=$(find "$OUT/mfma" -name '*counter_collection.csv' | head -n 1)
 python3 "$R/tools/mfma_util.py" "$MF" "$OUT/bench.json" > "$OUT/mfma_util.json"
-head -n 1 "$MF" > "$MF.gemm"; grep -E 'conv1d|split_reduce|unit_kernel|unit_split|stack_split|pqmf' "$MF" >> "$MF.gemm" || true
+head -n 1 "$MF" > "$MF.gemm"; grep -E 'conv1d|split_reduce|unit_kernel|unit_split|stack_split|pqmf|encoder_head|decoder_tail' "$MF" >> "$MF.gemm" || true
 rm -f "$MF"
 KT=$(find "$OUT/kt" -name '*kernel_trace.csv' | head -n 1)
 FE=$(find "$OUT/fetch" -name '*counter_collection.csv' | head -n 1)
@@ -43,10 +43,22 @@ WR=$(find "$OUT/write" -name '*counter_collection.csv' | head -n 1)
 python3 "$R/tools/rocprof_summary.py" --trace "$KT" --fetch "$FE" --write "$WR" \
     --bench "$OUT/bench.json" --out "$OUT/summary.json" --traffic-out "$OUT/traffic.json" \
     --precision auto
-find "$OUT" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
+find "$OUT/kt" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
+# the exact-fp32 mode's own kernel trace (f32_tuned headline run), so the fp32
+# line's fractions are reproducible from rocprof too
+timeout -k 10 300 python3 $R/bench.py --steps 10 --warmup 3 --precision f32_tuned --no-cpu-baseline --pipeline 1 \
+    --tuning-out "$OUT/tuning_f32.json" > "$OUT/bench_f32.json" 2> "$OUT/bench_f32.err"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_f32" -o run -- \
+    python3 $R/bench.py --steps 10 --warmup 3 --precision f32_tuned --no-cpu-baseline --pipeline 1 \
+    --tuning-in "$OUT/tuning_f32.json" > "$OUT/bench_f32_kt.json" 2> "$OUT/bench_f32_kt.err"
+KT32=$(find "$OUT/kt_f32" -name '*kernel_trace.csv' | head -n 1)
+python3 "$R/tools/rocprof_summary.py" --trace "$KT32" --bench "$OUT/bench_f32.json" --out "$OUT/summary_f32.json" \
+    --precision f32_tuned > /dev/null
+find "$OUT/kt_f32" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats_f32.csv" \;
+echo "f32 kernel-trace pass done"
 # counter CSVs are large; keep the GEMM-family rows only
 for f in "$FE" "$WR"; do
-    head -n 1 "$f" > "$f.gemm"; grep -E 'conv1d|split_reduce|unit_kernel|unit_split|stack_split|pqmf' "$f" >> "$f.gemm" || true
+    head -n 1 "$f" > "$f.gemm"; grep -E 'conv1d|split_reduce|unit_kernel|unit_split|stack_split|pqmf|encoder_head|decoder_tail' "$f" >> "$f.gemm" || true
     rm -f "$f"
 done
 ls -la "$OUT"
