@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 12
+#define RAVE_ABI_VERSION 13
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 
@@ -317,6 +317,8 @@ typedef struct rave_unit_args {
     const float* weight;
     const float* bias1; const float* bias2;
     const float* alpha0; const float* alpha2;
+    float* workspace;   /* optional, rave_unit_workspace() floats, zeroed once before its first
+                           use (every launch leaves its counters zero); NULL: one workgroup per slab */
 } rave_unit_args;
 int64_t rave_unit_packed_size(int channels);
 int rave_unit_pack_weight(const float* w1, const float* w2, int channels, float* packed);
@@ -326,6 +328,17 @@ int rave_unit_pack_weight(const float* w1, const float* w2, int channels, float*
  * split16 rave_conv1d calls). */
 int64_t rave_unit_split_packed_size(int channels);
 int rave_unit_split_pack_weight(const float* w1, const float* w2, int channels, float* packed);
+/* RAVE_PREC_F32_RING unit weights (exact fp32 on the split kernel's machinery):
+ * the split image's layout with 8 fp32 values per lane and K-step, row scales 1
+ * (sizes as rave_unit_split_packed_size). */
+int rave_unit_ring_pack_weight(const float* w1, const float* w2, int channels, float* packed);
+/* Workspace (floats) of the cooperative fused unit (C in {256, 512}, RAVE_PREC_SPLIT16 /
+ * RAVE_PREC_F32_RING): groups of C/128 workgroups share a 32-column slab, each owning
+ * C/(C/128) output rows of both GEMMs, and hand the intermediate act2(h) rows to each
+ * other inside the launch.  0: this shape runs one workgroup per slab.  The first
+ * RAVE_SPLITK_TICKETS words are counters, like rave_conv1d_workspace's: one buffer
+ * serves both when ops run in stream order. */
+int64_t rave_unit_workspace(const rave_unit_args* a);
 int rave_residual_unit(const rave_unit_args* a, void* stream);
 
 /* ---------------------------------------------------------------- residual stack

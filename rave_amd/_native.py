@@ -41,7 +41,7 @@ OP_UNIT = 11
 OP_STACK = 12
 OP_HEAD = 13
 OP_TAIL = 14
-ABI_VERSION = 12
+ABI_VERSION = 13
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 
 # GEMM arithmetic of conv / unit ops (include/rave_amd.h RAVE_PREC_*)
@@ -134,7 +134,8 @@ class UnitArgs(C.Structure):
                 ("pad_left", i32), ("act", i32), ("leaky_slope", f32), ("precision", i32),
                 ("x", vp), ("x_sb", i64), ("x_sc", i64),
                 ("y", vp), ("y_sb", i64), ("y_sc", i64),
-                ("weight", vp), ("bias1", vp), ("bias2", vp), ("alpha0", vp), ("alpha2", vp)]
+                ("weight", vp), ("bias1", vp), ("bias2", vp), ("alpha0", vp), ("alpha2", vp),
+                ("workspace", vp)]
 
 
 STACK_UNITS = 3
@@ -239,7 +240,8 @@ EXPORTS = [
     "rave_pqmf_analysis", "rave_pqmf_synthesis", "rave_fill_channels", "rave_copy",
     "rave_rvq_workspace", "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
     "rave_unit_packed_size", "rave_unit_pack_weight", "rave_residual_unit",
-    "rave_unit_split_packed_size", "rave_unit_split_pack_weight",
+    "rave_unit_split_packed_size", "rave_unit_split_pack_weight", "rave_unit_ring_pack_weight",
+    "rave_unit_workspace",
     "rave_stack_supported", "rave_residual_stack",
     "rave_plan_create", "rave_plan_run", "rave_plan_destroy", "rave_plan_size",
     "rave_plan_profile", "rave_plan_op_times", "rave_fill_uniform",
@@ -286,10 +288,13 @@ def _load():
     lib.rave_unit_packed_size.argtypes = [C.c_int]
     lib.rave_unit_packed_size.restype = i64
     lib.rave_unit_pack_weight.argtypes = [vp, vp, C.c_int, vp]
+    lib.rave_unit_workspace.argtypes = [C.c_void_p]
+    lib.rave_unit_workspace.restype = i64
     lib.rave_unit_split_packed_size.argtypes = [C.c_int]
     lib.rave_stack_supported.argtypes = [C.c_int]
     lib.rave_unit_split_packed_size.restype = i64
     lib.rave_unit_split_pack_weight.argtypes = [vp, vp, C.c_int, vp]
+    lib.rave_unit_ring_pack_weight.argtypes = [vp, vp, C.c_int, vp]
     lib.rave_conv1d_workspace.restype = i64
     lib.rave_rvq_workspace.argtypes = [C.POINTER(RvqArgs)]
     lib.rave_rvq_workspace.restype = i64
@@ -472,6 +477,8 @@ def pack_unit_weight(w1, w2, channels, precision=PREC_F32):
     (PREC_SPLIT16: f16 fragment image + row scales, in 4-byte units)."""
     import numpy as np
     size_fn, pack_fn = ((lib.rave_unit_packed_size, lib.rave_unit_pack_weight) if precision == PREC_F32
+                        else (lib.rave_unit_split_packed_size, lib.rave_unit_ring_pack_weight)
+                        if precision == PREC_F32_RING
                         else (lib.rave_unit_split_packed_size, lib.rave_unit_split_pack_weight))
     n = int(size_fn(int(channels)))
     if n <= 0:

@@ -1081,8 +1081,13 @@ static int split_launch_family(ConvKArgs k, const SplitCfg& c, bool f32, hipStre
     const unsigned rl = (unsigned)(k.XW * SFam<KT>::S);
     k.rl_magic = (unsigned)((0x100000000ull + rl - 1) / rl);
     const bool snake = k.act == RAVE_ACT_SNAKE;
-    auto fn = f32 ? (snake ? (k.x_vec ? split_launch_inst<KT, true, true, true> : split_launch_inst<KT, true, false, true>)
-                           : (k.x_vec ? split_launch_inst<KT, false, true, true> : split_launch_inst<KT, false, false, true>))
+    if (f32 && !k.x_vec) {
+        // the fp32 ring kernels are built for 16-byte window DMA only (the
+        // register-staged RAVE_PREC_F32 kernel covers unaligned inputs)
+        set_error("conv1d(f32_ring): needs 16-byte aligned input rows and t_in % 4 == 0");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    auto fn = f32 ? (snake ? split_launch_inst<KT, true, true, true> : split_launch_inst<KT, false, true, true>)
                   : (snake ? (k.x_vec ? split_launch_inst<KT, true, true, false> : split_launch_inst<KT, true, false, false>)
                            : (k.x_vec ? split_launch_inst<KT, false, true, false> : split_launch_inst<KT, false, false, false>));
     return fn(k, c.tile, st);

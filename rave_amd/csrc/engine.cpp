@@ -386,6 +386,7 @@ struct Model {
     void conv_op(Plan& p, const Node& n, int B, int t_in, const View& src, const View& dst, const View* res);
     double unit_time(const Node& k3, const Node& k1, int B, int T);
     int unit_pick(const Node& k3, int B, int T, bool timed);
+    bool unit_coop(const Node& k3, int B, int T);
     bool fuse_unit(const Node& k3, const Node& k1, int B, int T);
     double unit_best_ms(const Node& k3, const Node& k1, int B, int T);
     rave_unit_args unit_desc(const Node& k3, const Node& k1, int B, int T, int prec) const;
@@ -659,14 +660,28 @@ int Model::unit_pick(const Node& k3, int B, int T, bool timed) {
     for (int pr : precs)
         if (unit_pack.count({k3.name, pr})) cands.push_back(pr);
     if (cands.empty()) fail(RAVE_ERR_STATE, "unit " + k3.name + ": no fused pack");
-    if (cands.size() == 1 && !timed) return cands[0];
+    if (cands.size() == 1 && !timed) {
+        rave_unit_args q{};
+        q.channels = k3.c_in;
+        q.batch = B;
+        q.t_len = T;
+        q.precision = cands[0];
+        if (rave_unit_workspace(&q) <= 0) return cands[0];   // one form: nothing to time
+    }
     const std::string key = key_of({"unit", k3.name, std::to_string(B), std::to_string(T)});
     if (!tuned.count(key)) {
         const Node* k1 = nullptr;
         for (const Node* n : g.convs())
             if (n->src == k3.dst && n->kernel == 1) k1 = n;
         const int64_t n_el = (int64_t)B * k3.c_in * T;
-        float* sc = scratch_buf(2 * n_el + 128);
+        int64_t nws = 0;
+        for (int pr : cands) {
+            rave_unit_args q = unit_desc(k3, *k1, B, T, pr);
+            nws = std::max(nws, rave_unit_workspace(&q));
+        }
+        float* sc = scratch_buf(2 * n_el + 128 + nws);
+        float* ws = nws > 0 ? sc + 2 * n_el + 128 : nullptr;   // (64-float aligned)
+        if (ws) RAVE_HIP_OR_THROW(hipMemset(ws, 0, (size_t)RAVE_SPLITK_TICKETS * 4));   // counters at rest
         double best = 1e30;
         int bp = cands[0];
         for (int pr : cands) {
@@ -675,15 +690,26 @@ int Model::unit_pick(const Node& k3, int B, int T, bool timed) {
             u.y = sc + n_el + 64;
             u.x_sb = u.y_sb = (int64_t)k3.c_in * T;
             u.x_sc = u.y_sc = T;
-            const double ms = time_native([&](hipStream_t st) { return rave_residual_unit(&u, st); });
-            if (ms >= 0 && ms < best) {
-                best = ms;
-                bp = pr;
+            // both forms where the cooperative one exists (one workgroup per slab /
+            // groups of workgroups sharing a slab): value = precision | coop << 8
+            for (int coop = 0; coop <= (rave_unit_workspace(&u) > 0 ? 1 : 0); ++coop) {
+                u.workspace = coop ? ws : nullptr;
+                const double ms = time_native([&](hipStream_t st) { return rave_residual_unit(&u, st); });
+                if (ms >= 0 && ms < best) {
+                    best = ms;
+                    bp = pr | (coop << 8);
+                }
             }
         }
         tuned[key] = {bp, best};
     }
-    return (int)tuned.at(key).first;
+    return (int)tuned.at(key).first & 255;
+}
+
+bool Model::unit_coop(const Node& k3, int B, int T) {
+    const std::string key = key_of({"unit", k3.name, std::to_string(B), std::to_string(T)});
+    auto it = tuned.find(key);
+    return it != tuned.end() && ((int)it->second.first >> 8) != 0;
 }
 
 // Residual(DilatedUnit) as the fused kernel (true) or as its two convs (false):
@@ -723,6 +749,9 @@ void Model::unit_op(Plan& p, const Node& k3, const Node& k1, int B, int T, const
     u.y_sb = dst.sb;
     u.y_sc = dst.sc;
     const std::string label = k3.name.substr(0, k3.name.rfind(".net.")) + ".unit";
+    // cooperative form (when timed faster): the plan's split-K buffer
+    const int64_t nws = unit_coop(k3, B, T) ? rave_unit_workspace(&u) : 0;
+    if (nws < 0) fail(RAVE_ERR_ARG, "unit " + k3.name + ": workspace query failed: " + rave_last_error());
     PlanOp& o = p.add(RAVE_OP_UNIT, u, label);
     rave_unit_args& U = *reinterpret_cast<rave_unit_args*>(o.op.u.raw);
     View wv = arena_view(unit_pack.at({k3.name, pr}));
@@ -737,6 +766,8 @@ void Model::unit_op(Plan& p, const Node& k3, const Node& k1, int B, int T, const
     p.bind(o, U, U.bias2, k1.bias ? &b2 : nullptr);
     p.bind(o, U, U.alpha0, k3.act == RAVE_ACT_SNAKE ? &a0 : nullptr);
     p.bind(o, U, U.alpha2, k1.act == RAVE_ACT_SNAKE ? &a2 : nullptr);
+    View sk = p.splitk(nws);
+    p.bind(o, U, U.workspace, nws > 0 ? &sk : nullptr);
     o.prec = pr;
     const double C_ = k3.c_in;
     o.flops = 2.0 * B * T * C_ * C_ * 4;
@@ -1600,13 +1631,14 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
             std::vector<float> w1 = fold_wn(get(k3.name + ".weight_g"), get(k3.name + ".weight_v"), C_, (int64_t)C_ * 3);
             std::vector<float> w2 = fold_wn(get(k1.name + ".weight_g"), get(k1.name + ".weight_v"), C_, C_);
             for (int p : m->precs) {
-                if (p == RAVE_PREC_F32_RING) continue;   // fused units: the fp32 and split16 kernels
-                const bool sp = p == RAVE_PREC_SPLIT16;
+                // split16 and the fp32 ring kernel share the fragment image layout
+                const bool sp = p == RAVE_PREC_SPLIT16 || p == RAVE_PREC_F32_RING;
                 const int64_t sz = sp ? rave_unit_split_packed_size(C_) : rave_unit_packed_size(C_);
                 if (sz <= 0) continue;
                 std::vector<float> packed((size_t)sz, 0.f);
-                check_rc(sp ? rave_unit_split_pack_weight(w1.data(), w2.data(), C_, packed.data())
-                            : rave_unit_pack_weight(w1.data(), w2.data(), C_, packed.data()),
+                check_rc(p == RAVE_PREC_SPLIT16 ? rave_unit_split_pack_weight(w1.data(), w2.data(), C_, packed.data())
+                         : p == RAVE_PREC_F32_RING ? rave_unit_ring_pack_weight(w1.data(), w2.data(), C_, packed.data())
+                                                   : rave_unit_pack_weight(w1.data(), w2.data(), C_, packed.data()),
                          "unit pack " + k3.name);
                 m->unit_pack[{k3.name, p}] = m->add(packed);
                 m->unit_ok.insert(k3.name);

@@ -112,15 +112,24 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
     const auto xrs = ss_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);
 
     // ------------------------------------------------------------ per-unit row tables -> LDS
+    // (every load in flight at once: a rolled loop waits out one round trip per pass)
+    {
+        constexpr int NTB = (kSSUnits * 6 * C + NT - 1) / NT;
+        float tv[NTB];
 #pragma unroll
-    for (int u = 0; u < kSSUnits; ++u) {
-        for (int i = tid; i < 6 * C; i += NT) {
-            const int k = i / C, m = i - k * C;
-            const float* src = k == 0 ? a.rs1[u] : k == 1 ? a.b1[u] : k == 2 ? a.a2[u]
-                             : k == 3 ? a.rs2[u] : k == 4 ? a.b2[u] : a.a0[u];
-            const bool has = (k == 1 || k == 4) ? a.has_bias != 0 : (k == 2 || k == 5) ? SNAKE : true;
-            tab[u * 6 * C + i] = has ? src[m] : 0.f;
+        for (int r = 0; r < NTB; ++r) {
+            const int i = tid + r * NT;
+            const int u = i / (6 * C), iu = i - u * 6 * C;
+            const int k = iu / C, m = iu - k * C;
+            const int uu = min(u, kSSUnits - 1);
+            const float* src = k == 0 ? a.rs1[uu] : k == 1 ? a.b1[uu] : k == 2 ? a.a2[uu]
+                             : k == 3 ? a.rs2[uu] : k == 4 ? a.b2[uu] : a.a0[uu];
+            const bool has = u < kSSUnits && ((k == 1 || k == 4) ? a.has_bias != 0 : (k == 2 || k == 5) ? SNAKE : true);
+            tv[r] = has ? src[m] : 0.f;
         }
+#pragma unroll
+        for (int r = 0; r < NTB; ++r)
+            if (tid + r * NT < kSSUnits * 6 * C) tab[tid + r * NT] = tv[r];
     }
 
     // ------------------------------------------------------------ weight ring (crosses units)

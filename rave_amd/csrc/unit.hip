@@ -356,7 +356,7 @@ int residual_unit_split(const rave_unit_args& a, void* stream);   // unit_split.
 extern "C" int rave_residual_unit(const rave_unit_args* p, void* stream) {
     RAVE_CHECK_ARG(p && p->x && p->y && p->weight, "residual_unit: null pointer");
     const rave_unit_args& a = *p;
-    RAVE_CHECK_ARG(a.precision == RAVE_PREC_F32 || a.precision == RAVE_PREC_SPLIT16,
+    RAVE_CHECK_ARG(a.precision == RAVE_PREC_F32 || a.precision == RAVE_PREC_SPLIT16 || a.precision == RAVE_PREC_F32_RING,
                    "residual_unit: unknown precision");
     if (!unit_supported(a.channels)) {
         set_error("residual_unit: fused residual unit supports C in {64, 128, 256, 512}");
@@ -370,7 +370,7 @@ extern "C" int rave_residual_unit(const rave_unit_args* p, void* stream) {
                    "residual_unit: bad activation");
     RAVE_CHECK_ARG(a.act != RAVE_ACT_SNAKE || (a.alpha0 && a.alpha2), "residual_unit: snake needs alphas");
     RAVE_CHECK_ARG(a.x != a.y, "residual_unit: y must not alias x (other slabs still read it)");
-    if (a.precision == RAVE_PREC_SPLIT16) return residual_unit_split(a, stream);
+    if (a.precision == RAVE_PREC_SPLIT16 || a.precision == RAVE_PREC_F32_RING) return residual_unit_split(a, stream);
     const int C = a.channels;
     UnitKArgs k{};
     k.x = a.x; k.y = a.y; k.w = a.weight;

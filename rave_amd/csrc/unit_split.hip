@@ -19,10 +19,25 @@
 //   phase 2   y = W2 (C x C) . h, ring running on from W1 into W2
 //   epilogue  y * rs2 + b2 + x (residual re-read, L2-hot) -> HBM
 // Each wave owns 32 rows x 64 columns (1 x 2 blocks of 32x32).
+//
+// Cooperative form (RB > 1, C in {256, 512}; needs the rave_unit_workspace
+// buffer): a GROUP of RB workgroups shares one column slab, workgroup rb owning
+// output rows [rb C/RB, (rb+1) C/RB) of BOTH GEMMs, so a slab's weights stream
+// through RB CUs instead of one (1 MB per CU at C = 512 instead of 4 MB).  Phase 2
+// needs every row of h: at the seam each member publishes its act2(h) rows
+// write-through (sc1 stores, drained, then an agent-scope counter add), waits for
+// the group's other members (ONE wave polls, bounded, one agent acquire), and
+// stages their rows into its planes.  Members are dealt so that a group's RB
+// blocks are consecutive in one XCD's dispatch order (blocks b, b + 8, ...): a
+// group is resident together whenever its first member is, and every other
+// resident group completes without waiting on a non-resident one.  The range
+// guard of h is group-wide (members publish their max |h|).  The arithmetic and
+// the K order are those of the one-workgroup form: the results are identical.
 #include "common.h"
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -33,8 +48,16 @@ typedef _Float16 us_h4 __attribute__((ext_vector_type(4)));
 typedef float us_f32x8 __attribute__((ext_vector_type(8)));
 typedef float us_f32x4 __attribute__((ext_vector_type(4)));
 typedef float us_f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned us_u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kUSMaxDil = 16;
+#ifndef RAVE_US_R
+#define RAVE_US_R 3
+#endif
+#ifndef RAVE_US_RC
+#define RAVE_US_RC 6                // weight ring depth of the cooperative form (4 waves per CU)
+#endif
+constexpr unsigned kUSSpinLimit = 1u << 18;   // cooperative seam: bounded poll (give-up -> NaN outputs)
 template <int V> struct IC {
     static constexpr int value = V;
 };
@@ -65,6 +88,13 @@ struct USArgs {
     int act;
     float slope;
     unsigned xw_magic;
+    // cooperative form: per group {arrivals, departures} counters (zero at rest),
+    // the give-up word, members' max |h|, the act2(h) exchange [group][BN][C]
+    unsigned* flags; unsigned* tmo; float* xmax; float* xch;
+    int ngroups, xch_bytes;
+    int xv;                  // 16-byte window loads (T % 4 == 0, 16-byte aligned rows)
+    unsigned nb_magic;       // ceil(2^24 / window blocks per row)
+    int flag_stride;         // counter words per group (cooperative form)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t us_rsrc(const void* p, int bytes) {
@@ -88,8 +118,8 @@ __device__ __forceinline__ float us_act(float v, float slope, float alpha) {
 
 // C channels; WGN waves along time (each 64 columns); C/(32 MI) waves along
 // rows (each MI 32-row blocks).
-template <int C, int WGN, int MI, int KG = 1, int CB = 2> struct USGeo {
-    static constexpr int WGM = C / (32 * MI), NWT = WGM * WGN, NW = NWT * KG, NT = 64 * NW;
+template <int C, int WGN, int MI, int KG = 1, int CB = 2, int RB = 1> struct USGeo {
+    static constexpr int WGM = C / (32 * MI * RB), NWT = WGM * WGN, NW = NWT * KG, NT = 64 * NW;
     static constexpr int BN = 32 * CB * WGN;           // CB 32-column blocks per wave
     static constexpr int S1 = 3 * C / 16, S2 = C / 16, ST = S1 + S2;   // K-steps
     static constexpr int PH = C + 8;                  // halves per LDS row (conflict-free b128)
@@ -102,21 +132,29 @@ template <int C, int WGN, int MI, int KG = 1, int CB = 2> struct USGeo {
     static constexpr int LDS = VRED + 64;
     static constexpr int G8 = C / 8;                  // 8-channel groups per window row
     static constexpr int XT = (XW_MAX * G8 + NT - 1) / NT;
-    static constexpr int R = 3;                       // weight ring depth (K-steps)
+    static constexpr int R = RB > 1 ? RAVE_US_RC : RAVE_US_R;   // weight ring depth (K-steps)
+    static constexpr int G8R = C / (8 * RB);          // 8-channel groups of one member's rows
     // K-groups: two waves per output tile take alternate K-steps (both phases)
     static constexpr int RED = NWT * MI * CB * 16 * 64 * 4;  // partial-sum hand-off (bytes)
     static_assert(C % 64 == 0 && (MI == 1 || MI == 2) && NW <= 16, "geometry");
+    static_assert(RB == 1 || (KG == 1 && WGN == 1 && C % (32 * MI * RB) == 0), "cooperative geometry");
     static_assert(KG == 1 || (KG == 2 && S1 % 2 == 0 && S2 % 2 == 0 && RED <= PLANES), "K-groups");
 };
 
-template <int C, int WGN, int MI, int KG, int CB, bool SNAKE>
-__global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_kernel(USArgs a) {
-    using G = USGeo<C, WGN, MI, KG, CB>;
+// F32 (RAVE_PREC_F32_RING): the same kernel in exact fp32 -- one fp32 plane in
+// the bytes of the (hi, lo) pair (row pitch PH floats), weight fragments of 8
+// floats per lane in the split image's slots (rave_unit_ring_pack_weight),
+// eight v_mfma_f32_32x32x2_f32 per 16-deep K-step (K-slot (s, half h) =
+// channel 8h + s), no range guard, row scales 1.
+template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, bool F32, int RB>
+__device__ __forceinline__ void unit_split_body(const USArgs& a) {
+    using G = USGeo<C, WGN, MI, KG, CB, RB>;
     constexpr int NT = G::NT, PH = G::PH, G8 = G::G8, XT = G::XT, R = G::R;
     constexpr int S1 = G::S1, ST = G::ST, CG = C / 16;
     extern __shared__ __attribute__((aligned(16))) char lds[];
     _Float16* ph = reinterpret_cast<_Float16*>(lds);
     _Float16* pl = reinterpret_cast<_Float16*>(lds + G::PLANES / 2);
+    float* pf = reinterpret_cast<float*>(lds);                 // F32: the fp32 plane
     float* tab = reinterpret_cast<float*>(lds + G::TAB);      // [6][C]
     unsigned char* vote = reinterpret_cast<unsigned char*>(lds + G::VOTE);
     float* vred = reinterpret_cast<float*>(lds + G::VRED);
@@ -129,7 +167,17 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     const int twave = wave - kg * G::NWT;
     const int wm = twave % G::WGM, wn = twave / G::WGM;
     const int hh = lane >> 5, l32 = lane & 31;
-    const int lg = __builtin_amdgcn_readfirstlane(xcd_major(blockIdx.x, gridDim.x));
+    int lg, rb = 0;
+    if constexpr (RB == 1) {
+        lg = __builtin_amdgcn_readfirstlane(xcd_major(blockIdx.x, gridDim.x));
+    } else {
+        // block b -> XCD slot b & 7; along that XCD's blocks (b >> 3) the members
+        // of one group are consecutive; groups XCD-major (gridDim = 8k RB)
+        const int q = blockIdx.x >> 3;
+        rb = q % RB;
+        lg = (blockIdx.x & 7) * (int)(gridDim.x / (8 * RB)) + q / RB;
+        if (lg >= a.ngroups) return;             // padding group (all its members leave)
+    }
     const int b = lg / a.ntiles;
     const int n0 = (lg - b * a.ntiles) * G::BN;
     const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
@@ -145,7 +193,8 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     // this wave's m-blocks MI*wm .. MI*wm+MI-1; fragment (mb, s, plane) at ((mb*ST + s)*2 + plane) KB
     // (ring slot = this wave's local step t % R; s = the global K-step, t*KG + kg)
     us_h8 ring[R][MI][2];
-    const unsigned abase = (unsigned)((MI * wm) * ST * 2) * 1024u + (unsigned)lane * 16u;
+    const int wmg = wm + rb * G::WGM;                // this wave's row-block index in the unit
+    const unsigned abase = (unsigned)((MI * wmg) * ST * 2) * 1024u + (unsigned)lane * 16u;
     auto load_a = [&](int slot, int s) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
@@ -158,12 +207,23 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     for (int t = 0; t < R; ++t) load_a(t, t * KG + kg);
 
     // ------------------------------------------------------------ per-row table -> LDS
-    for (int i = tid; i < 6 * C; i += NT) {
+    // every load in flight at once (a rolled loop waits out one round trip per
+    // pass); issued here, stored after the window loads are issued
+    constexpr int NTAB = (6 * C + NT - 1) / NT;
+    float tabv[NTAB];
+#pragma unroll
+    for (int r = 0; r < NTAB; ++r) {
+        const int i = tid + r * NT;
         const int k = i / C, m = i - k * C;
         const float* src = k == 0 ? a.rs1 : k == 1 ? a.b1 : k == 2 ? a.a2 : k == 3 ? a.rs2 : k == 4 ? a.b2 : a.a0;
-        const bool has = (k == 1 || k == 4) ? a.bias_bytes > 0 : (k == 2 || k == 5) ? SNAKE : true;
-        tab[i] = has ? src[m] : 0.f;
+        const bool has = i < 6 * C && ((k == 1 || k == 4) ? a.bias_bytes > 0 : (k == 2 || k == 5) ? SNAKE : true);
+        tabv[r] = has ? src[m] : 0.f;
     }
+    auto store_tab = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < NTAB; ++r)
+            if (tid + r * NT < 6 * C) tab[tid + r * NT] = tabv[r];
+    };
 
     // ------------------------------------------------------------ prologue: act0(x) window
     // (xs: the range guard's power-of-two scale; returns max |act0(x) xs| of the
@@ -196,12 +256,76 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
                 const float al = SNAKE ? a.a0[min(g * 8 + v, C - 1)] : 0.f;   // L1-hot
                 v8[v] = ok ? us_act<SNAKE>(rx[i][v], slope, al) * xs : 0.f;
             }
-            cmax = fmaxf(cmax, absmax8(v8));
-            const us_h8 hi = __builtin_convertvector(v8, us_h8);
-            const us_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, us_f32x8)) * 2048.0f, us_h8);
-            if (e < ntask) {
-                *reinterpret_cast<us_h8*>(ph + w * PH + g * 8) = hi;
-                *reinterpret_cast<us_h8*>(pl + w * PH + g * 8) = lo;
+            if constexpr (F32) {
+                if (e < ntask) {
+                    *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8) = us_f32x4{v8[0], v8[1], v8[2], v8[3]};
+                    *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8 + 4) = us_f32x4{v8[4], v8[5], v8[6], v8[7]};
+                }
+            } else {
+                cmax = fmaxf(cmax, absmax8(v8));
+                const us_h8 hi = __builtin_convertvector(v8, us_h8);
+                const us_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, us_f32x8)) * 2048.0f, us_h8);
+                if (e < ntask) {
+                    *reinterpret_cast<us_h8*>(ph + w * PH + g * 8) = hi;
+                    *reinterpret_cast<us_h8*>(pl + w * PH + g * 8) = lo;
+                }
+            }
+        }
+        return cmax;
+    };
+    // 16-byte form (rows of whole 4-sample pieces, a.xv): task (8-channel group g,
+    // 4-sample block k), k fastest along the lanes (coalesced rows); 8 b128
+    // loads per task, every load of the window in flight at once, then four
+    // transposed 8-channel plane rows per task.  Blocks are wholly inside or
+    // wholly outside [0, T) (T % 4 == 0, 4-aligned block starts).
+    auto stage_window_v = [&]() __attribute__((always_inline)) {
+        constexpr int NBM = (G::XW_MAX + 3) / 4 + 1, XTV = (G8 * NBM + NT - 1) / NT;
+        const int ta = t0 & ~3;
+        const int nb = (t0 + XW - ta + 3) >> 2;
+        const int ntv = G8 * nb;
+        float cmax = 0.f;
+        us_f32x4 rx[XTV][8];
+#pragma unroll
+        for (int i = 0; i < XTV; ++i) {
+            const int e = tid + i * NT;
+            const int g = (int)(((unsigned)e * a.nb_magic) >> 24);
+            const int kb = e - g * nb;
+            const int t = ta + 4 * kb;
+            const bool ok = (e < ntv) && t >= 0 && t < a.T;
+#pragma unroll
+            for (int v = 0; v < 8; ++v)
+                rx[i][v] = __builtin_bit_cast(us_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                    xrs, ok ? (unsigned)((g * 8 + v) * a.x_sc + t) * 4u : kUSOOB, 0, 0));
+        }
+        store_tab();
+        __syncthreads();                             // the per-row table (Snake alphas) is in LDS
+#pragma unroll
+        for (int i = 0; i < XTV; ++i) {
+            const int e = tid + i * NT;
+            const int g = (int)(((unsigned)e * a.nb_magic) >> 24);
+            const int kb = e - g * nb;
+            if (e < ntv) {
+                float al[8];
+#pragma unroll
+                for (int v = 0; v < 8; ++v) al[v] = SNAKE ? tab[5 * C + g * 8 + v] : 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int w = ta + 4 * kb + q - t0;
+                    us_f32x8 v8;
+#pragma unroll
+                    for (int v = 0; v < 8; ++v) v8[v] = us_act<SNAKE>(rx[i][v][q], slope, al[v]);
+                    if (w < 0 || w >= XW) continue;
+                    if constexpr (F32) {
+                        *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8) = us_f32x4{v8[0], v8[1], v8[2], v8[3]};
+                        *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8 + 4) = us_f32x4{v8[4], v8[5], v8[6], v8[7]};
+                    } else {
+                        cmax = fmaxf(cmax, absmax8(v8));
+                        const us_h8 hi = __builtin_convertvector(v8, us_h8);
+                        const us_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, us_f32x8)) * 2048.0f, us_h8);
+                        *reinterpret_cast<us_h8*>(ph + w * PH + g * 8) = hi;
+                        *reinterpret_cast<us_h8*>(pl + w * PH + g * 8) = lo;
+                    }
+                }
             }
         }
         return cmax;
@@ -209,10 +333,16 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     // range guard: when a wave saw |act0(x)| >= 2^15 the window is staged again
     // as act0(x) * 2^-sh0 by a rolled loop (small code, few registers: rare)
     {
-        const float cmax = stage_window(1.0f);
-        vote_cast(vote, wave, cmax);
+        float cmax;
+        if (a.xv) {
+            cmax = stage_window_v();
+        } else {
+            store_tab();
+            cmax = stage_window(1.0f);
+        }
+        if constexpr (!F32) vote_cast(vote, wave, cmax);
         __syncthreads();
-        if (__builtin_expect(vote_any<G::NW>(vote), 0)) {
+        if (!F32 && __builtin_expect(vote_any<G::NW>(vote), 0)) {
             sh0 = __builtin_amdgcn_readfirstlane(split_shift(block_max<G::NW>(cmax, vred)));
             const float xs = ldexpf(1.0f, -sh0);
 #pragma nounroll
@@ -240,13 +370,27 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     US_STAMP(1);
 
     // ------------------------------------------------------------ K loop (both phases)
-    us_f32x16 acc[MI][CB];
+    // DA (cooperative form, one wave per SIMD): alternate K-steps accumulate into
+    // two chains, so consecutive MFMAs do not wait on each other's result
+    constexpr bool DA = RB > 1;
+    us_f32x16 acc[MI][CB], accb[MI][CB];
+    auto zero_acc = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < CB; ++j)
+            for (int j = 0; j < CB; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = accb[i][j][r] = 0.f;
+    };
+    auto fold_acc = [&]() __attribute__((always_inline)) {
+        if constexpr (DA) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < CB; ++j) acc[i][j] += accb[i][j];
+        }
+    };
+    zero_acc();
 
     // B fragments: column wn*64 + j*32 + l32, 8 channels at 8*hh
     const int col0 = wn * 32 * CB + l32;
@@ -266,11 +410,16 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
 #pragma unroll
         for (int j = 0; j < CB; ++j) {
             const int off = (row + j * 32) * PH + ch + 8 * hh;
-            f.h[j] = *reinterpret_cast<const us_h8*>(ph + off);
-            f.l[j] = *reinterpret_cast<const us_h8*>(pl + off);
+            if constexpr (F32) {   // 8 floats: channels 8hh..8hh+7 of the step's 16
+                f.h[j] = *reinterpret_cast<const us_h8*>(pf + off);
+                f.l[j] = *reinterpret_cast<const us_h8*>(pf + off + 4);
+            } else {
+                f.h[j] = *reinterpret_cast<const us_h8*>(ph + off);
+                f.l[j] = *reinterpret_cast<const us_h8*>(pl + off);
+            }
         }
     };
-    auto step = [&](int t, int s, const BF& f) __attribute__((always_inline)) {
+    auto step = [&](int t, int s, const BF& f, us_f32x16 (&acc)[MI][CB]) __attribute__((always_inline)) {
         us_h8 ah[MI], al[MI], a2[MI];
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
@@ -279,6 +428,21 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
             a2[i] = ah[i] * (_Float16)2048.0f;
         }
         load_a(t % R, s + R * KG);                   // refill the slot (runs on into W2)
+        if constexpr (F32) {
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int i = 0; i < MI; ++i)
+#pragma unroll
+                        for (int j = 0; j < CB; ++j) {
+                            const us_f32x4 wv = __builtin_bit_cast(us_f32x4, hf ? al[i] : ah[i]);
+                            const us_f32x4 xv = __builtin_bit_cast(us_f32x4, hf ? f.l[j] : f.h[j]);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[e], xv[e], acc[i][j], 0, 0, 0);
+                        }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -294,7 +458,7 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     };
 
     // per-lane rows of the accumulators: m = 32 MI wm + 32i + 8g + 4hh + e
-    const int mrow0 = 32 * MI * wm + 4 * hh;
+    const int mrow0 = 32 * MI * wmg + 4 * hh;
     // own K-steps [t0, t1) of this wave's group: global step t*KG + GG
     auto kloop = [&](auto gtag, auto t0tag, auto t1tag) __attribute__((always_inline)) {
         constexpr int GG = decltype(gtag)::value;
@@ -305,7 +469,8 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
         for (int t = T0; t < T1; ++t) {
             if (t + 1 < T1) read_b((t + 1) * KG + GG, f[(t + 1 - T0) & 1]);
             __builtin_amdgcn_sched_barrier(0);
-            step(t, t * KG + GG, f[(t - T0) & 1]);
+            if (DA && ((t - T0) & 1)) step(t, t * KG + GG, f[(t - T0) & 1], accb);
+            else step(t, t * KG + GG, f[(t - T0) & 1], acc);
         }
     };
     // group 1 hands its partial sums to group 0 through LDS (over the dead planes)
@@ -335,6 +500,7 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     };
     if (KG == 1 || kg == 0) kloop(IC<0>{}, IC<0>{}, IC<S1 / KG>{});
     else kloop(IC<1>{}, IC<0>{}, IC<S1 / KG>{});
+    fold_acc();
     combine();
     __syncthreads();                                 // window (and hand-off area) dead
     US_STAMP(2);
@@ -343,7 +509,11 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     // (phase 1 ran on act0(x) 2^-sh0: its scale 2^sh0 rides on rs1; xs = the
     // range guard's scale of h; returns max |h xs| of the thread's values)
     const float f0 = ldexpf(1.0f, sh0);
-    auto seam = [&](float xs) __attribute__((always_inline)) {
+    // cooperative form: this group's exchange slot (act2(h) as [BN columns][C] fp32)
+    const auto xcrs = us_rsrc(a.xch, RB > 1 ? a.xch_bytes : 0);
+    const unsigned xslot = (unsigned)lg * (unsigned)(G::BN * C);
+    auto seam = [&](float xs, auto pubtag) __attribute__((always_inline)) {
+        constexpr bool publish = decltype(pubtag)::value != 0 && RB > 1;
         float cmax = 0.f;
         if (KG == 1 || kg == 0) {
 #pragma unroll
@@ -361,6 +531,14 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
                             v[e] = us_act<SNAKE>(acc[i][j][4 * g + e] * rs[e] + bb[e], slope, al[e]) * xs;
+                        if constexpr (publish)   // write-through (sc1): read by the other members
+                            __builtin_amdgcn_raw_buffer_store_b128(
+                                __builtin_bit_cast(us_u32x4, v), xcrs,
+                                (xslot + (unsigned)((col0 + 32 * j) * C + m)) * 4u, 0, 16);
+                        if constexpr (F32) {
+                            *reinterpret_cast<us_f32x4*>(pf + (col0 + 32 * j) * PH + m) = v;
+                            continue;
+                        }
 #pragma unroll
                         for (int e = 0; e < 4; ++e) cmax = fmaxf(cmax, fabsf(v[e]));
                         const us_h4 hv = __builtin_convertvector(v, us_h4);
@@ -372,26 +550,112 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
         }
         return cmax;
     };
-    {                                            // range guard of h (rare path: h * 2^-sh2)
-        const float cmax = seam(1.0f);
-        vote_cast(vote, wave, cmax);
+    bool gave_up = false;                        // cooperative seam: a member never arrived
+    if constexpr (RB == 1) {                     // range guard of h (rare path: h * 2^-sh2)
+        const float cmax = seam(1.0f, IC<0>{});
+        if constexpr (!F32) vote_cast(vote, wave, cmax);
         __syncthreads();
-        if (__builtin_expect(vote_any<G::NW>(vote), 0)) {
+        if (!F32 && __builtin_expect(vote_any<G::NW>(vote), 0)) {
             sh2 = __builtin_amdgcn_readfirstlane(split_shift(block_max<G::NW>(cmax, vred)));
-            (void)seam(ldexpf(1.0f, -sh2));
+            (void)seam(ldexpf(1.0f, -sh2), IC<0>{});
             __syncthreads();
         }
+    } else {
+        // publish own rows (and own planes, optimistically unscaled), then the
+        // workgroup's max |h|; every storing wave drains; one lane signals
+        const float cmax = seam(1.0f, IC<1>{});
+        const float mx = block_max<G::NW>(cmax, vred);
+        unsigned* arrive = a.flags + a.flag_stride * lg;
+        if (tid == 0)
+            __hip_atomic_store(reinterpret_cast<unsigned*>(a.xmax) + lg * RB + rb, __builtin_bit_cast(unsigned, mx),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (wave == 0) {
+            if (lane == 0) __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned spins = 0;
+            bool ok = true;
+            for (;;) {
+                const unsigned n = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (n >= (unsigned)RB) break;
+                if (++spins > kUSSpinLimit) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) {
+                vote[0] = ok ? 0 : 1;
+                if (!ok) __hip_atomic_store(a.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        US_STAMP(6);
+        gave_up = __builtin_amdgcn_readfirstlane(vote[0]) != 0;
+        // group-wide range guard: the members' maxima (vector sc1 loads, not the scalar path)
+        float gmax = 0.f;
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+            gmax = fmaxf(gmax, __builtin_bit_cast(float, __hip_atomic_load(reinterpret_cast<unsigned*>(a.xmax) + lg * RB + r,
+                                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+        if constexpr (!F32) sh2 = __builtin_amdgcn_readfirstlane((RAVE_SPLIT_GUARD && gmax >= kSplitLimit) ? split_shift(gmax) : 0);
+        // stage the other members' rows (all rows, scaled, on the rare guarded path)
+        auto stage_rows = [&](auto alltag, float xs) __attribute__((always_inline)) {
+            constexpr bool all = decltype(alltag)::value != 0;
+            constexpr int NG = all ? C / 8 : C / 8 - G::G8R;           // 8-channel groups per column
+            constexpr int NTK = (G::BN * NG + NT - 1) / NT;
+            us_f32x4 v0[NTK], v1[NTK];
+#pragma unroll
+            for (int i = 0; i < NTK; ++i) {
+                const int e = min(tid + i * NT, G::BN * NG - 1);
+                const int w = e / NG;
+                int g = e - w * NG;
+                if (!all && g >= rb * G::G8R) g += G::G8R;
+                const float* src = a.xch + xslot + w * C + g * 8;
+                v0[i] = *reinterpret_cast<const us_f32x4*>(src);
+                v1[i] = *reinterpret_cast<const us_f32x4*>(src + 4);
+            }
+#pragma unroll
+            for (int i = 0; i < NTK; ++i) {
+                const int e = tid + i * NT;
+                if (e >= G::BN * NG) break;
+                const int w = e / NG;
+                int g = e - w * NG;
+                if (!all && g >= rb * G::G8R) g += G::G8R;
+                if constexpr (F32) {
+                    *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8) = v0[i];
+                    *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8 + 4) = v1[i];
+                } else {
+                    const us_f32x8 v8 = us_f32x8{v0[i][0], v0[i][1], v0[i][2], v0[i][3],
+                                                 v1[i][0], v1[i][1], v1[i][2], v1[i][3]} * xs;
+                    const us_h8 hi = __builtin_convertvector(v8, us_h8);
+                    const us_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, us_f32x8)) * 2048.0f, us_h8);
+                    *reinterpret_cast<us_h8*>(ph + w * PH + g * 8) = hi;
+                    *reinterpret_cast<us_h8*>(pl + w * PH + g * 8) = lo;
+                }
+            }
+        };
+        if (__builtin_expect(sh2 != 0, 0)) stage_rows(IC<1>{}, ldexpf(1.0f, -sh2));
+        else stage_rows(IC<0>{}, 1.0f);
+        __syncthreads();
+        // departures: the last member to leave re-arms the group's counters
+        if (tid == 0) {
+            const unsigned prev = __hip_atomic_fetch_add(arrive + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev == (unsigned)RB - 1) {
+                __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(arrive + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < CB; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    zero_acc();
     US_STAMP(3);
 
     if (KG == 1 || kg == 0) kloop(IC<0>{}, IC<S1 / KG>{}, IC<ST / KG>{});
     else kloop(IC<1>{}, IC<S1 / KG>{}, IC<ST / KG>{});
+    fold_acc();
     combine();
     if (KG == 2 && kg == 1) return;                  // (no barrier follows)
 
@@ -429,7 +693,8 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
                         __builtin_amdgcn_raw_buffer_store_b32(
-                            __builtin_bit_cast(unsigned, acc[i][j][4 * g + e] * rs[e] + bb[e] + res[i][j][4 * g + e]),
+                            __builtin_bit_cast(unsigned, gave_up ? __builtin_nanf("")
+                                                                 : acc[i][j][4 * g + e] * rs[e] + bb[e] + res[i][j][4 * g + e]),
                             yrs, nok ? (unsigned)((m + e) * a.y_sc + n) * 4u : kUSOOB, 0, RAVE_YAUX);
                 }
             }
@@ -437,23 +702,38 @@ __global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_split_ke
     US_STAMP(5);
 }
 
-template <int C, int WGN, int MI, int KG, int CB>
-static int us_launch(USArgs k, int B, bool snake, hipStream_t st) {
-    using G = USGeo<C, WGN, MI, KG, CB>;
+template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, int RB>
+__global__ __launch_bounds__(64 * (C / (32 * MI * RB)) * WGN * KG) void unit_split_kernel(USArgs a) {
+    unit_split_body<C, WGN, MI, KG, CB, SNAKE, false, RB>(a);
+}
+template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, int RB>
+__global__ __launch_bounds__(64 * (C / (32 * MI * RB)) * WGN * KG) void unit_ring_f32_kernel(USArgs a) {
+    unit_split_body<C, WGN, MI, KG, CB, SNAKE, true, RB>(a);
+}
+
+template <int C, int WGN, int MI, int KG, int CB, int RB = 1>
+static int us_launch(USArgs k, int B, bool snake, bool f32, hipStream_t st) {
+    using G = USGeo<C, WGN, MI, KG, CB, RB>;
     if (k.XW > G::XW_MAX) {
         set_error("residual_unit(split16): dilation too large");
         return RAVE_ERR_UNSUPPORTED;
     }
     k.ntiles = ceil_div(k.T, G::BN);
-    auto kern = snake ? unit_split_kernel<C, WGN, MI, KG, CB, true> : unit_split_kernel<C, WGN, MI, KG, CB, false>;
-    static bool attr[2] = {false, false};
-    if (G::LDS > 65536 && !attr[snake]) {
+    auto kern = f32 ? (snake ? unit_ring_f32_kernel<C, WGN, MI, KG, CB, true, RB> : unit_ring_f32_kernel<C, WGN, MI, KG, CB, false, RB>)
+                    : (snake ? unit_split_kernel<C, WGN, MI, KG, CB, true, RB> : unit_split_kernel<C, WGN, MI, KG, CB, false, RB>);
+    static bool attr[4] = {false, false, false, false};
+    if (G::LDS > 65536 && !attr[2 * f32 + snake]) {
         RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr[snake] = true;
+        attr[2 * f32 + snake] = true;
     }
-    launch(kern, dim3(k.ntiles * B), dim3(G::NT), (uint32_t)G::LDS, st, k);
-    return launch_status("unit_split_kernel");
+    int grid = k.ntiles * B;
+    if constexpr (RB > 1) {
+        k.ngroups = grid;
+        grid = ceil_div(grid, 8) * 8 * RB;          // whole groups per XCD slot
+    }
+    launch(kern, dim3(grid), dim3(G::NT), (uint32_t)G::LDS, st, k);
+    return launch_status(f32 ? "unit_ring_f32_kernel" : "unit_split_kernel");
 }
 
 static bool us_supported(int C) { return C == 64 || C == 128 || C == 256 || C == 512; }
@@ -467,6 +747,7 @@ static int us_row_exponent(double amax) {
     return e;
 }
 
+
 }  // namespace rave
 
 using namespace rave;
@@ -479,7 +760,7 @@ extern "C" int64_t rave_unit_split_packed_size(int C) {
     return (int64_t)(C / 32) * ST * 2 * 256 + 2 * C;
 }
 
-extern "C" int rave_unit_split_pack_weight(const float* w1, const float* w2, int C, float* packed) {
+static int unit_pack(const float* w1, const float* w2, int C, float* packed, bool f32) {
     RAVE_CHECK_ARG(w1 && w2 && packed, "unit_split_pack_weight: null pointer");
     if (!us_supported(C)) {
         set_error("unit_split_pack_weight: split16 fused residual unit supports C in {64, 128, 256, 512}");
@@ -491,14 +772,15 @@ extern "C" int rave_unit_split_pack_weight(const float* w1, const float* w2, int
         double a1 = 0.0, a2 = 0.0;
         for (int k = 0; k < 3 * C; ++k) a1 = std::max(a1, (double)std::fabs(w1[(int64_t)m * 3 * C + k]));
         for (int k = 0; k < C; ++k) a2 = std::max(a2, (double)std::fabs(w2[(int64_t)m * C + k]));
-        e1[m] = us_row_exponent(a1);
-        e2[m] = us_row_exponent(a2);
+        e1[m] = f32 ? 0 : us_row_exponent(a1);
+        e2[m] = f32 ? 0 : us_row_exponent(a2);
     }
     _Float16* out = reinterpret_cast<_Float16*>(packed);
     for (int mb = 0; mb < C / 32; ++mb)
         for (int s = 0; s < ST; ++s) {
             _Float16* hi = out + ((int64_t)(mb * ST + s) * 2) * 512;
             _Float16* lo = hi + 512;
+            float* f32s = packed + ((int64_t)(mb * ST + s) * 2) * 256;   // fp32: floats 0-3 slot 0, 4-7 slot 1
             for (int l = 0; l < 64; ++l)
                 for (int e = 0; e < 8; ++e) {
                     const int m = mb * 32 + (l & 31);
@@ -511,6 +793,10 @@ extern "C" int rave_unit_split_pack_weight(const float* w1, const float* w2, int
                         const int ci = (s - S1) * 16 + kk;
                         v = std::ldexp(w2[(int64_t)m * C + ci], e2[m]);
                     }
+                    if (f32) {
+                        f32s[(e >> 2) * 256 + l * 4 + (e & 3)] = v;
+                        continue;
+                    }
                     const _Float16 vh = (_Float16)v;
                     hi[l * 8 + e] = vh;
                     lo[l * 8 + e] = (_Float16)((v - (float)vh) * 2048.0f);
@@ -518,10 +804,18 @@ extern "C" int rave_unit_split_pack_weight(const float* w1, const float* w2, int
         }
     float* rs = packed + (int64_t)(C / 32) * ST * 2 * 256;
     for (int m = 0; m < C; ++m) {
-        rs[m] = (float)std::ldexp(1.0, -(e1[m] + 11));
-        rs[C + m] = (float)std::ldexp(1.0, -(e2[m] + 11));
+        rs[m] = f32 ? 1.0f : (float)std::ldexp(1.0, -(e1[m] + 11));
+        rs[C + m] = f32 ? 1.0f : (float)std::ldexp(1.0, -(e2[m] + 11));
     }
     return RAVE_OK;
+}
+
+extern "C" int rave_unit_split_pack_weight(const float* w1, const float* w2, int C, float* packed) {
+    return unit_pack(w1, w2, C, packed, false);
+}
+
+extern "C" int rave_unit_ring_pack_weight(const float* w1, const float* w2, int C, float* packed) {
+    return unit_pack(w1, w2, C, packed, true);
 }
 
 #ifdef RAVE_STAMPS
@@ -532,6 +826,42 @@ extern "C" int rave_diag_unit_stamps(void* p) {
 #endif
 
 namespace rave {
+// Cooperative form (header comment): C = 256 and 512, groups of C/128 workgroups
+// over 32-column slabs.  RAVE_UNIT_COOP=0 keeps one workgroup per slab (A/B).
+static bool coop_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("RAVE_UNIT_COOP");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+constexpr int kCoopBN = 32;
+struct CoopLayout {
+    int rb = 1, stride = 2;                               // counter words per group
+    int64_t groups = 0, xmax = 0, xch = 0, floats = 0;   // offsets / sizes in floats
+};
+static CoopLayout coop_layout(const rave_unit_args& a) {
+    CoopLayout L;
+    const int C = a.channels;
+    if ((C != 256 && C != 512) || !coop_enabled() || a.batch <= 0 || a.t_len <= 0) return L;
+    if (a.precision != RAVE_PREC_SPLIT16 && a.precision != RAVE_PREC_F32_RING) return L;
+    const int64_t ng = (int64_t)ceil_div(a.t_len, kCoopBN) * a.batch;
+    const int64_t ngp = ceil_div64(ng, 8) * 8;
+    // counters live in the split-K ticket words (zero at rest, as the conv
+    // kernels leave theirs); the last ticket word is the give-up word
+    if (2 * ngp > RAVE_SPLITK_TICKETS - 1) return L;
+    // a group's counters on a 128-byte line of their own where the words allow
+    while (L.stride < 32 && 2 * L.stride * ngp <= RAVE_SPLITK_TICKETS - 1) L.stride *= 2;
+    const int rb = C / 128;
+    L.groups = ng;
+    L.xmax = RAVE_SPLITK_TICKETS;
+    L.xch = L.xmax + ceil_div64(ngp * rb, 64) * 64;
+    L.floats = L.xch + ngp * kCoopBN * C;
+    if (ngp * kCoopBN * C * 4 >= (1ll << 31)) return CoopLayout{};
+    L.rb = rb;
+    return L;
+}
+
 int residual_unit_split(const rave_unit_args& a, void* stream) {
     const int C = a.channels;
     if (!us_supported(C)) {
@@ -557,13 +887,30 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
     // one 32-row block per wave (MI = 1): C/32 waves along rows, 64 columns each
     // (measured against two row blocks per wave, other column counts and
     // K-groups: tools/layer_bench.py unit_64/128/256)
-    auto go = [&](auto cc, auto wgn, auto mi, auto kgt, auto cb) {
+    auto go = [&](auto cc, auto wgn, auto mi, auto kgt, auto cb, auto rbt) {
         constexpr int CC = decltype(cc)::value, WGN = decltype(wgn)::value, MI = decltype(mi)::value,
-                      KG = decltype(kgt)::value, CB = decltype(cb)::value;
-        k.XW = USGeo<CC, WGN, MI, KG, CB>::BN + 2 * a.dilation;
+                      KG = decltype(kgt)::value, CB = decltype(cb)::value, RB = decltype(rbt)::value;
+        k.XW = USGeo<CC, WGN, MI, KG, CB, RB>::BN + 2 * a.dilation;
         k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
-        return us_launch<CC, WGN, MI, KG, CB>(k, a.batch, snake, st);
+        const int off = (4 - a.pad_left % 4) % 4;      // window start past its 4-aligned block start
+        const int nb = (off + k.XW + 3) / 4;
+        k.nb_magic = (unsigned)(((1u << 24) + nb - 1) / nb);
+        return us_launch<CC, WGN, MI, KG, CB, RB>(k, a.batch, snake, a.precision == RAVE_PREC_F32_RING, st);
     };
+    k.xv = (a.t_len % 4 == 0 && a.x_sc % 4 == 0 && a.x_sb % 4 == 0 &&
+            reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && std::getenv("RAVE_UNIT_XV") == nullptr) ? 1 : 0;
+    // cooperative form when the caller passed its workspace
+    const CoopLayout L = coop_layout(a);
+    if (L.rb > 1 && a.workspace) {
+        k.flag_stride = L.stride;
+        k.flags = reinterpret_cast<unsigned*>(a.workspace);
+        k.tmo = k.flags + RAVE_SPLITK_TICKETS - 1;
+        k.xmax = a.workspace + L.xmax;
+        k.xch = a.workspace + L.xch;
+        k.xch_bytes = (int)((L.floats - L.xch) * 4);
+        if (C == 256) return go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<2>{});
+        return go(IC<512>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<4>{});
+    }
     // (K-groups, KG = 2, measured slower for every C: 13.3/11.6/19.5 -> 16.8/12.0/21.5 us)
     // (WGN, CB) per C, measured (tools/layer_bench.py unit_*): C=256 with one
     // column block per wave 19.6 -> 14.4 us; C=128 11.6 -> 11.3 us; wider waves
@@ -577,15 +924,21 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
 #ifndef RAVE_U128_WGN
 #define RAVE_U128_WGN 2
 #endif
-    if (C == 64) return go(IC<64>{}, IC<RAVE_U64_WGN>{}, IC<1>{}, IC<1>{}, IC<RAVE_U64_CB>{});
+    if (C == 64) return go(IC<64>{}, IC<RAVE_U64_WGN>{}, IC<1>{}, IC<1>{}, IC<RAVE_U64_CB>{}, IC<1>{});
 #ifndef RAVE_U128_KG
 #define RAVE_U128_KG 1
 #endif
 #ifndef RAVE_U256_KG
 #define RAVE_U256_KG 1
 #endif
-    if (C == 128) return go(IC<128>{}, IC<RAVE_U128_WGN>{}, IC<1>{}, IC<RAVE_U128_KG>{}, IC<1>{});
-    if (C == 256) return go(IC<256>{}, IC<1>{}, IC<1>{}, IC<RAVE_U256_KG>{}, IC<1>{});
-    return go(IC<512>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{});
+    if (C == 128) return go(IC<128>{}, IC<RAVE_U128_WGN>{}, IC<1>{}, IC<RAVE_U128_KG>{}, IC<1>{}, IC<1>{});
+    if (C == 256) return go(IC<256>{}, IC<1>{}, IC<1>{}, IC<RAVE_U256_KG>{}, IC<1>{}, IC<1>{});
+    return go(IC<512>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{});
 }
+
 }  // namespace rave
+
+extern "C" int64_t rave_unit_workspace(const rave_unit_args* a) {
+    RAVE_CHECK_ARG(a, "unit_workspace: null pointer");
+    return rave::coop_layout(*a).floats;
+}

@@ -149,11 +149,17 @@ def conv_case(case):
     return x, w, b, alpha.reshape(-1) if alpha is not None else None, res, pad, ref
 
 
+def _ring_skip(precision, T):
+    if precision == "f32_ring" and T % 4:
+        pytest.skip("the fp32 ring kernels need 16-byte aligned rows (refusal: test_conv_ring_refuses_unaligned)")
+
+
 @pytest.mark.parametrize("precision", ["f32", "split16", "f32_ring"])
 @pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("case", CONV_CASES, ids=[str(c[:8]) for c in CONV_CASES])
 def test_conv_layer(N, dev, case, split, precision):
     c_in, c_out, k, s, d, transposed, act, has_res, B, T = case
+    _ring_skip(precision, T)
     x, w, b, alpha, res, pad, ref = conv_case(case)
     got = run_conv(N, dev, x, w, b, alpha, res,
                    c_in, c_out, k, s, d, pad, transposed, act, split, N.PRECISION[precision])
@@ -170,6 +176,7 @@ def test_conv_every_config(N, dev, case, precision):
     """Every launch configuration rave_conv1d_configs() offers the autotuner
     (tile shape x K-splits x split-K combine) meets the layer tolerance."""
     c_in, c_out, k, s, d, transposed, act, has_res, B, T = case
+    _ring_skip(precision, T)
     x, w, b, alpha, res, pad, ref = conv_case(case)
     t_out = ref.shape[-1]
     a = N.ConvArgs(c_in=c_in, c_out=c_out, kernel=k, stride=s, dilation=d,
@@ -184,6 +191,16 @@ def test_conv_every_config(N, dev, case, precision):
                        N.PRECISION[precision], config=cfg)
         err = maxabs(got, ref)
         assert np.isfinite(got).all() and err <= 2e-5 * max(1.0, np.abs(ref).max()), (cfg, err)
+
+
+def test_conv_ring_refuses_unaligned(N, dev):
+    """RAVE_PREC_F32_RING refuses rows it cannot DMA in 16-byte pieces (the
+    autotuner then keeps the register-staged fp32 kernel for that op)."""
+    c_in, c_out, k, T = 64, 64, 3, 257
+    x, w = np.zeros((1, c_in, T), np.float32), np.zeros((c_out, c_in, k), np.float32)
+    with pytest.raises(NotImplementedError, match="16-byte aligned"):
+        run_conv(N, dev, x, w, None, None, None, c_in, c_out, k, 1, 1, (1, 1), 0, "leaky", False,
+                 N.PREC_F32_RING)
 
 
 # ------------------------------------------------------------------ PQMF
@@ -764,7 +781,7 @@ UNIT_CASES = [
 ]
 
 
-@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("precision", PRECISIONS + ["f32_ring"])
 @pytest.mark.parametrize("case", UNIT_CASES, ids=[str(c) for c in UNIT_CASES])
 def test_residual_unit_kernel(N, dev, case, precision):
     """rave_residual_unit == x + conv1x1(act(conv3_d(act(x)) + b1)) + b2 (oracle, float64)."""
@@ -799,6 +816,68 @@ def test_residual_unit_kernel(N, dev, case, precision):
     N.check(N.lib.rave_residual_unit(C_.byref(a), C_.c_void_p(torch.cuda.current_stream().cuda_stream)))
     torch.cuda.synchronize()
     got = y.cpu().numpy()
+    assert np.isfinite(got).all()
+    assert maxabs(got, ref) <= 2e-5 * max(1.0, float(np.abs(ref).max()))
+
+
+COOP_CASES = [
+    # C, d, act, causal, B, T
+    (256, 3, "leaky", False, 16, 256),
+    (256, 9, "snake", True, 3, 77),
+    (512, 3, "leaky", False, 16, 128),
+    (512, 1, "snake", False, 2, 40),
+    (512, 9, "leaky", True, 5, 333),
+]
+
+
+@pytest.mark.parametrize("precision", ["split16", "f32_ring"])
+@pytest.mark.parametrize("case", COOP_CASES, ids=[str(c) for c in COOP_CASES])
+def test_residual_unit_cooperative(N, dev, case, precision):
+    """The cooperative fused unit (groups of C/128 workgroups handing act2(h) rows
+    to each other inside the launch, rave_unit_workspace) matches the one-
+    workgroup-per-slab kernel (same operands; its K-steps alternate over two
+    accumulator chains, so sums differ in the last bits only), meets the
+    oracle, leaves its counters zero (three calls on one workspace) and never
+    gives up waiting (a give-up writes NaN)."""
+    from oracle.rave_oracle import conv1d, leaky_relu, snake
+    C, d, act, causal, B, T = case
+    prec = N.PRECISION[precision]
+    if precision == "f32_ring" and T % 4:
+        pytest.skip("fp32 ring units need whole 16-byte rows")
+    rng = np.random.default_rng(C + d + T)
+    x = rng.standard_normal((B, C, T)).astype(np.float32)
+    w1 = (rng.standard_normal((C, C, 3)) / np.sqrt(3 * C)).astype(np.float32)
+    w2 = (rng.standard_normal((C, C, 1)) / np.sqrt(C)).astype(np.float32)
+    b1, b2 = (rng.standard_normal(C).astype(np.float32) * 0.1 for _ in range(2))
+    a0, a2 = ((1 + 0.3 * rng.standard_normal(C)).astype(np.float32) for _ in range(2))
+    pad = (2 * d, 0) if causal else (d, d)
+    f = (lambda v, al: snake(v, al.reshape(-1, 1))) if act == "snake" else (lambda v, al: leaky_relu(v, 0.2))
+    h = f(conv1d(f(x.astype(np.float64), a0), w1, b1, 1, d, pad), a2)
+    ref = x + conv1d(h, w2, b2, 1, 1, (0, 0))
+    packed = torch.from_numpy(N.pack_unit_weight(w1, w2, C, precision=prec)).to(dev)
+    xd = torch.from_numpy(x).to(dev)
+    dd = {k: torch.from_numpy(v).to(dev) for k, v in dict(b1=b1, b2=b2, a0=a0, a2=a2).items()}
+
+    def args(y, ws):
+        return N.UnitArgs(channels=C, batch=B, t_len=T, dilation=d, pad_left=pad[0], act=N.ACT[act],
+                          leaky_slope=0.2, precision=prec, x=xd.data_ptr(), x_sb=C * T, x_sc=T, y=y.data_ptr(),
+                          y_sb=C * T, y_sc=T, weight=packed.data_ptr(), bias1=dd["b1"].data_ptr(),
+                          bias2=dd["b2"].data_ptr(), alpha0=dd["a0"].data_ptr() if act == "snake" else None,
+                          alpha2=dd["a2"].data_ptr() if act == "snake" else None,
+                          workspace=ws.data_ptr() if ws is not None else None)
+    st = C_.c_void_p(torch.cuda.current_stream().cuda_stream)
+    y1 = torch.full_like(xd, float("nan"))
+    N.check(N.lib.rave_residual_unit(C_.byref(args(y1, None)), st))
+    nws = N.lib.rave_unit_workspace(C_.byref(args(y1, None)))
+    assert nws > N.SPLITK_TICKETS
+    ws = torch.zeros(nws, device=dev)
+    for _ in range(3):
+        y2 = torch.full_like(xd, float("nan"))
+        N.check(N.lib.rave_residual_unit(C_.byref(args(y2, ws)), st))
+        torch.cuda.synchronize()
+        assert float((y1 - y2).abs().max()) <= 1e-6 * float(y1.abs().max())
+        assert int(torch.count_nonzero(ws[:N.SPLITK_TICKETS])) == 0      # counters re-armed, no give-up
+    got = y2.cpu().numpy()
     assert np.isfinite(got).all()
     assert maxabs(got, ref) <= 2e-5 * max(1.0, float(np.abs(ref).max()))
 

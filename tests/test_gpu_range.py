@@ -126,10 +126,14 @@ def _unit_ref(x, w1, w2, b1, b2, d, pad):
     return x + conv1d(h, w2, b2, 1, 1, (0, 0))
 
 
-@pytest.mark.parametrize("C_,where", [(64, "input"), (128, "seam"), (256, "input"), (512, "seam")])
-def test_unit_range_guard(N, dev, C_, where):
+@pytest.mark.parametrize("C_,where,coop", [(64, "input", False), (128, "seam", False), (256, "input", False),
+                                           (512, "seam", False), (256, "input", True), (512, "seam", True),
+                                           (256, "seam_one", True), (512, "seam_one", True)])
+def test_unit_range_guard(N, dev, C_, where, coop):
     """rave_residual_unit (split16): the act0(x) window past f16 (input), or
-    in-range input whose k3 output h is (the seam's own guard)."""
+    in-range input whose k3 output h is (the seam's own guard); cooperative
+    form (rave_unit_workspace): h past f16 in every member, or only in the rows
+    of one member (seam_one: the group-wide guard)."""
     d, B, T = 3, 2, 200
     rng = np.random.default_rng(C_)
     x = rng.standard_normal((B, C_, T)).astype(np.float32)
@@ -137,6 +141,9 @@ def test_unit_range_guard(N, dev, C_, where):
     w2 = (rng.standard_normal((C_, C_, 1)) / np.sqrt(C_)).astype(np.float32)
     if where == "input":
         x *= 1e6
+    elif where == "seam_one":
+        w1[:128] *= 1e6                   # rows of the group's first member only
+        w2 *= 1e-3
     else:
         w1 *= 1e6
         w2 *= 1e-3
@@ -150,8 +157,16 @@ def test_unit_range_guard(N, dev, C_, where):
     a = N.UnitArgs(channels=C_, batch=B, t_len=T, dilation=d, pad_left=d, act=N.ACT["leaky"], leaky_slope=0.2,
                    precision=N.PREC_SPLIT16, x=xd.data_ptr(), x_sb=C_ * T, x_sc=T, y=y.data_ptr(), y_sb=C_ * T,
                    y_sc=T, weight=packed.data_ptr(), bias1=bd1.data_ptr(), bias2=bd2.data_ptr())
+    ws = None
+    if coop:
+        nws = N.lib.rave_unit_workspace(C.byref(a))
+        assert nws > 0
+        ws = torch.zeros(nws, device=dev)
+        a.workspace = ws.data_ptr()
     N.check(N.lib.rave_residual_unit(C.byref(a), _stream()))
     torch.cuda.synchronize()
+    if coop:
+        assert int(torch.count_nonzero(ws[:N.SPLITK_TICKETS])) == 0
     got = y.cpu().numpy()
     assert np.isfinite(got).all()
     err = maxabs(got, ref)

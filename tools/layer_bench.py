@@ -57,6 +57,7 @@ def stamp_report(s_):
 
 def run_unit(name, B, iters, dev):
     C, d, T = UNITS[name]
+    name0 = name
     rng = np.random.default_rng(0)
     w1 = (rng.standard_normal((C, C, 3)) / np.sqrt(3 * C)).astype(np.float32)
     w2 = (rng.standard_normal((C, C, 1)) / np.sqrt(C)).astype(np.float32)
@@ -67,6 +68,12 @@ def run_unit(name, B, iters, dev):
     a = N.UnitArgs(channels=C, batch=B, t_len=T, dilation=d, pad_left=d, act=N.ACT["leaky"],
                    leaky_slope=0.2, precision=PREC, x=x.data_ptr(), x_sb=C * T, x_sc=T, y=y.data_ptr(),
                    y_sb=C * T, y_sc=T, weight=packed.data_ptr(), bias1=b1.data_ptr(), bias2=b2.data_ptr())
+    ws = None
+    nws = N.lib.rave_unit_workspace(C_.byref(a))
+    if nws > 0 and os.environ.get("LB_UNIT_COOP", "1") != "0":   # cooperative form (C 256 / 512)
+        ws = torch.zeros(nws, device=dev)
+        a.workspace = ws.data_ptr()
+        name = name + "_coop"
     st = C_.c_void_p(torch.cuda.current_stream().cuda_stream)
     stamps = None
     if STAMPS and PREC == N.PREC_SPLIT16:
@@ -168,7 +175,7 @@ def main():
     ap.add_argument("--layers", default=",".join(list(LAYERS) + list(UNITS)))
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--batch", type=int, default=16)
-    ap.add_argument("--precision", default="split16", choices=["f32", "split16"])
+    ap.add_argument("--precision", default="split16", choices=["f32", "split16", "f32_ring"])
     ap.add_argument("--config", default="0", help="launch config value, or 'all' (every listed one)")
     a = ap.parse_args()
     global PREC

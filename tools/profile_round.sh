@@ -19,14 +19,14 @@ BENCH="$R/bench.py --steps 10 --warmup 3"
 timeout -k 10 300 python3 $BENCH --tuning-out "$OUT/tuning.json" > "$OUT/bench.json" 2> "$OUT/bench.err"
 echo "bench: $(cat $OUT/bench.json)"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
-    python3 $BENCH --no-cpu-baseline --pipeline 1 --tuning-in "$OUT/tuning.json" > "$OUT/bench_kt.json" 2> "$OUT/bench_kt.err"
+    python3 $BENCH --no-cpu-baseline --no-f32 --pipeline 1 --tuning-in "$OUT/tuning.json" > "$OUT/bench_kt.json" 2> "$OUT/bench_kt.err"
 echo "kernel-trace pass done"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run -- \
-    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --pipeline 1 \
+    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --pipeline 1 --no-f32 \
     --tuning-in "$OUT/tuning.json" > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
 echo "fetch pass done"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run -- \
-    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --pipeline 1 \
+    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --pipeline 1 --no-f32 \
     --tuning-in "$OUT/tuning.json" > "$OUT/bench_write.json" 2> "$OUT/bench_write.err"
 echo "write pass done"
 timeout -k 10 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/mfma" -o run -- \
