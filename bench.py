@@ -67,6 +67,10 @@ FAMILIES = {
                      "MFMA 16x16x32 / 32x32x16", PEAK_SPLIT16_TFLOPS),
     "tail_split16": ("decoder_tail_kernel: GeneratorV2's last conv + epilogue + PQMF synthesis, split-f16 "
                      "MFMA 32x32x16 / 16x16x32", PEAK_SPLIT16_TFLOPS),
+    "head_f32": ("encoder_head_kernel<F32>: PQMF analysis (phase-packed) + EncoderV2's first conv, exact fp32 "
+                 "MFMA 16x16x4 / 32x32x2", PEAK_FP32_TFLOPS),
+    "tail_f32": ("decoder_tail_kernel<F32>: GeneratorV2's last conv + epilogue + PQMF synthesis, exact fp32 "
+                 "MFMA 32x32x2 / 16x16x4", PEAK_FP32_TFLOPS),
 }
 
 
@@ -84,9 +88,9 @@ def op_family(kind: int, precision: int) -> str:
     if kind == N.OP_PQMF_SYNTHESIS:
         return "pqmf_synthesis_" + prec
     if kind == N.OP_HEAD:
-        return "head_split16"
+        return "head_" + prec
     if kind == N.OP_TAIL:
-        return "tail_split16"
+        return "tail_" + prec
     return "other"
 
 

@@ -389,6 +389,8 @@ int rave_residual_stack(const rave_stack_args* a, void* stream);
  *   rave_decoder_tail_pack_filter image; act RAVE_ACT_LEAKY / RAVE_ACT_SNAKE
  *   (alpha: 64 floats).
  * weight: the conv's rave_conv1d_split_pack_weight image (7 taps, stride 1).
+ * precision RAVE_PREC_F32_RING: exact fp32 (v_mfma_f32_16x16x4 / 32x32x2) with the
+ * conv's rave_conv1d_ring_pack_weight image and a *_pack_filter_f32 filter image.
  */
 typedef struct rave_edge_args {
     int32_t batch, frames;          /* PQMF frames (audio samples / 16)                    */
@@ -396,7 +398,8 @@ typedef struct rave_edge_args {
     int32_t pqmf_taps, pqmf_pad_left;
     int32_t mode, act;              /* tail: synthesis mode 1 / 2; the conv input act      */
     float leaky_slope;
-    int32_t fill_channels, fill_t, _pad0;
+    int32_t fill_channels, fill_t;
+    int32_t precision;  /* 0 / RAVE_PREC_SPLIT16, or RAVE_PREC_F32_RING (exact fp32)      */
     const float* x;     int64_t x_sb, x_sc;
     float* y;           int64_t y_sb, y_sc;
     const float* weight;
@@ -417,6 +420,9 @@ int rave_decoder_tail(const rave_edge_args* a, void* stream);
 #define RAVE_EDGE_FILTER_FLOATS 8836
 int rave_encoder_head_pack_filter(const float* hkf, int n_band, int taps, int n_out_bands, float* image);
 int rave_decoder_tail_pack_filter(const float* hki, int n_band, int taps, float* image);
+/* exact-fp32 images (precision RAVE_PREC_F32_RING): fp32 rows of 552, scale 1 */
+int rave_encoder_head_pack_filter_f32(const float* hkf, int n_band, int taps, int n_out_bands, float* image);
+int rave_decoder_tail_pack_filter_f32(const float* hki, int n_band, int taps, float* image);
 
 /* ---------------------------------------------------------------- plans
  * A plan is a recorded sequence of the ops above (the module graph of

@@ -183,7 +183,7 @@ class MaxPoolArgs(C.Structure):
 class EdgeArgs(C.Structure):
     _fields_ = [("batch", i32), ("frames", i32), ("conv_c_in", i32), ("conv_c_out", i32), ("conv_kernel", i32),
                 ("conv_pad_left", i32), ("pqmf_taps", i32), ("pqmf_pad_left", i32), ("mode", i32), ("act", i32),
-                ("leaky_slope", f32), ("fill_channels", i32), ("fill_t", i32), ("_pad0", i32),
+                ("leaky_slope", f32), ("fill_channels", i32), ("fill_t", i32), ("precision", i32),
                 ("x", vp), ("x_sb", i64), ("x_sc", i64), ("y", vp), ("y_sb", i64), ("y_sc", i64),
                 ("weight", vp), ("bias", vp), ("alpha", vp), ("filter", vp),
                 ("noise", vp), ("n_sb", i64), ("n_sc", i64),
@@ -256,6 +256,7 @@ EXPORTS = [
     "rave_stream_delay",
     "rave_fir", "rave_row_stats", "rave_attn_pool", "rave_linear", "rave_maxpool",
     "rave_encoder_head", "rave_decoder_tail", "rave_encoder_head_pack_filter", "rave_decoder_tail_pack_filter",
+    "rave_encoder_head_pack_filter_f32", "rave_decoder_tail_pack_filter_f32",
 ]
 EDGE_FILTER_FLOATS = 8836   # RAVE_EDGE_FILTER_FLOATS
 
@@ -284,6 +285,8 @@ def _load():
     lib.rave_conv1d_split_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
     lib.rave_conv1d_ring_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
     lib.rave_encoder_head_pack_filter.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp]
+    lib.rave_encoder_head_pack_filter_f32.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp]
+    lib.rave_decoder_tail_pack_filter_f32.argtypes = [vp, C.c_int, C.c_int, vp]
     lib.rave_decoder_tail_pack_filter.argtypes = [vp, C.c_int, C.c_int, vp]
     lib.rave_unit_packed_size.argtypes = [C.c_int]
     lib.rave_unit_packed_size.restype = i64
@@ -447,18 +450,19 @@ def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed, out_s
     return out
 
 
-def pack_edge_filter(filt, head: bool, n_out_bands: int = 6):
+def pack_edge_filter(filt, head: bool, n_out_bands: int = 6, f32: bool = False):
     """PQMF filter -> the fused edges' pre-split image (numpy float32):
-    head: hkf (16, taps) analysis rows; tail: hki (16, 16, taps)."""
+    head: hkf (16, taps) analysis rows; tail: hki (16, 16, taps).  f32: the
+    exact-fp32 image (edges run with precision RAVE_PREC_F32_RING)."""
     import numpy as np
     f = np.ascontiguousarray(filt, dtype=np.float32)
     out = np.zeros(EDGE_FILTER_FLOATS, np.float32)
     if head:
-        check(lib.rave_encoder_head_pack_filter(f.ctypes.data, f.shape[0], f.shape[-1], int(n_out_bands),
-                                                out.ctypes.data), "encoder_head_pack_filter")
+        fn = lib.rave_encoder_head_pack_filter_f32 if f32 else lib.rave_encoder_head_pack_filter
+        check(fn(f.ctypes.data, f.shape[0], f.shape[-1], int(n_out_bands), out.ctypes.data), "encoder_head_pack_filter")
     else:
-        check(lib.rave_decoder_tail_pack_filter(f.ctypes.data, f.shape[0], f.shape[-1], out.ctypes.data),
-              "decoder_tail_pack_filter")
+        fn = lib.rave_decoder_tail_pack_filter_f32 if f32 else lib.rave_decoder_tail_pack_filter
+        check(fn(f.ctypes.data, f.shape[0], f.shape[-1], out.ctypes.data), "decoder_tail_pack_filter")
     return out
 
 

@@ -25,6 +25,13 @@
 // 12 of 16 rows (the unpacked form computes 16 rows for 6 bands and half the
 // frames per MFMA).
 //
+// F32 (rave_edge_args.precision = RAVE_PREC_F32_RING): the same kernels in
+// exact fp32 -- every (hi, lo) plane pair becomes one fp32 plane in the same
+// bytes, each 3-MFMA split-f16 group becomes eight v_mfma_f32_16x16x4 /
+// v_mfma_f32_32x32x2 (lane slot g of a K-group of 8 holds K index 8g + e for
+// MFMA e, on both operands), the filter image is fp32 (scale 1) and the conv
+// weight the ring image (rave_conv1d_ring_pack_weight); no range guard.
+//
 // Ranges: every staged operand block is scaled by one power of two from the
 // workgroup's maximum (PQMF filters: max |h 2^e| in [8, 16); signals: 2^-s
 // with |v 2^-s| < 2^15), so no f16 half overflows; the epilogues undo the
@@ -40,6 +47,12 @@ typedef _Float16 e_h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 e_h4 __attribute__((ext_vector_type(4)));
 typedef float e_f32x4 __attribute__((ext_vector_type(4)));
 typedef float e_f32x16 __attribute__((ext_vector_type(16)));
+typedef float e_f32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ e_f32x8 e_ld8(const float* p) {    // 8 floats (two b128 LDS reads)
+    const e_f32x4 u = *reinterpret_cast<const e_f32x4*>(p), v = *reinterpret_cast<const e_f32x4*>(p + 4);
+    return e_f32x8{u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
+}
 
 constexpr int kEdgeWaves = 8;
 constexpr int kEdgeNT = 64 * kEdgeWaves;
@@ -93,6 +106,11 @@ struct EdgeW {
     __device__ e_h8 frag(int chunk, int mb, int tap, int plane, int lane) const {
         return __builtin_bit_cast(e_h8, __builtin_amdgcn_raw_buffer_load_b128(rs, off(chunk, mb, tap, plane, lane), 0, 0));
     }
+    // ring image (F32): the same slots carry floats 0-3 (plane 0) and 4-7 (plane 1)
+    __device__ static e_f32x8 f32(const e_h8& p0, const e_h8& p1) {
+        const e_f32x4 u = __builtin_bit_cast(e_f32x4, p0), v = __builtin_bit_cast(e_f32x4, p1);
+        return e_f32x8{u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
+    }
 };
 
 // Diagnostic stage cut (tools/probes/edge_probe.hip builds with -DRAVE_EDGE_STOP=n;
@@ -125,6 +143,7 @@ __host__ __device__ constexpr int e_xi(int i) { return i + 8 * (i >> 7); }   // 
 constexpr int kHXP = e_xi(kHXS) + 8;                // halves per window plane
 constexpr int kHeadLds = (2 * 16 * kEdgeFP + 2 * kHXP + 2 * kHBR * kHBP) * 2 + 4 * kEdgeWaves * 4 + 16;
 
+template <bool F32>
 __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a, EdgeGeo geo) {
     const int tiles = geo.tiles;
     extern __shared__ __attribute__((aligned(16))) char e_smem[];
@@ -135,6 +154,10 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     _Float16* bh = xl + kHXP;                                      // [kHBR][kHBP]
     _Float16* bl = bh + kHBR * kHBP;
     float* red = reinterpret_cast<float*>(bl + kHBR * kHBP);
+    // F32: one fp32 plane in the bytes of each (hi, lo) pair
+    float* ff = reinterpret_cast<float*>(fh);                     // [16][kEdgeFP]
+    float* xf = reinterpret_cast<float*>(xh);                     // [kHXP] flat, padded
+    float* bf = reinterpret_cast<float*>(bh);                     // [kHBR][kHBP]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nmain = tiles * a.batch;
@@ -181,17 +204,25 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
 #pragma unroll
     for (int it = 0; it < XT; ++it) {
         const int i = tid + it * kEdgeNT;
-        if (i < kHXS) e_split(xv[it], xh[e_xi(i)], xl[e_xi(i)]);
+        if (i < kHXS) {
+            if constexpr (F32) xf[e_xi(i)] = xv[it];
+            else e_split(xv[it], xh[e_xi(i)], xl[e_xi(i)]);
+        }
     }
-    vote_cast(vote, wave, xmax);
+    if constexpr (!F32) vote_cast(vote, wave, xmax);
     // band-plane channels 8..15 stay zero (the conv chunk is 16 channels wide)
     for (int i = tid; i < kHBR; i += kEdgeNT) {
-        *reinterpret_cast<e_h8*>(bh + i * kHBP + 8) = e_h8{0, 0, 0, 0, 0, 0, 0, 0};
-        *reinterpret_cast<e_h8*>(bl + i * kHBP + 8) = e_h8{0, 0, 0, 0, 0, 0, 0, 0};
+        if constexpr (F32) {
+            *reinterpret_cast<e_f32x4*>(bf + i * kHBP + 8) = e_f32x4{0.f, 0.f, 0.f, 0.f};
+            *reinterpret_cast<e_f32x4*>(bf + i * kHBP + 12) = e_f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+            *reinterpret_cast<e_h8*>(bh + i * kHBP + 8) = e_h8{0, 0, 0, 0, 0, 0, 0, 0};
+            *reinterpret_cast<e_h8*>(bl + i * kHBP + 8) = e_h8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
     }
     __syncthreads();
     float xs = 1.f;
-    if (__builtin_expect(vote_any<kEdgeWaves>(vote), 0)) {
+    if (!F32 && __builtin_expect(vote_any<kEdgeWaves>(vote), 0)) {
         // rare: audio at 2^15 or beyond -- the window again as x 2^-s
         xs = ldexpf(1.f, -__builtin_amdgcn_readfirstlane(split_shift(block_max<kEdgeWaves>(xmax, red))));
 #pragma unroll
@@ -208,6 +239,20 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     // three independent accumulator chains (one per product), summed at the end
     auto analysis_block = [&](int blk, e_f32x4& acc) __attribute__((always_inline)) {
         e_f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0;
+        if constexpr (F32) {
+#pragma unroll
+            for (int s = 0; s < kEdgeKW / 32; ++s) {
+                const e_f32x8 af = e_ld8(ff + col * kEdgeFP + 32 * s + 8 * g);
+                const e_f32x8 xf8 = e_ld8(xf + e_xi(512 * blk + 32 * col + 32 * s + 8 * g));
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[e], xf8[e], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[e + 1], xf8[e + 1], c1, 0, 0, 0);
+                }
+            }
+            acc = c0 + c1;
+            return;
+        }
 #pragma unroll
         for (int s = 0; s < kEdgeKW / 32; ++s) {
             const int ka = col * kEdgeFP + 32 * s + 8 * g;
@@ -250,6 +295,10 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     }
     auto put_bands = [&](int blk, const e_f32x4& v, float bs) __attribute__((always_inline)) {
         const int row = 32 * blk + 2 * col + (g >> 1);
+        if constexpr (F32) {
+            *reinterpret_cast<e_f32x4*>(bf + row * kHBP + 4 * (g & 1)) = v;
+            return;
+        }
         e_h4 hv4, lv4;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -274,10 +323,10 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     // band planes split optimistically, with a range vote (rare: a rescale by 2^-s)
     put_bands(wave, v0, 1.f);
     if (extra) put_bands(wave + kEdgeWaves, v1, 1.f);
-    vote_cast(vote + 8, wave, bmax);
+    if constexpr (!F32) vote_cast(vote + 8, wave, bmax);
     __syncthreads();
     float bs = 1.f;
-    if (__builtin_expect(vote_any<kEdgeWaves>(vote + 8), 0)) {
+    if (!F32 && __builtin_expect(vote_any<kEdgeWaves>(vote + 8), 0)) {
         bs = ldexpf(1.f, -__builtin_amdgcn_readfirstlane(split_shift(block_max<kEdgeWaves>(bmax, red))));
         put_bands(wave, v0, bs);
         if (extra) put_bands(wave + kEdgeWaves, v1, bs);
@@ -295,6 +344,17 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
 #pragma unroll
     for (int q = 0; q < kEdgeK7; ++q) {
         const int row = 32 * wave + l32 + q;
+        if constexpr (F32) {
+            const e_f32x8 x8 = e_ld8(bf + row * kHBP + 8 * h);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (j >= MB) break;
+                const e_f32x8 w8 = EdgeW::f32(wr[q][j][0], wr[q][j][1]);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(x8[e], w8[e], acc[j], 0, 0, 0);
+            }
+            continue;
+        }
         const e_h8 xh8 = *reinterpret_cast<const e_h8*>(bh + row * kHBP + 8 * h);
         const e_h8 xl8 = *reinterpret_cast<const e_h8*>(bl + row * kHBP + 8 * h);
 #pragma unroll
@@ -352,7 +412,7 @@ constexpr int kTPlane = 2 * kTXR * kTXP;            // halves of the two act(x) 
 static_assert(2 * kTSW * kTSP <= kTPlane, "synthesis planes reuse the act(x) planes");
 constexpr int kTailLds = (2 * 16 * kEdgeFP + kTPlane) * 2 + 2 * kEdgeWaves * 4 + 16;
 
-template <bool SNAKE, bool AM>
+template <bool SNAKE, bool AM, bool F32>
 __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a, EdgeGeo geo) {
     const int tiles = geo.tiles;
     extern __shared__ __attribute__((aligned(16))) char e_smem[];
@@ -363,6 +423,9 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
     _Float16* sh = xh;                                             // [kTSW][kTSP] (after the conv)
     _Float16* sl = xh + kTSW * kTSP;
     float* red = reinterpret_cast<float*>(xh + kTPlane);
+    float* ff = reinterpret_cast<float*>(fh);                     // F32: [16][kEdgeFP]
+    float* xf = reinterpret_cast<float*>(xh);                     // F32: [kTXR][kTXP] act(x)
+    float* sf = xf;                                                // F32: [kTSW][kTSP] (after the conv)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nmain = tiles * a.batch;
@@ -426,6 +489,10 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
             if (i < NG * kTXR) {
                 const int cg = i / kTXR, w = i - cg * kTXR;
                 const e_f32x4 v = xv[it] * xs;
+                if constexpr (F32) {
+                    *reinterpret_cast<e_f32x4*>(xf + w * kTXP + 4 * cg) = v;
+                    continue;
+                }
                 const e_h4 hi = __builtin_convertvector(v, e_h4);
                 const e_h4 lo = __builtin_convertvector((v - __builtin_convertvector(hi, e_f32x4)) * 2048.0f, e_h4);
                 *reinterpret_cast<e_h4*>(xh + w * kTXP + 4 * cg) = hi;
@@ -434,10 +501,10 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
         }
     };
     put_x(1.f);
-    vote_cast(vote, wave, xmax);
+    if constexpr (!F32) vote_cast(vote, wave, xmax);
     __syncthreads();
     float xs = 1.f;
-    if (__builtin_expect(vote_any<kEdgeWaves>(vote), 0)) {
+    if (!F32 && __builtin_expect(vote_any<kEdgeWaves>(vote), 0)) {
         // rare: act(x) at 2^15 or beyond -- the window again as act(x) 2^-s
         xs = ldexpf(1.f, -__builtin_amdgcn_readfirstlane(split_shift(block_max<kEdgeWaves>(xmax, red))));
         put_x(xs);
@@ -458,6 +525,16 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
     const int xblk = kEdgeWaves + (wave >> 2), xchunk = wave & 3;
     auto mfma3 = [&](int row, int ch, const e_h8& b2, const e_h8& bh8, const e_h8& bl8, e_f32x16& c0,
                      e_f32x16& c1) __attribute__((always_inline)) {
+        if constexpr (F32) {
+            const e_f32x8 x8 = e_ld8(xf + row * kTXP + 16 * ch + 8 * h);
+            const e_f32x8 w8 = EdgeW::f32(bh8, bl8);
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+                c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x8[e], w8[e], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x8[e + 1], w8[e + 1], c1, 0, 0, 0);
+            }
+            return;
+        }
         const e_h8 xh8 = *reinterpret_cast<const e_h8*>(xh + row * kTXP + 16 * ch + 8 * h);
         const e_h8 xl8 = *reinterpret_cast<const e_h8*>(xl + row * kTXP + 16 * ch + 8 * h);
         c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh8, b2, c0, 0, 0, 0);
@@ -530,7 +607,10 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
             // tanh(x) = 1 - 2 / (e^2x + 1): saturates to +-1 through inf / 0
             out = 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * out) + 1.0f);
             if ((c_out & 1) && !(f & 1)) out = -out;
-            if (w < kTSW) e_split(ok ? out : 0.f, sh[w * kTSP + c_out], sl[w * kTSP + c_out]);
+            if (w < kTSW) {
+                if constexpr (F32) sf[w * kTSP + c_out] = ok ? out : 0.f;
+                else e_split(ok ? out : 0.f, sh[w * kTSP + c_out], sl[w * kTSP + c_out]);
+            }
         }
     };
     put_block(wave, acc);
@@ -548,10 +628,23 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
 #pragma unroll
     for (int s = 0; s < kEdgeKW / 32; ++s) {
         const int ka = col * kEdgeFP + 32 * s + 8 * g;
+        const int tap = 2 * s + (g >> 1);
+        if constexpr (F32) {
+            const e_f32x8 af = e_ld8(ff + ka);
+#pragma unroll
+            for (int q = 0; q < BLK; ++q) {
+                const e_f32x8 b8 = e_ld8(sf + (fb + 16 * q + col + tap) * kTSP + 8 * (g & 1));
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {
+                    sacc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[e], b8[e], sacc[q], 0, 0, 0);
+                    sac1[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[e + 1], b8[e + 1], sac1[q], 0, 0, 0);
+                }
+            }
+            continue;
+        }
         const e_h8 ah = *reinterpret_cast<const e_h8*>(fh + ka);
         const e_h8 al = *reinterpret_cast<const e_h8*>(fl + ka);
         const e_h8 a2 = ah * (_Float16)2048.0f;
-        const int tap = 2 * s + (g >> 1);
 #pragma unroll
         for (int q = 0; q < BLK; ++q) {
             const int xi = (fb + 16 * q + col + tap) * kTSP + 8 * (g & 1);
@@ -612,9 +705,17 @@ static int edge_row_exponent(double amax) {   // max |h 2^e| in [8, 16)
     return e;
 }
 
-// A[r][k] (16 rows x kEdgeKW, zero beyond) -> hi / lo planes + 2^-(e + 11)
+// A[r][k] (16 rows x kEdgeKW, zero beyond) -> hi / lo planes + 2^-(e + 11);
+// f32: one fp32 plane [16][kEdgeFP] in the same bytes, then 1
 template <typename Fn>
-static void edge_filter_image(Fn&& A, float* image) {
+static void edge_filter_image(Fn&& A, float* image, bool f32) {
+    if (f32) {
+        for (int r = 0; r < 16; ++r)
+            for (int k = 0; k < kEdgeFP; ++k) image[r * kEdgeFP + k] = k < kEdgeKW ? A(r, k) : 0.f;
+        image[kEdgeFilterHalves / 2] = 1.f;
+        for (int i = kEdgeFilterHalves / 2 + 1; i < kEdgeFilterFloats; ++i) image[i] = 0.f;
+        return;
+    }
     double amax = 0.0;
     for (int r = 0; r < 16; ++r)
         for (int k = 0; k < kEdgeKW; ++k) amax = std::max(amax, std::fabs((double)A(r, k)));
@@ -632,7 +733,7 @@ static void edge_filter_image(Fn&& A, float* image) {
     for (int i = kEdgeFilterHalves / 2 + 1; i < kEdgeFilterFloats; ++i) image[i] = 0.f;
 }
 
-extern "C" int rave_encoder_head_pack_filter(const float* hkf, int n_band, int taps, int n_out_bands, float* image) {
+static int head_pack(const float* hkf, int n_band, int taps, int n_out_bands, float* image, bool f32) {
     RAVE_CHECK_ARG(hkf && image, "encoder_head_pack_filter: null pointer");
     if (n_band != 16 || taps != kAnaTapsE || n_out_bands < 1 || n_out_bands > 8) {
         set_error("encoder_head_pack_filter: built for 16 bands, 513 taps, <= 8 output bands");
@@ -642,11 +743,18 @@ extern "C" int rave_encoder_head_pack_filter(const float* hkf, int n_band, int t
     edge_filter_image([&](int r, int j) -> float {
         const int p = r >> 3, k = r & 7, jj = j - 16 * p;
         return (k < n_out_bands && jj >= 0 && jj < taps) ? hkf[(int64_t)k * taps + jj] : 0.f;
-    }, image);
+    }, image, f32);
     return RAVE_OK;
 }
+extern "C" int rave_encoder_head_pack_filter(const float* hkf, int n_band, int taps, int n_out_bands, float* image) {
+    return head_pack(hkf, n_band, taps, n_out_bands, image, false);
+}
+extern "C" int rave_encoder_head_pack_filter_f32(const float* hkf, int n_band, int taps, int n_out_bands,
+                                                 float* image) {
+    return head_pack(hkf, n_band, taps, n_out_bands, image, true);
+}
 
-extern "C" int rave_decoder_tail_pack_filter(const float* hki, int n_band, int taps, float* image) {
+static int tail_pack(const float* hki, int n_band, int taps, float* image, bool f32) {
     RAVE_CHECK_ARG(hki && image, "decoder_tail_pack_filter: null pointer");
     if (n_band != 16 || taps != kSynTapsE) {
         set_error("decoder_tail_pack_filter: built for 16 bands, 33 taps");
@@ -656,7 +764,23 @@ extern "C" int rave_decoder_tail_pack_filter(const float* hki, int n_band, int t
     edge_filter_image([&](int m, int k) -> float {
         const int tap = k >> 4, c = k & 15;
         return tap < taps ? hki[((int64_t)m * n_band + c) * taps + tap] : 0.f;
-    }, image);
+    }, image, f32);
+    return RAVE_OK;
+}
+extern "C" int rave_decoder_tail_pack_filter(const float* hki, int n_band, int taps, float* image) {
+    return tail_pack(hki, n_band, taps, image, false);
+}
+extern "C" int rave_decoder_tail_pack_filter_f32(const float* hki, int n_band, int taps, float* image) {
+    return tail_pack(hki, n_band, taps, image, true);
+}
+
+// rave_edge_args.precision: 0 / RAVE_PREC_SPLIT16 (split-f16) or RAVE_PREC_F32_RING (exact fp32)
+static int edge_prec(const rave_edge_args& a, bool& f32) {
+    f32 = a.precision == RAVE_PREC_F32_RING;
+    if (a.precision != 0 && a.precision != RAVE_PREC_SPLIT16 && !f32) {
+        set_error("edges: precision must be RAVE_PREC_SPLIT16 or RAVE_PREC_F32_RING");
+        return RAVE_ERR_ARG;
+    }
     return RAVE_OK;
 }
 
@@ -671,12 +795,16 @@ extern "C" int rave_encoder_head(const rave_edge_args* p, void* stream) {
     }
     RAVE_CHECK_ARG(a.fill_channels == 0 || (a.fill_y && a.fill_values && a.fill_t > 0),
                    "encoder_head: fill needs fill_y, fill_values and fill_t");
+    bool f32;
+    int rc = edge_prec(a, f32);
+    if (rc != RAVE_OK) return rc;
     const EdgeGeo g = edge_geometry(a, kHF);
-    static bool attr = false;
-    const int rc = edge_lds_attr(encoder_head_kernel, kHeadLds, attr);
+    static bool attr[2] = {false, false};
+    auto kern = f32 ? encoder_head_kernel<true> : encoder_head_kernel<false>;
+    rc = edge_lds_attr(kern, kHeadLds, attr[f32]);
     if (rc != RAVE_OK) return rc;
     const int grid = g.tiles * a.batch;
-    launch(encoder_head_kernel, dim3(grid), dim3(kEdgeNT), (uint32_t)kHeadLds, as_stream(stream), a, g);
+    launch(kern, dim3(grid), dim3(kEdgeNT), (uint32_t)kHeadLds, as_stream(stream), a, g);
     return launch_status("encoder_head_kernel");
 }
 
@@ -695,13 +823,20 @@ extern "C" int rave_decoder_tail(const rave_edge_args* p, void* stream) {
                    "decoder_tail: act must be RAVE_ACT_LEAKY or RAVE_ACT_SNAKE (with alpha)");
     RAVE_CHECK_ARG(reinterpret_cast<uintptr_t>(a.y) % 16 == 0 && a.y_sb % 4 == 0,
                    "decoder_tail: output must be 16-byte aligned");
+    bool f32;
+    int rc = edge_prec(a, f32);
+    if (rc != RAVE_OK) return rc;
     const EdgeGeo g = edge_geometry(a, kTF);
     const dim3 grid(g.tiles * a.batch);
     const bool snake = a.act == RAVE_ACT_SNAKE, am = a.mode == 1;
-    auto kern = snake ? (am ? decoder_tail_kernel<true, true> : decoder_tail_kernel<true, false>)
-                      : (am ? decoder_tail_kernel<false, true> : decoder_tail_kernel<false, false>);
-    static bool attr[4] = {false, false, false, false};
-    const int rc = edge_lds_attr(kern, kTailLds, attr[2 * snake + am]);
+    auto pick = [&](auto f32t) {
+        constexpr bool FF = decltype(f32t)::value != 0;
+        return snake ? (am ? decoder_tail_kernel<true, true, FF> : decoder_tail_kernel<true, false, FF>)
+                     : (am ? decoder_tail_kernel<false, true, FF> : decoder_tail_kernel<false, false, FF>);
+    };
+    auto kern = f32 ? pick(EdgeN<1>{}) : pick(EdgeN<0>{});
+    static bool attr[8] = {false, false, false, false, false, false, false, false};
+    rc = edge_lds_attr(kern, kTailLds, attr[4 * f32 + 2 * snake + am]);
     if (rc != RAVE_OK) return rc;
     launch(kern, grid, dim3(kEdgeNT), (uint32_t)kTailLds, as_stream(stream), a, g);
     return launch_status("decoder_tail_kernel");

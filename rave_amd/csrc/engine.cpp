@@ -332,6 +332,13 @@ struct Model {
     std::set<std::string> unit_ok;     // k=3 names of units with a fused pack in some arithmetic
     int64_t hkf_off = 0, hki_off = 0, spk_off = 0, cb_off = -1;
     int64_t head_filt_off = -1, tail_filt_off = -1;   // rave_*_pack_filter images (-1: shape unsupported)
+    int64_t head_filt32_off = -1, tail_filt32_off = -1;   // exact-fp32 images (*_pack_filter_f32)
+    // the edges' arithmetic: split16 where the model has it, else the exact-fp32 ring (-1: none)
+    int edge_prec() const {
+        if (std::find(precs.begin(), precs.end(), RAVE_PREC_SPLIT16) != precs.end()) return RAVE_PREC_SPLIT16;
+        if (std::find(precs.begin(), precs.end(), RAVE_PREC_F32_RING) != precs.end()) return RAVE_PREC_F32_RING;
+        return -1;
+    }
     int taps_a = 0, taps_s = 0;
     // AdaIN buffers (rave/blocks.py:858-868), device
     int max_batch = 64;
@@ -1165,14 +1172,16 @@ static bool edges_enabled() {
 }
 
 bool Model::use_head(int B, int T) {
-    if (!edges_enabled() || head_filt_off < 0) return false;
+    const int ep = edge_prec();
+    const int64_t filt = ep == RAVE_PREC_F32_RING ? head_filt32_off : head_filt_off;
+    if (!edges_enabled() || ep < 0 || filt < 0) return false;
     const Node& n = g.encoder.front();
     const int F = T / cfg.n_band;
-    if (std::find(precs.begin(), precs.end(), RAVE_PREC_SPLIT16) == precs.end()) return false;
+    if (!w_pack.count({n.name, ep})) return false;
     if (cfg.n_band != 16 || n.kernel != 7 || n.stride != 1 || n.dilation != 1 || n.act != RAVE_ACT_NONE ||
         n.transposed || n.c_in > 8 || n.c_out > 64 || !n.adain.empty() || F * cfg.n_band != T)
         return false;
-    const std::string key = key_of({"head", std::to_string(B), std::to_string(T)});
+    const std::string key = key_of({"head", std::to_string(ep), std::to_string(B), std::to_string(T)});
     if (!tuned.count(key)) {
         rave_edge_args a = head_desc(B, F);
         const int64_t nx = (int64_t)B * T, ny = (int64_t)B * n.c_out * F, nb = (int64_t)B * n.c_in * F;
@@ -1182,9 +1191,10 @@ bool Model::use_head(int B, int T) {
         a.y = sc + nx + 64;
         a.y_sb = (int64_t)n.c_out * F;
         a.y_sc = F;
-        a.weight = aptr(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
+        a.weight = aptr(w_pack.at({n.name, ep}));
         a.bias = n.bias ? aptr(bias_off.at(n.name)) : nullptr;
-        a.filter = aptr(head_filt_off);
+        a.filter = aptr(filt);
+        a.precision = ep;
         const double fused = time_native([&](hipStream_t st) { return rave_encoder_head(&a, st); });
         double split = 1e30;
         if (precs.size() == 1) {
@@ -1207,6 +1217,7 @@ bool Model::use_head(int B, int T) {
             q.hkf = aptr(hkf_off);
             double ta = 1e30;
             for (int pr : {RAVE_PREC_F32, RAVE_PREC_SPLIT16}) {
+                if (pr == RAVE_PREC_SPLIT16 && ep != RAVE_PREC_SPLIT16) continue;   // the exact model's own ops
                 q.precision = pr;
                 const double ms = time_native([&](hipStream_t st) { return rave_pqmf_analysis(&q, st); });
                 if (ms >= 0) ta = std::min(ta, ms);
@@ -1236,11 +1247,13 @@ void Model::head_op(Plan& p, int B, int T, const View& x, const View& y, const V
         a.f_sb = fill_z->sb;
         a.f_sc = fill_z->sc;
     }
+    const int ep = edge_prec();
+    a.precision = ep;
     PlanOp& o = p.add(RAVE_OP_HEAD, a, "encoder_head:pqmf_analysis+" + n.name);
     rave_edge_args& A = *reinterpret_cast<rave_edge_args*>(o.op.u.raw);
-    View wv = arena_view(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
+    View wv = arena_view(w_pack.at({n.name, ep}));
     View bv = n.bias ? arena_view(bias_off.at(n.name)) : View{};
-    View hv = arena_view(head_filt_off);
+    View hv = arena_view(ep == RAVE_PREC_F32_RING ? head_filt32_off : head_filt_off);
     View sv = arena_view(spk_off);
     p.bind(o, A, A.x, &x);
     p.bind(o, A, A.y, &y);
@@ -1249,20 +1262,22 @@ void Model::head_op(Plan& p, int B, int T, const View& x, const View& y, const V
     p.bind(o, A, A.filter, &hv);
     p.bind(o, A, A.fill_y, a.fill_channels ? fill_z : nullptr);
     p.bind(o, A, A.fill_values, a.fill_channels ? &sv : nullptr);
-    o.prec = RAVE_PREC_SPLIT16;
+    o.prec = ep;
     o.flops = 2.0 * B * F * ((double)n.c_in * taps_a + (double)n.c_out * n.c_in * n.kernel);
     o.bytes = 4.0 * ((double)B * T + (double)B * n.c_out * F);
 }
 
 bool Model::use_tail(int B, int F) {
-    if (!edges_enabled() || tail_filt_off < 0) return false;
+    const int ep = edge_prec();
+    const int64_t filt = ep == RAVE_PREC_F32_RING ? tail_filt32_off : tail_filt_off;
+    if (!edges_enabled() || ep < 0 || filt < 0) return false;
     const Node& n = g.decoder.back();
-    if (std::find(precs.begin(), precs.end(), RAVE_PREC_SPLIT16) == precs.end()) return false;
+    if (!w_pack.count({n.name, ep})) return false;
     const int c_want = cfg.amplitude_modulation ? 2 * cfg.n_band : cfg.n_band;
     if (cfg.n_band != 16 || n.kernel != 7 || n.stride != 1 || n.dilation != 1 || n.transposed || n.c_in != 64 ||
         n.c_out != c_want || (n.act != RAVE_ACT_LEAKY && n.act != RAVE_ACT_SNAKE) || !n.adain.empty())
         return false;
-    const std::string key = key_of({"tail", std::to_string(B), std::to_string(F)});
+    const std::string key = key_of({"tail", std::to_string(ep), std::to_string(B), std::to_string(F)});
     if (!tuned.count(key)) {
         rave_edge_args a = tail_desc(B, F);
         const int64_t nx = (int64_t)B * n.c_in * F, nw = (int64_t)B * n.c_out * F, ny = (int64_t)B * F * cfg.n_band;
@@ -1272,10 +1287,11 @@ bool Model::use_tail(int B, int F) {
         a.x_sc = F;
         a.y = sc + ((nx + nw + 63) / 64 + 1) * 64;     // 16-byte aligned
         a.y_sb = (int64_t)F * cfg.n_band;
-        a.weight = aptr(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
+        a.weight = aptr(w_pack.at({n.name, ep}));
         a.bias = n.bias ? aptr(bias_off.at(n.name)) : nullptr;
         a.alpha = n.act == RAVE_ACT_SNAKE ? aptr(alpha_off.at(n.alpha)) : nullptr;
-        a.filter = aptr(tail_filt_off);
+        a.filter = aptr(filt);
+        a.precision = ep;
         const double fused = time_native([&](hipStream_t st) { return rave_decoder_tail(&a, st); });
         double split = 1e30;
         if (precs.size() == 1) {
@@ -1296,6 +1312,7 @@ bool Model::use_tail(int B, int F) {
             q.hki = aptr(hki_off);
             double ts = 1e30;
             for (int pr : {RAVE_PREC_F32, RAVE_PREC_SPLIT16}) {
+                if (pr == RAVE_PREC_SPLIT16 && ep != RAVE_PREC_SPLIT16) continue;   // the exact model's own ops
                 q.precision = pr;
                 const double ms = time_native([&](hipStream_t st) { return rave_pqmf_synthesis(&q, st); });
                 if (ms >= 0) ts = std::min(ts, ms);
@@ -1320,12 +1337,14 @@ void Model::tail_op(Plan& p, int B, int F, const View& x, const View& y, const V
     a.y_sb = y.sb;
     a.n_sb = noise ? noise->sb : 0;
     a.n_sc = noise ? noise->sc : 0;
+    const int ep = edge_prec();
+    a.precision = ep;
     PlanOp& o = p.add(RAVE_OP_TAIL, a, "decoder_tail:" + n.name + "+pqmf_synthesis");
     rave_edge_args& A = *reinterpret_cast<rave_edge_args*>(o.op.u.raw);
-    View wv = arena_view(w_pack.at({n.name, RAVE_PREC_SPLIT16}));
+    View wv = arena_view(w_pack.at({n.name, ep}));
     View bv = n.bias ? arena_view(bias_off.at(n.name)) : View{};
     View av = n.act == RAVE_ACT_SNAKE ? arena_view(alpha_off.at(n.alpha)) : View{};
-    View hv = arena_view(tail_filt_off);
+    View hv = arena_view(ep == RAVE_PREC_F32_RING ? tail_filt32_off : tail_filt_off);
     p.bind(o, A, A.x, &x);
     p.bind(o, A, A.y, &y);
     p.bind(o, A, A.weight, &wv);
@@ -1333,7 +1352,7 @@ void Model::tail_op(Plan& p, int B, int F, const View& x, const View& y, const V
     p.bind(o, A, A.alpha, n.act == RAVE_ACT_SNAKE ? &av : nullptr);
     p.bind(o, A, A.filter, &hv);
     p.bind(o, A, A.noise, noise);
-    o.prec = RAVE_PREC_SPLIT16;
+    o.prec = ep;
     o.flops = 2.0 * B * F * ((double)n.c_out * n.c_in * n.kernel + (double)cfg.n_band * cfg.n_band * taps_s);
     o.bytes = 4.0 * ((double)B * n.c_in * F + (double)B * F * cfg.n_band + (noise ? (double)B * cfg.n_band * F : 0.0));
 }
@@ -1672,6 +1691,10 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
             m->head_filt_off = m->add(img);
         if (rave_decoder_tail_pack_filter(hki.data(), nb, m->taps_s, img.data()) == RAVE_OK)
             m->tail_filt_off = m->add(img);
+        if (rave_encoder_head_pack_filter_f32(hkf.data(), nb, m->taps_a, cfg.enc_bands, img.data()) == RAVE_OK)
+            m->head_filt32_off = m->add(img);
+        if (rave_decoder_tail_pack_filter_f32(hki.data(), nb, m->taps_s, img.data()) == RAVE_OK)
+            m->tail_filt32_off = m->add(img);
     }
     m->spk_off = cfg.speaker_size > 0 ? m->add(speaker, cfg.speaker_size) : 0;
     if (cfg.rvq_quantizers > 0) {

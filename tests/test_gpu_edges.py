@@ -9,7 +9,9 @@ against the separate ops they replace.
 
 Tolerances: layer outputs 2e-5 relative to max|ref| (as the single-layer tests);
 model outputs 1e-4 max-abs (north star).  Ragged lengths (frames not a
-multiple of the 256-frame tiles) and both padding modes are covered."""
+multiple of the 256-frame tiles) and both padding modes are covered, in both
+arithmetics: split-f16 and exact fp32 (precision RAVE_PREC_F32_RING: the
+ring weight image and the fp32 filter image)."""
 import ctypes as C
 
 import numpy as np
@@ -47,9 +49,10 @@ def _filters(golden):
     return pqmf_filters(hk)
 
 
+@pytest.mark.parametrize("prec", ["split16", "f32_ring"])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("F,B,scale", [(600, 2, 1.0), (4096, 3, 1.0), (257, 1, 3e6)])
-def test_encoder_head(N, dev, golden, causal, F, B, scale):
+def test_encoder_head(N, dev, golden, causal, F, B, scale, prec):
     from oracle.rave_oracle import conv1d, get_padding, reverse_half
     hkf, _ = _filters(golden)
     rng = np.random.default_rng(F + 7 * causal)
@@ -62,20 +65,21 @@ def test_encoder_head(N, dev, golden, causal, F, B, scale):
                                 pad=get_padding(hkf.shape[-1], causal=causal)))[:, :nb]
     cpad = get_padding(k, causal=causal)
     ref = conv1d(bands, w.astype(np.float64), b.astype(np.float64), pad=cpad)
-    packed = torch.from_numpy(N.pack_conv_weight(w, nb, co, k, 1, 1, 0, precision=N.PREC_SPLIT16)).to(dev)
+    P = N.PRECISION[prec]
+    packed = torch.from_numpy(N.pack_conv_weight(w, nb, co, k, 1, 1, 0, precision=P)).to(dev)
     xd = torch.from_numpy(x).to(dev)
     y = torch.full((B, co, F), float("nan"), device=dev)
     spk = torch.from_numpy(rng.standard_normal(256).astype(np.float32)).to(dev)
     Fz = max(1, F // 64)
     z = torch.full((B, 320, Fz), float("nan"), device=dev)
-    hd = torch.from_numpy(N.pack_edge_filter(hkf, head=True, n_out_bands=nb)).to(dev)
+    hd = torch.from_numpy(N.pack_edge_filter(hkf, head=True, n_out_bands=nb, f32=P == N.PREC_F32_RING)).to(dev)
     bd = torch.from_numpy(b).to(dev)
     a = N.EdgeArgs(batch=B, frames=F, conv_c_in=nb, conv_c_out=co, conv_kernel=k, conv_pad_left=cpad[0],
                    pqmf_taps=hkf.shape[-1], pqmf_pad_left=get_padding(hkf.shape[-1], causal=causal)[0],
                    x=xd.data_ptr(), x_sb=T, y=y.data_ptr(), y_sb=co * F, y_sc=F,
                    weight=packed.data_ptr(), bias=bd.data_ptr(), filter=hd.data_ptr(),
                    fill_channels=256, fill_t=Fz, fill_y=z[:, 64:].data_ptr(), f_sb=320 * Fz, f_sc=Fz,
-                   fill_values=spk.data_ptr())
+                   fill_values=spk.data_ptr(), precision=P)
     N.check(N.lib.rave_encoder_head(C.byref(a), _st()), "encoder_head")
     torch.cuda.synchronize()
     got = y.cpu().numpy()
@@ -87,10 +91,11 @@ def test_encoder_head(N, dev, golden, causal, F, B, scale):
     assert np.isnan(zz[:, :64]).all()            # the latent rows are the encoder's, untouched
 
 
+@pytest.mark.parametrize("prec", ["split16", "f32_ring"])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("am,act,noise", [(True, "leaky", False), (False, "snake", True), (True, "snake", True)])
 @pytest.mark.parametrize("F,B", [(600, 2), (4096, 2), (100, 1)])
-def test_decoder_tail(N, dev, golden, causal, am, act, noise, F, B):
+def test_decoder_tail(N, dev, golden, causal, am, act, noise, F, B, prec):
     from oracle.rave_oracle import conv1d, get_padding, leaky_relu, reverse_half, snake
     _, hki = _filters(golden)
     rng = np.random.default_rng(F + 3 * am + 5 * causal)
@@ -111,17 +116,18 @@ def test_decoder_tail(N, dev, golden, causal, am, act, noise, F, B):
     spad = get_padding(hki.shape[-1], causal=causal)
     ys = conv1d(reverse_half(wv), hki.astype(np.float64), None, pad=spad) * 16
     ref = ys[:, ::-1, :].transpose(0, 2, 1).reshape(B, 1, F * 16)
-    packed = torch.from_numpy(N.pack_conv_weight(w, ci, co, k, 1, 1, 0, precision=N.PREC_SPLIT16)).to(dev)
+    P = N.PRECISION[prec]
+    packed = torch.from_numpy(N.pack_conv_weight(w, ci, co, k, 1, 1, 0, precision=P)).to(dev)
     xd = torch.from_numpy(x).to(dev)
     y = torch.full((B, 1, 16 * F), float("nan"), device=dev)
     bd, ad = (torch.from_numpy(v).to(dev) for v in (b, alpha))
-    hd = torch.from_numpy(N.pack_edge_filter(hki, head=False)).to(dev)
+    hd = torch.from_numpy(N.pack_edge_filter(hki, head=False, f32=P == N.PREC_F32_RING)).to(dev)
     nd = torch.from_numpy(nz).to(dev) if noise else None
     a = N.EdgeArgs(batch=B, frames=F, conv_c_in=ci, conv_c_out=co, conv_kernel=k, conv_pad_left=cpad[0],
                    pqmf_taps=hki.shape[-1], pqmf_pad_left=spad[0], mode=1 if am else 2, act=N.ACT[act],
                    leaky_slope=0.2, x=xd.data_ptr(), x_sb=ci * F, x_sc=F, y=y.data_ptr(), y_sb=16 * F,
                    weight=packed.data_ptr(), bias=bd.data_ptr(), alpha=ad.data_ptr(), filter=hd.data_ptr(),
-                   noise=nd.data_ptr() if noise else None, n_sb=16 * F, n_sc=F)
+                   noise=nd.data_ptr() if noise else None, n_sb=16 * F, n_sc=F, precision=P)
     N.check(N.lib.rave_decoder_tail(C.byref(a), _st()), "decoder_tail")
     torch.cuda.synchronize()
     got = y.cpu().numpy()
@@ -139,11 +145,13 @@ def test_edges_refuse_unsupported(N):
     assert N.lib.rave_encoder_head(C.byref(a), None) == N.RAVE_ERR_UNSUPPORTED     # > 8 bands
 
 
-@pytest.mark.parametrize("cfg_name", ["v2", "v3_noise"])
-def test_model_uses_edges_and_matches_oracle(dev, golden, cfg_name):
-    """A split16 model lays both fused edges into its plans, and its forward
-    matches the float64 oracle (the model golden tests cover auto / split16
-    against the reference fixtures)."""
+@pytest.mark.parametrize("cfg_name,precision", [("v2", "split16"), ("v3_noise", "split16"), ("v2", "f32_tuned"),
+                                                ("v3_noise", "f32_tuned")])
+def test_model_uses_edges_and_matches_oracle(dev, golden, cfg_name, precision):
+    """A split16 model lays both fused edges into its plans (an exact-fp32
+    f32_tuned model: where they time faster than the separate ops), and its
+    forward matches the float64 oracle (the model golden tests cover auto /
+    split16 against the reference fixtures)."""
     from oracle.rave_oracle import Oracle
     from rave_amd import _native as N
     from rave_amd import config as rcfg
@@ -152,13 +160,17 @@ def test_model_uses_edges_and_matches_oracle(dev, golden, cfg_name):
     cfg = rcfg.get_config(cfg_name)
     params = init_params(cfg, seed=3)
     spk = init_speaker(cfg, seed=3)
-    m = RAVE(cfg, params, spk, device=dev, hk=golden("pqmf")["hk"], precision="split16")
+    m = RAVE(cfg, params, spk, device=dev, hk=golden("pqmf")["hk"], precision=precision)
     B, T = 2, 16384
     Fz = T // cfg.hop
     kinds_e = [o["kind"] for o in m.ops(ENCODE, B, T)]
     kinds_d = [o["kind"] for o in m.ops(DECODE, B, Fz)]
-    assert N.OP_HEAD in kinds_e and N.OP_PQMF_ANALYSIS not in kinds_e and N.OP_FILL not in kinds_e
-    assert N.OP_TAIL in kinds_d and N.OP_PQMF_SYNTHESIS not in kinds_d
+    if precision == "split16":
+        assert N.OP_HEAD in kinds_e and N.OP_PQMF_ANALYSIS not in kinds_e and N.OP_FILL not in kinds_e
+        assert N.OP_TAIL in kinds_d and N.OP_PQMF_SYNTHESIS not in kinds_d
+    else:
+        assert (N.OP_HEAD in kinds_e) != (N.OP_PQMF_ANALYSIS in kinds_e)
+        assert (N.OP_TAIL in kinds_d) != (N.OP_PQMF_SYNTHESIS in kinds_d)
     rng = np.random.default_rng(4)
     x = (0.3 * np.sin(np.arange(T) * 2 * np.pi * 440 / 48000)[None, None]
          + 0.1 * rng.standard_normal((B, 1, T))).astype(np.float32)

@@ -28,7 +28,7 @@ from collections import defaultdict
 FAMILIES = {
     "conv_f32": (("conv1d_mfma_kernel", "conv1d_ring_f32_kernel"), ("conv1d_splitk_reduce_kernel",)),
     "conv_split16": (("conv1d_split_kernel",), ("split_reduce_kernel",)),
-    "unit_f32": (("residual_unit_kernel",), ()),
+    "unit_f32": (("residual_unit_kernel", "unit_ring_f32_kernel"), ()),
     "unit_split16": (("unit_split_kernel",), ()),
     "stack_split16": (("stack_split_kernel",), ()),
     "pqmf_analysis_f32": (("pqmf_analysis_kernel",), ()),
@@ -37,6 +37,8 @@ FAMILIES = {
     "pqmf_synthesis_split16": (("pqmf_synthesis_split_kernel",), ()),
     "head_split16": (("encoder_head_kernel",), ()),
     "tail_split16": (("decoder_tail_kernel",), ()),
+    "head_f32": ((), ()),
+    "tail_f32": ((), ()),
 }
 _KERNEL_FAMILY = {}
 for _fam, (_mains, _helpers) in FAMILIES.items():
@@ -51,6 +53,8 @@ def set_precision(precision: str) -> None:
     the fp32 ring convs (conv1d_ring_f32_kernel), not to a split16 family."""
     if precision in ("f32", "f32_tuned"):
         _KERNEL_FAMILY["split_reduce_kernel"] = ("conv_f32", False)
+        _KERNEL_FAMILY["encoder_head_kernel"] = ("head_f32", True)     # the edges' exact-fp32 form
+        _KERNEL_FAMILY["decoder_tail_kernel"] = ("tail_f32", True)
 
 
 _NAME = re.compile(r"(?:^|[\s:])([A-Za-z_][A-Za-z0-9_]*)\s*[<(]")
