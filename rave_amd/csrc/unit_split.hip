@@ -203,8 +203,13 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
                 ring[slot][i][p] = __builtin_bit_cast(us_h8, __builtin_amdgcn_raw_buffer_load_b128(
                     wrs, s < ST ? abase + (unsigned)(((i * ST + s) * 2 + p) * 1024) : kUSOOB, 0, 0));
     };
+    // (the 16-byte window path issues the ring's first fill after its window
+    // loads, so the window's wait does not include the weights)
+    auto prefetch_ring = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int t = 0; t < R; ++t) load_a(t, t * KG + kg);
+        for (int t = 0; t < R; ++t) load_a(t, t * KG + kg);
+    };
+    if (!a.xv) prefetch_ring();
 
     // ------------------------------------------------------------ per-row table -> LDS
     // every load in flight at once (a rolled loop waits out one round trip per
@@ -297,8 +302,12 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
                 rx[i][v] = __builtin_bit_cast(us_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                     xrs, ok ? (unsigned)((g * 8 + v) * a.x_sc + t) * 4u : kUSOOB, 0, 0));
         }
-        store_tab();
-        __syncthreads();                             // the per-row table (Snake alphas) is in LDS
+        prefetch_ring();
+        if constexpr (SNAKE) {
+            store_tab();
+            __syncthreads();                         // the per-row table (Snake alphas) is in LDS
+        }
+        if (RB == 1) US_STAMP(6);
 #pragma unroll
         for (int i = 0; i < XTV; ++i) {
             const int e = tid + i * NT;
@@ -328,6 +337,7 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
                 }
             }
         }
+        if constexpr (!SNAKE) store_tab();           // (published by the barrier after the staging)
         return cmax;
     };
     // range guard: when a wave saw |act0(x)| >= 2^15 the window is staged again
@@ -419,6 +429,15 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
             }
         }
     };
+    // execution order of the K-steps.  Cooperative form: phase 2 starts with the
+    // member's own channel block (its planes are ready before the hand-off) and
+    // wraps round; the weight ring follows the same order.
+    auto smap = [&](int t) __attribute__((always_inline)) {
+        if (RB == 1 || t < S1 || t >= ST) return t;   // (past ST: the ring's tail reads nothing)
+        int u = t - S1 + rb * (CG / RB);
+        if (u >= CG) u -= CG;
+        return S1 + u;
+    };
     auto step = [&](int t, int s, const BF& f, us_f32x16 (&acc)[MI][CB]) __attribute__((always_inline)) {
         us_h8 ah[MI], al[MI], a2[MI];
 #pragma unroll
@@ -427,7 +446,7 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
             al[i] = ring[t % R][i][1];
             a2[i] = ah[i] * (_Float16)2048.0f;
         }
-        load_a(t % R, s + R * KG);                   // refill the slot (runs on into W2)
+        load_a(t % R, RB > 1 ? smap(t + R) : s + R * KG);   // refill the slot (runs on into W2)
         if constexpr (F32) {
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf)
@@ -464,13 +483,14 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
         constexpr int GG = decltype(gtag)::value;
         constexpr int T0 = decltype(t0tag)::value, T1 = decltype(t1tag)::value;
         BF f[2];
-        read_b(T0 * KG + GG, f[0]);
+        auto sidx = [&](int t) __attribute__((always_inline)) { return RB > 1 ? smap(t) : t * KG + GG; };
+        read_b(sidx(T0), f[0]);
 #pragma unroll
         for (int t = T0; t < T1; ++t) {
-            if (t + 1 < T1) read_b((t + 1) * KG + GG, f[(t + 1 - T0) & 1]);
+            if (t + 1 < T1) read_b(sidx(t + 1), f[(t + 1 - T0) & 1]);
             __builtin_amdgcn_sched_barrier(0);
-            if (DA && ((t - T0) & 1)) step(t, t * KG + GG, f[(t - T0) & 1], accb);
-            else step(t, t * KG + GG, f[(t - T0) & 1], acc);
+            if (DA && ((t - T0) & 1)) step(t, sidx(t), f[(t - T0) & 1], accb);
+            else step(t, sidx(t), f[(t - T0) & 1], acc);
         }
     };
     // group 1 hands its partial sums to group 0 through LDS (over the dead planes)
@@ -571,8 +591,13 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // phase 2 over the member's own rows while the others finish publishing
+        constexpr int OWN = S1 + CG / RB;
+        zero_acc();
+        US_STAMP(3);
+        kloop(IC<0>{}, IC<S1>{}, IC<OWN>{});
         if (wave == 0) {
-            if (lane == 0) __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             unsigned spins = 0;
             bool ok = true;
             for (;;) {
@@ -638,23 +663,38 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
                 }
             }
         };
-        if (__builtin_expect(sh2 != 0, 0)) stage_rows(IC<1>{}, ldexpf(1.0f, -sh2));
-        else stage_rows(IC<0>{}, 1.0f);
-        __syncthreads();
-        // departures: the last member to leave re-arms the group's counters
-        if (tid == 0) {
-            const unsigned prev = __hip_atomic_fetch_add(arrive + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (prev == (unsigned)RB - 1) {
-                __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(arrive + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        auto depart = [&]() __attribute__((always_inline)) {
+            // the last member to leave re-arms the group's counters
+            if (tid == 0) {
+                const unsigned prev = __hip_atomic_fetch_add(arrive + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (prev == (unsigned)RB - 1) {
+                    __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(arrive + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
+        };
+        if (__builtin_expect(sh2 != 0, 0)) {
+            // rare: h past the f16 range somewhere in the group -- every row again
+            // as h 2^-sh2, and the own block's K-steps again (ring refilled in order)
+            stage_rows(IC<1>{}, ldexpf(1.0f, -sh2));
+            __syncthreads();
+            zero_acc();
+#pragma unroll
+            for (int t = S1; t < S1 + R; ++t) load_a(t % R, smap(t));
+            kloop(IC<0>{}, IC<S1>{}, IC<OWN>{});
+        } else {
+            stage_rows(IC<0>{}, 1.0f);
+            __syncthreads();
         }
+        depart();
+        kloop(IC<0>{}, IC<OWN>{}, IC<ST>{});
     }
-    zero_acc();
-    US_STAMP(3);
-
-    if (KG == 1 || kg == 0) kloop(IC<0>{}, IC<S1 / KG>{}, IC<ST / KG>{});
-    else kloop(IC<1>{}, IC<S1 / KG>{}, IC<ST / KG>{});
+    if constexpr (RB == 1) {
+        zero_acc();
+        US_STAMP(3);
+        if (KG == 1 || kg == 0) kloop(IC<0>{}, IC<S1 / KG>{}, IC<ST / KG>{});
+        else kloop(IC<1>{}, IC<S1 / KG>{}, IC<ST / KG>{});
+    }
     fold_acc();
     combine();
     if (KG == 2 && kg == 1) return;                  // (no barrier follows)
