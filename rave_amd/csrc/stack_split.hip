@@ -118,9 +118,10 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
         float tv[NTB];
 #pragma unroll
         for (int r = 0; r < NTB; ++r) {
+            // (segments of C, a multiple of 64: u and k are wave-uniform -- no masked loads)
             const int i = tid + r * NT;
-            const int u = i / (6 * C), iu = i - u * 6 * C;
-            const int k = iu / C, m = iu - k * C;
+            const int u = __builtin_amdgcn_readfirstlane(i / (6 * C)), iu = i - u * 6 * C;
+            const int k = __builtin_amdgcn_readfirstlane(iu / C), m = iu - k * C;
             const int uu = min(u, kSSUnits - 1);
             const float* src = k == 0 ? a.rs1[uu] : k == 1 ? a.b1[uu] : k == 2 ? a.a2[uu]
                              : k == 3 ? a.rs2[uu] : k == 4 ? a.b2[uu] : a.a0[uu];
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
         }
 #pragma unroll
         for (int r = 0; r < NTB; ++r)
-            if (tid + r * NT < kSSUnits * 6 * C) tab[tid + r * NT] = tv[r];
+            if (__builtin_amdgcn_readfirstlane(tid + r * NT) < kSSUnits * 6 * C) tab[tid + r * NT] = tv[r];
     }
 
     // ------------------------------------------------------------ weight ring (crosses units)

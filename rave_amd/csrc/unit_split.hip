@@ -214,20 +214,23 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
     // ------------------------------------------------------------ per-row table -> LDS
     // every load in flight at once (a rolled loop waits out one round trip per
     // pass); issued here, stored after the window loads are issued
+    // (C is a multiple of 64: the segment k = i / C and the range test are
+    // wave-uniform, so the source pointer is a scalar and no load sits under an
+    // exec mask -- a masked load made the compiler drain every load at the merge)
     constexpr int NTAB = (6 * C + NT - 1) / NT;
     float tabv[NTAB];
 #pragma unroll
     for (int r = 0; r < NTAB; ++r) {
         const int i = tid + r * NT;
-        const int k = i / C, m = i - k * C;
+        const int k = __builtin_amdgcn_readfirstlane(i / C), m = i - k * C;
         const float* src = k == 0 ? a.rs1 : k == 1 ? a.b1 : k == 2 ? a.a2 : k == 3 ? a.rs2 : k == 4 ? a.b2 : a.a0;
-        const bool has = i < 6 * C && ((k == 1 || k == 4) ? a.bias_bytes > 0 : (k == 2 || k == 5) ? SNAKE : true);
+        const bool has = k < 6 && ((k == 1 || k == 4) ? a.bias_bytes > 0 : (k == 2 || k == 5) ? SNAKE : true);
         tabv[r] = has ? src[m] : 0.f;
     }
     auto store_tab = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int r = 0; r < NTAB; ++r)
-            if (tid + r * NT < 6 * C) tab[tid + r * NT] = tabv[r];
+            if (__builtin_amdgcn_readfirstlane(tid + r * NT) < 6 * C) tab[tid + r * NT] = tabv[r];
     };
 
     // ------------------------------------------------------------ prologue: act0(x) window
