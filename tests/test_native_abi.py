@@ -202,3 +202,42 @@ def test_engine_config_validation():
     h = C.c_void_p()
     with pytest.raises(ValueError):   # rejected before any device work
         N.check(N.lib.rave_model_create(C.byref(ccfg), None, 0, None, 0, C.byref(h)), "model_create")
+
+
+def test_unit_workspace_sizes():
+    """rave_unit_workspace (host logic, no GPU): the cooperative form exists for
+    C = 256 / 512 in split16 and the exact-fp32 ring arithmetic only; its
+    counters fit the split-K ticket words and the exchange follows them."""
+    def ws(ch, prec, B=16, T=256):
+        a = N.UnitArgs(channels=ch, batch=B, t_len=T, dilation=3, pad_left=3, act=N.ACT["leaky"],
+                       leaky_slope=0.2, precision=prec)
+        return N.lib.rave_unit_workspace(C.byref(a))
+    assert ws(128, N.PREC_SPLIT16) == 0 and ws(64, N.PREC_SPLIT16) == 0
+    assert ws(256, N.PREC_F32) == 0
+    for C_, prec in [(256, N.PREC_SPLIT16), (512, N.PREC_SPLIT16), (512, N.PREC_F32_RING)]:
+        n = ws(C_, prec)
+        groups = -(-256 // 32) * 16
+        assert n >= N.SPLITK_TICKETS + groups * 32 * C_
+    # more groups than the ticket words can count: no cooperative form
+    assert ws(512, N.PREC_SPLIT16, B=512, T=4096) == 0
+
+
+def test_edge_precision_and_f32_filter_images(golden):
+    """rave_edge_args.precision is validated before any launch, and the fp32
+    filter images are the plain filter rows (scale word 1)."""
+    from oracle.rave_oracle import pqmf_filters
+    hkf, hki = pqmf_filters(golden("pqmf")["hk"])
+    a = N.EdgeArgs(batch=1, frames=64, conv_c_in=6, conv_c_out=64, conv_kernel=7, pqmf_taps=513,
+                   x=16, y=16, weight=16, filter=16, precision=2)
+    assert N.lib.rave_encoder_head(C.byref(a), None) == N.RAVE_ERR_ARG
+    img = N.pack_edge_filter(hkf, head=True, n_out_bands=6, f32=True)
+    rows = img[:16 * 552].reshape(16, 552)
+    assert img[16 * 552] == 1.0
+    h2 = np.asarray(hkf, np.float32).reshape(16, -1)
+    np.testing.assert_array_equal(rows[0, :513], h2[0])
+    np.testing.assert_array_equal(rows[8, 16:16 + 513], h2[0])                       # phase 1 row
+    assert not rows[6].any() and not rows[7].any()                                   # bands past 6
+    timg = N.pack_edge_filter(hki, head=False, f32=True)
+    trows = timg[:16 * 552].reshape(16, 552)
+    h3 = np.asarray(hki, np.float32).reshape(16, 16, -1)
+    np.testing.assert_array_equal(trows[3, 5 * 16 + 2], h3[3, 2, 5])
