@@ -111,6 +111,18 @@ def traffic_per_launch(config: str, B: int, T: int, precision: str):
     return {k: v["bytes_per_launch"] for k, v in t.get("families", {}).items()}
 
 
+def tuning_path(config: str, B: int, T: int, precision: str) -> str:
+    """The committed launch-choice file of one workload and arithmetic mode."""
+    return os.path.join(REPO, "profiles", "tuning", f"{config}_{B}x{T}_{precision}.json")
+
+
+def tuning_hash(tuning) -> str:
+    """sha256 (16 hex) of a RAVE.tuning() list, order-independent."""
+    import hashlib
+    rows = sorted(f"{k} {int(c)}" for k, c, _ in tuning)
+    return hashlib.sha256("\n".join(rows).encode()).hexdigest()[:16]
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -180,22 +192,27 @@ def pipelined(a, cfg, params, spk, precision, model, x, dev):
         ev.record()
         for s in streams:
             s.wait_event(ev)
+        last = [None] * depth          # every stream's last output
         for i in range(k):
             with torch.cuda.stream(streams[i % depth]):
                 m = models[i % depth]
-                y = m.decode(m.encode(x))
+                last[i % depth] = m.decode(m.encode(x))
         for s in streams:
             torch.cuda.current_stream(dev).wait_stream(s)
-        return y
+        return [y for y in last if y is not None]
 
     run(depth * max(1, a.warmup))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    y = run(a.steps)
+    ys = run(a.steps)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    if not torch.isfinite(y).all():
+    # every stream's output finite, and no cooperative-unit give-up in any step
+    # (the engine's status words are sticky until read: rave_model_check)
+    if not all(bool(torch.isfinite(y).all()) for y in ys):
         raise RuntimeError("non-finite output (pipelined)")
+    for m in models:
+        m.check()
     v = B * T * a.steps / el
     return {"streams": depth, "value": round(v, 1), "ms_per_step": round(1e3 * el / a.steps, 4),
             "x_realtime": round(v / SR, 1),
@@ -212,12 +229,19 @@ def run_mode(a, cfg, params, spk, precision, x, dev, world, rank, log_ops):
     from rave_amd.distributed import ShardedRunner
     from rave_amd.model import RAVE
 
-    tuning = None
-    if a.tuning_in and precision == a.precision:
-        with open(a.tuning_in) as fh:
-            tuning = json.load(fh)
-    model = RAVE(cfg, params, spk, device=dev, precision=precision, tuning=tuning)
     B, T = x.shape[0], x.shape[-1]
+    # the plan's launch choices: pinned by the committed tuning file of this
+    # workload and arithmetic mode (profiles/tuning/), so every box runs the same
+    # arithmetic mix and kernels; --retune times them afresh at plan build
+    tuning, src = None, "autotuned at plan build"
+    path = a.tuning_in if (a.tuning_in and precision == a.precision) else None
+    if path is None and not a.retune and os.path.exists(tuning_path(cfg.name, B, T, precision)):
+        path = tuning_path(cfg.name, B, T, precision)
+    if path:
+        with open(path) as fh:
+            tuning = json.load(fh)
+        src = os.path.relpath(path, REPO)
+    model = RAVE(cfg, params, spk, device=dev, precision=precision, tuning=tuning)
     Fz = T // cfg.hop
     runner = ShardedRunner(model, shard_sizes=[B] * world)   # encode -> RCCL all-gather of latents -> decode
 
@@ -227,9 +251,16 @@ def run_mode(a, cfg, params, spk, precision, x, dev, world, rank, log_ops):
     from rave_amd.model import DECODE, ENCODE
     plans = ((ENCODE, T), (DECODE, Fz))
     ops = {w: model.ops(w, B, t) for w, t in plans}          # builds (and autotunes) both plans
+    eff = model.tuning()
     if a.tuning_out and rank == 0 and precision == a.precision:
         with open(a.tuning_out, "w") as fh:
-            json.dump(model.tuning(), fh)
+            json.dump(eff, fh)
+    if a.save_tuning and rank == 0:
+        os.makedirs(os.path.dirname(tuning_path(cfg.name, B, T, precision)), exist_ok=True)
+        with open(tuning_path(cfg.name, B, T, precision), "w") as fh:
+            json.dump(eff, fh, indent=0)
+    tuning_info = {"source": src, "sha16": tuning_hash(eff), "entries": len(eff),
+                   "retimed": (len(eff) - len(tuning)) if tuning is not None else len(eff)}
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -248,9 +279,10 @@ def run_mode(a, cfg, params, spk, precision, x, dev, world, rank, log_ops):
         el = float(t.item())
     if not torch.isfinite(y).all():
         raise RuntimeError("non-finite output")
+    model.check()     # a cooperative-unit give-up in any timed step is an error, not a number
     value = world * B * T * a.steps / el
     res = {"value": round(value, 1), "ms_per_step": round(1e3 * el / a.steps, 4),
-           "x_realtime": round(value / SR, 1), "dtype": DTYPE[precision]}
+           "x_realtime": round(value / SR, 1), "dtype": DTYPE[precision], "tuning": tuning_info}
     if a.pipeline > 1 and world == 1 and precision == a.precision:
         res["pipelined"] = pipelined(a, cfg, params, spk, precision, model, x, dev)
     launches = {}
@@ -407,6 +439,10 @@ def main():
                     help="skip the exact-fp32 run that rides along a non-f32 headline")
     ap.add_argument("--tuning-in", help="JSON of RAVE.tuning() to reuse (no timing runs at plan build)")
     ap.add_argument("--tuning-out", help="write RAVE.tuning() here after the plans are built")
+    ap.add_argument("--retune", action="store_true",
+                    help="ignore the committed profiles/tuning/ files: time every launch choice at plan build")
+    ap.add_argument("--save-tuning", action="store_true",
+                    help="write each mode's effective launch choices to profiles/tuning/ (to pin them)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="torch CPU threads of the baseline (the GPU box's CPU share is 16)")
@@ -479,6 +515,7 @@ def main():
             "x_realtime": head["x_realtime"],
             "per_gpu_samples_per_s": round(head["value"] / world, 1),
             "gemm_launches_by_family": head["gemm_launches_by_family"],
+            "tuning": head["tuning"],
             "roofline": head.get("roofline"),
             "pipelined": head.get("pipelined"),
             "f32_exact": exact,

@@ -44,9 +44,14 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 13
+#define RAVE_ABI_VERSION 14
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
+/* The last of those words is reserved: no conv ticket uses it.  A cooperative
+ * fused unit (rave_unit_workspace) whose in-launch hand-off gave up sets it to
+ * nonzero and leaves it set (sticky); whoever owns the workspace reads it and
+ * zeroes it (the model engine does after every plan that holds such a unit). */
+#define RAVE_SPLITK_STATUS_WORD (RAVE_SPLITK_TICKETS - 1)
 
 /* ---------------------------------------------------------------- status */
 enum {
@@ -54,7 +59,9 @@ enum {
     RAVE_ERR_ARG = -1,          /* invalid argument (ValueError in Python)      */
     RAVE_ERR_HIP = -2,          /* HIP runtime error (RuntimeError)             */
     RAVE_ERR_UNSUPPORTED = -3,  /* shape/config the kernels do not implement    */
-    RAVE_ERR_STATE = -4         /* bad handle / plan                            */
+    RAVE_ERR_STATE = -4,        /* bad handle / plan                            */
+    RAVE_ERR_COOP = -5          /* a cooperative unit's in-launch hand-off gave up:
+                                   that call's outputs are NaN (RuntimeError)   */
 };
 
 /* activation applied to a conv INPUT (fused prologue) */
@@ -319,6 +326,9 @@ typedef struct rave_unit_args {
     const float* alpha0; const float* alpha2;
     float* workspace;   /* optional, rave_unit_workspace() floats, zeroed once before its first
                            use (every launch leaves its counters zero); NULL: one workgroup per slab */
+    uint32_t* status;   /* optional (cooperative form): a group whose hand-off gave up also sets
+                           this word to 1 (system-scope store: host-mapped memory works), beside
+                           the workspace's RAVE_SPLITK_STATUS_WORD; the caller clears it */
 } rave_unit_args;
 int64_t rave_unit_packed_size(int channels);
 int rave_unit_pack_weight(const float* w1, const float* w2, int channels, float* packed);
@@ -340,6 +350,11 @@ int rave_unit_ring_pack_weight(const float* w1, const float* w2, int channels, f
  * serves both when ops run in stream order. */
 int64_t rave_unit_workspace(const rave_unit_args* a);
 int rave_residual_unit(const rave_unit_args* a, void* stream);
+/* Debug / test hook for the cooperative hand-off (process-wide, read at each launch):
+ * spin_limit = polls before a member gives up (< 0: the default, 2^18); force_giveup != 0
+ * makes every group report a give-up after a normal hand-off (outputs NaN, status set),
+ * so the error path can be exercised deterministically. */
+int rave_debug_coop(int64_t spin_limit, int force_giveup);
 
 /* ---------------------------------------------------------------- residual stack
  * RAVE_STACK_UNITS consecutive Residual(DilatedUnit)s of one width (an
@@ -659,6 +674,15 @@ int rave_model_forward(rave_model* m, const float* x, int batch, int t, float* y
 int rave_model_encode_codes(rave_model* m, const float* x, int batch, int t, int64_t* idx, void* stream);
 int rave_model_decode_codes(rave_model* m, const int64_t* idx, int batch, int frames, float* y,
                             const float* noise_u, void* stream);
+/* Cooperative-unit status.  The cooperative fused unit (rave_unit_workspace)
+ * hands rows between workgroups inside a launch with a bounded wait; when a
+ * wait gives up, that call's outputs are NaN and a host-mapped status word of
+ * the model is set.  Every encode / decode / forward / stream call first checks
+ * the word (no synchronisation: it reports give-ups of calls that have already
+ * run) and returns RAVE_ERR_COOP, rave_last_error naming the units, clearing
+ * it.  rave_model_check does the same on demand; with `wait` nonzero it first
+ * synchronises `stream`, so it covers every call queued there. */
+int rave_model_check(rave_model* m, int wait, void* stream);
 /* dims of NoiseGeneratorV2's noise for a decode of `frames` latent frames:
  * (B, noise frames, n_band, target) written to out[0..3]. */
 int rave_model_noise_shape(const rave_model* m, int batch, int frames, int64_t* out4);

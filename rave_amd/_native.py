@@ -24,6 +24,7 @@ RAVE_ERR_ARG = -1
 RAVE_ERR_HIP = -2
 RAVE_ERR_UNSUPPORTED = -3
 RAVE_ERR_STATE = -4
+RAVE_ERR_COOP = -5         # a cooperative unit's in-launch hand-off gave up (RuntimeError)
 
 ACT = {"none": 0, "leaky": 1, "snake": 2}
 
@@ -41,8 +42,9 @@ OP_UNIT = 11
 OP_STACK = 12
 OP_HEAD = 13
 OP_TAIL = 14
-ABI_VERSION = 13
+ABI_VERSION = 14
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
+SPLITK_STATUS_WORD = SPLITK_TICKETS - 1   # RAVE_SPLITK_STATUS_WORD: the cooperative unit's give-up word
 
 # GEMM arithmetic of conv / unit ops (include/rave_amd.h RAVE_PREC_*)
 PREC_F32 = 0
@@ -135,7 +137,7 @@ class UnitArgs(C.Structure):
                 ("x", vp), ("x_sb", i64), ("x_sc", i64),
                 ("y", vp), ("y_sb", i64), ("y_sc", i64),
                 ("weight", vp), ("bias1", vp), ("bias2", vp), ("alpha0", vp), ("alpha2", vp),
-                ("workspace", vp)]
+                ("workspace", vp), ("status", vp)]
 
 
 STACK_UNITS = 3
@@ -241,7 +243,7 @@ EXPORTS = [
     "rave_rvq_workspace", "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
     "rave_unit_packed_size", "rave_unit_pack_weight", "rave_residual_unit",
     "rave_unit_split_packed_size", "rave_unit_split_pack_weight", "rave_unit_ring_pack_weight",
-    "rave_unit_workspace",
+    "rave_unit_workspace", "rave_debug_coop", "rave_model_check",
     "rave_stack_supported", "rave_residual_stack",
     "rave_plan_create", "rave_plan_run", "rave_plan_destroy", "rave_plan_size",
     "rave_plan_profile", "rave_plan_op_times", "rave_fill_uniform",
@@ -293,6 +295,7 @@ def _load():
     lib.rave_unit_pack_weight.argtypes = [vp, vp, C.c_int, vp]
     lib.rave_unit_workspace.argtypes = [C.c_void_p]
     lib.rave_unit_workspace.restype = i64
+    lib.rave_debug_coop.argtypes = [i64, C.c_int]
     lib.rave_unit_split_packed_size.argtypes = [C.c_int]
     lib.rave_stack_supported.argtypes = [C.c_int]
     lib.rave_unit_split_packed_size.restype = i64
@@ -330,6 +333,7 @@ def _load():
     lib.rave_model_forward.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp]
     lib.rave_model_encode_codes.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp]
     lib.rave_model_decode_codes.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp]
+    lib.rave_model_check.argtypes = [vp, C.c_int, vp]
     lib.rave_model_noise_shape.argtypes = [vp, C.c_int, C.c_int, C.POINTER(i64)]
     lib.rave_model_adain_control.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp]
     lib.rave_model_set_row0.argtypes = [vp, C.c_int]

@@ -97,12 +97,8 @@ class CachedPadding1d(nn.Module):
             return x
         if self.pad.shape[1] != x.shape[1] or self.pad.device != x.device:
             self.pad = torch.zeros(self.max_batch, x.shape[1], self.padding, device=x.device, dtype=x.dtype)
-        b = x.shape[0]
-        x = torch.cat([self.pad[:b], x], -1)
-        self.pad[:b].copy_(x[..., -self.padding:])
-        if self.crop:
-            x = x[..., :-self.padding]
-        return x
+        # [pad | x] and the newest `padding` columns back into pad, on rave_copy
+        return torch.ops.rave_amd.delay_line(x, self.pad, self.crop)
 
 
 class _PackedConv(nn.Module):
@@ -122,6 +118,11 @@ class _PackedConv(nn.Module):
         self.bias = nn.Parameter(ref.bias.detach().clone()) if bias else None
         self.register_buffer("packed", torch.zeros(0), persistent=False)
         self.packed_key: List[int] = [0, 0]
+
+    @torch.jit.export
+    def fused(self) -> Tuple[int, float, Optional[torch.Tensor]]:
+        """Not an activation (rave_amd.modules.FusedSequential's protocol)."""
+        return 0, 0.0, None            # ACT_NONE
 
     @torch.jit.export
     def prepare(self) -> None:
@@ -146,7 +147,10 @@ class _PackedConv(nn.Module):
 class Conv1d(_PackedConv):
     """cc.Conv1d (offline: F.pad + conv; cached: CachedConv1d), fused on the
     kernels with an optional input activation (``activation``: ACT_LEAKY with
-    ``slope`` or ACT_SNAKE with ``alpha``) and residual (``forward(x, res)``)."""
+    ``slope`` or ACT_SNAKE with ``alpha``) and residual (``forward(x, res)``).
+    ``forward(x, res, act, slope, alpha)`` with ``act >= 0`` takes the input
+    activation of this call instead (the module tree fuses the activation
+    module in front of each conv this way: rave_amd.modules)."""
 
     def __init__(self, in_channels: int, out_channels: int, kernel_size: int, stride: int = 1, padding=0,
                  dilation: int = 1, groups: int = 1, bias: bool = True, cumulative_delay: int = 0,
@@ -169,17 +173,19 @@ class Conv1d(_PackedConv):
         self.cache = CachedPadding1d(self.pad_l + self.pad_r, channels=in_channels)
         self.downsampling_delay = CachedPadding1d(self.stride_delay, crop=True, channels=in_channels)
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, act: int = -1, slope: float = 0.2,
+                alpha: Optional[torch.Tensor] = None) -> torch.Tensor:
         packed = self._packed_weight(x)
-        alpha: Optional[torch.Tensor] = self.alpha if self.act == 2 else None        # ACT_SNAKE
+        if act < 0:
+            act, slope = self.act, self.slope
+            alpha = self.alpha if self.act == 2 else None        # ACT_SNAKE
         if self.cached:
             x = self.cache(self.downsampling_delay(x))
             pl, pr = 0, 0
         else:
             pl, pr = self.pad_l, self.pad_r
         return torch.ops.rave_amd.conv1d(x.contiguous(), packed, self.bias, alpha, residual, self.c_out, self.kernel,
-                                         self.stride, self.dilation, pl, pr, False, 0, self.act, self.slope,
-                                         self.precision)
+                                         self.stride, self.dilation, pl, pr, False, 0, act, slope, self.precision)
 
 
 class ConvTranspose1d(_PackedConv):
@@ -202,17 +208,19 @@ class ConvTranspose1d(_PackedConv):
         self.cumulative_delay = (self.padding + cumulative_delay * stride) if cached else 0
         self.hist = CachedPadding1d(1, channels=in_channels)    # the one input column the polyphase form reads back
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, act: int = -1, slope: float = 0.2,
+                alpha: Optional[torch.Tensor] = None) -> torch.Tensor:
         packed = self._packed_weight(x)
-        alpha: Optional[torch.Tensor] = self.alpha if self.act == 2 else None        # ACT_SNAKE
+        if act < 0:
+            act, slope = self.act, self.slope
+            alpha = self.alpha if self.act == 2 else None        # ACT_SNAKE
         if self.cached:
             x = self.hist(x)
             pl = 1
         else:
             pl = 0
-        return torch.ops.rave_amd.conv1d(x.contiguous(), packed, self.bias, alpha, None, self.c_out, self.kernel,
-                                         self.stride, 1, pl, 0, True, self.out_shift, self.act, self.slope,
-                                         self.precision)
+        return torch.ops.rave_amd.conv1d(x.contiguous(), packed, self.bias, alpha, residual, self.c_out, self.kernel,
+                                         self.stride, 1, pl, 0, True, self.out_shift, act, slope, self.precision)
 
 
 class AlignBranches(nn.Module):
@@ -269,6 +277,7 @@ class CachedPQMF(nn.Module):
         self.pad_s = get_padding(int(hki.shape[-1]))[0]
         self.hist_a = CachedPadding1d(int(hkf.shape[-1]) - 1, channels=1)
         self.hist_s = CachedPadding1d(int(hki.shape[-1]) - 1, channels=self.n_band)
+        self.hist_n = CachedPadding1d(int(hki.shape[-1]) - 1, channels=self.n_band)   # the epilogue's noise
 
     def forward(self, x: torch.Tensor, n_out: int = -1) -> torch.Tensor:
         n = self.n_band if n_out < 0 else n_out
@@ -280,13 +289,35 @@ class CachedPQMF(nn.Module):
             return y[..., :T // self.n_band]
         return torch.ops.rave_amd.pqmf_analysis(x.contiguous(), self.hkf, n, self.pad_a, self.precision)
 
-    def inverse(self, x: torch.Tensor) -> torch.Tensor:
+    def inverse(self, x: torch.Tensor, mode: int = 0, noise: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """mode 1 / 2: GeneratorV2's epilogue fused in front of the synthesis --
+        x (B, 2 n_band, F) -> tanh(x[:n] sigmoid(x[n:]) + noise), or x (B, n_band,
+        F) -> tanh(x + noise) (rave/blocks.py:699-707); cached mode keeps the
+        history of x (and of noise) before the epilogue."""
         if self.cached:
             F = x.shape[-1]
             h = self.hist_s.padding
             xc = self.hist_s(x).contiguous()
-            return torch.ops.rave_amd.pqmf_synthesis(xc, self.hki, 0, F, -h, self.precision)
-        return torch.ops.rave_amd.pqmf_synthesis(x.contiguous(), self.hki, self.pad_s, 0, 0, self.precision)
+            nc: Optional[torch.Tensor] = None
+            if noise is not None:
+                nc = self.hist_n(noise).contiguous()
+            return torch.ops.rave_amd.pqmf_synthesis(xc, self.hki, 0, F, -h, self.precision, mode, nc)
+        return torch.ops.rave_amd.pqmf_synthesis(x.contiguous(), self.hki, self.pad_s, 0, 0, self.precision, mode,
+                                                 noise)
+
+
+def adain(x: torch.Tensor, mean_x: torch.Tensor, std_x: torch.Tensor, mean_y: torch.Tensor, std_y: torch.Tensor,
+          num_update_x: torch.Tensor, num_update_y: torch.Tensor, mode: int) -> torch.Tensor:
+    """AdaptiveInstanceNormalization.forward, eval mode (rave/blocks.py:899-919):
+    mode 0 transfer, 1 learn_x, 2 learn_y; updates the buffers in place."""
+    return torch.ops.rave_amd.adain(x, mean_x, std_x, mean_y, std_y, num_update_x, num_update_y, mode)
+
+
+def noise_synth(amp: torch.Tensor, u: torch.Tensor, n_band: int, noise_bands: int) -> torch.Tensor:
+    """NoiseGeneratorV2's filter stage (rave/blocks.py:281-291): pre-sigmoid
+    amplitudes (B, n_band noise_bands, F) and U[0,1) draws (B, F, n_band,
+    target) -> filtered noise (B, n_band, F target)."""
+    return torch.ops.rave_amd.noise_synth(amp, u, n_band, noise_bands)
 
 
 def rvq_encode(z: torch.Tensor, codebooks: torch.Tensor) -> torch.Tensor:

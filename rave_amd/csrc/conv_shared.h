@@ -14,6 +14,7 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
 constexpr int kSplitTickets = RAVE_SPLITK_TICKETS;   // int32 words ahead of the split-K slabs
+constexpr int kSplitTicketsUsable = RAVE_SPLITK_STATUS_WORD;   // tiles with a ticket (the last word is reserved)
 constexpr int kMaxDil = 16;       // largest dilation of a 3-tap conv the kernels stage
 
 struct ConvKArgs {

@@ -1153,7 +1153,7 @@ int conv1d_split_configs(const rave_conv1d_args& a, int32_t* cfgs, int max_cfgs)
             const int64_t waves = ntiles * nw * S;
             if (S > 1 && (waves > 16384 || ntiles * nw >= 4096)) continue;   // enough waves unsplit
             // in-launch combine: the last split reads S slabs serially -- only for few splits
-            if (S == 1 || (S <= 4 && ntiles <= kSplitTickets)) put(encode_config(ti, S, 0));
+            if (S == 1 || (S <= 4 && ntiles <= kSplitTicketsUsable)) put(encode_config(ti, S, 0));
             if (S > 1) put(encode_config(ti, S, 1));
         }
     }
@@ -1191,7 +1191,7 @@ int conv1d_split(const rave_conv1d_args& a, void* stream) {
     const int64_t ntiles = (int64_t)k.gx * k.gy * k.B;
     RAVE_CHECK_ARG(ntiles * k.S < (1ll << 31), "conv1d(split16): grid too large");
     // the last-arriving split sums the tile's slabs (16-byte slab rows, counters for every tile)
-    k.inlaunch = k.S > 1 && !c.sep && k.vec_p && ntiles <= kSplitTickets;
+    k.inlaunch = k.S > 1 && !c.sep && k.vec_p && ntiles <= kSplitTicketsUsable;
 #ifdef RAVE_STAMPS
     k.stamps = a.stamps;
 #endif

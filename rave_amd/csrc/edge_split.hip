@@ -795,6 +795,10 @@ extern "C" int rave_encoder_head(const rave_edge_args* p, void* stream) {
     }
     RAVE_CHECK_ARG(a.fill_channels == 0 || (a.fill_y && a.fill_values && a.fill_t > 0),
                    "encoder_head: fill needs fill_y, fill_values and fill_t");
+    if (a.act != RAVE_ACT_NONE) {   // EncoderV2's first conv has no input activation (rave/blocks.py:533-536)
+        set_error("encoder_head: the fused analysis + first conv applies no input activation (act must be RAVE_ACT_NONE)");
+        return RAVE_ERR_UNSUPPORTED;
+    }
     bool f32;
     int rc = edge_prec(a, f32);
     if (rc != RAVE_OK) return rc;

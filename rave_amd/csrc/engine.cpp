@@ -362,6 +362,14 @@ struct Model {
     float* scratch = nullptr;
     int64_t scratch_n = 0;
     hipStream_t cur_stream = nullptr;    // stream of the call that builds plans (timing runs)
+    // cooperative units' give-up words: host-mapped, one per cooperative op of any
+    // plan (rave_unit_args.status), read without synchronisation by coop_check
+    static constexpr int kCoopSlots = 256;
+    uint32_t* coop_host = nullptr;
+    uint32_t* coop_dev = nullptr;
+    std::vector<std::string> coop_labels;
+    View coop_status(const std::string& label);
+    void coop_check();
 
     ~Model();
     int64_t add(const float* p, int64_t n) {
@@ -435,6 +443,7 @@ struct Model {
 
 Model::~Model() {
     plans.clear();
+    if (coop_host) (void)hipHostFree(coop_host);
     for (void* p : {(void*)arena, (void*)ad_stats, (void*)ad_init, (void*)ad_counters, (void*)ad_tickets, (void*)fwd_z, (void*)noise,
                     (void*)scratch})
         if (p) (void)hipFree(p);
@@ -775,10 +784,44 @@ void Model::unit_op(Plan& p, const Node& k3, const Node& k1, int B, int T, const
     p.bind(o, U, U.alpha2, k1.act == RAVE_ACT_SNAKE ? &a2 : nullptr);
     View sk = p.splitk(nws);
     p.bind(o, U, U.workspace, nws > 0 ? &sk : nullptr);
+    View sv = nws > 0 ? coop_status(label + " (B=" + std::to_string(B) + ", T=" + std::to_string(T) + ")") : View{};
+    p.bind(o, U, U.status, nws > 0 ? &sv : nullptr);
     o.prec = pr;
     const double C_ = k3.c_in;
     o.flops = 2.0 * B * T * C_ * C_ * 4;
     o.bytes = 4.0 * (2.0 * B * C_ * T + 4.0 * C_ * C_);
+}
+
+// A status word for one cooperative unit op (the last slot is shared once
+// kCoopSlots ops exist).
+View Model::coop_status(const std::string& label) {
+    if (!coop_host) {
+        void* h = nullptr;
+        RAVE_HIP_OR_THROW(hipHostMalloc(&h, kCoopSlots * 4, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(h, 0, kCoopSlots * 4);
+        void* d = nullptr;
+        RAVE_HIP_OR_THROW(hipHostGetDevicePointer(&d, h, 0));
+        coop_host = static_cast<uint32_t*>(h);
+        coop_dev = static_cast<uint32_t*>(d);
+    }
+    const int slot = std::min<int>((int)coop_labels.size(), kCoopSlots - 1);
+    if (slot < kCoopSlots - 1) coop_labels.push_back(label);
+    else if (coop_labels.size() == kCoopSlots - 1) coop_labels.push_back(label + " (or a later cooperative unit)");
+    return abs_view(coop_dev + slot);
+}
+
+// Report (and clear) give-ups of cooperative units that have already run.
+void Model::coop_check() {
+    if (!coop_host) return;
+    std::string which;
+    for (size_t i = 0; i < coop_labels.size(); ++i) {
+        volatile uint32_t* w = coop_host + i;
+        if (*w == 0) continue;
+        *w = 0;
+        which += (which.empty() ? "" : ", ") + coop_labels[i];
+    }
+    if (!which.empty())
+        fail(RAVE_ERR_COOP, "cooperative residual unit hand-off gave up (outputs of that call are NaN): " + which);
 }
 
 // ------------------------------------------------------------------ residual stacks
@@ -1829,6 +1872,7 @@ static void check_len(Model* m, int batch, int t) {
 extern "C" int rave_model_encode(rave_model* h, const float* x, int batch, int t, float* z, void* stream) {
     return guarded([&] {
         Model* m = model_of(h);
+        m->coop_check();
         if (!x || !z) fail(RAVE_ERR_ARG, "encode: null tensor");
         check_len(m, batch, t);
         m->run_kind(0, batch, t, x, z, nullptr, as_stream(stream));
@@ -1839,6 +1883,7 @@ extern "C" int rave_model_decode(rave_model* h, const float* z, int batch, int f
                                  const float* noise_u, void* stream) {
     return guarded([&] {
         Model* m = model_of(h);
+        m->coop_check();
         if (!z || !y) fail(RAVE_ERR_ARG, "decode: null tensor");
         if (batch <= 0 || frames <= 0) fail(RAVE_ERR_ARG, "batch and frames must be positive");
         check_noise_frames(m, frames);
@@ -1851,6 +1896,7 @@ extern "C" int rave_model_forward(rave_model* h, const float* x, int batch, int 
                                   void* stream) {
     return guarded([&] {
         Model* m = model_of(h);
+        m->coop_check();
         if (!x || !y) fail(RAVE_ERR_ARG, "forward: null tensor");
         check_len(m, batch, t);
         const int Fz = t / m->hop;
@@ -1870,6 +1916,7 @@ extern "C" int rave_model_forward(rave_model* h, const float* x, int batch, int 
 extern "C" int rave_model_encode_codes(rave_model* h, const float* x, int batch, int t, int64_t* idx, void* stream) {
     return guarded([&] {
         Model* m = model_of(h);
+        m->coop_check();
         if (m->cfg.rvq_quantizers <= 0) fail(RAVE_ERR_ARG, "encode_codes needs a discrete (RVQ) config");
         if (!x || !idx) fail(RAVE_ERR_ARG, "encode_codes: null tensor");
         check_len(m, batch, t);
@@ -1881,12 +1928,21 @@ extern "C" int rave_model_decode_codes(rave_model* h, const int64_t* idx, int ba
                                        const float* noise_u, void* stream) {
     return guarded([&] {
         Model* m = model_of(h);
+        m->coop_check();
         if (m->cfg.rvq_quantizers <= 0) fail(RAVE_ERR_ARG, "decode_codes needs a discrete (RVQ) config");
         if (!idx || !y) fail(RAVE_ERR_ARG, "decode_codes: null tensor");
         if (batch <= 0 || frames <= 0) fail(RAVE_ERR_ARG, "batch and frames must be positive");
         check_noise_frames(m, frames);
         m->run_kind(3, batch, frames, idx, y, m->noise_ptr(noise_u, batch, frames, as_stream(stream)),
                     as_stream(stream));
+    });
+}
+
+extern "C" int rave_model_check(rave_model* h, int wait, void* stream) {
+    return guarded([&] {
+        Model* m = model_of(h);
+        if (wait) RAVE_HIP_OR_THROW(hipStreamSynchronize(as_stream(stream)));
+        m->coop_check();
     });
 }
 
@@ -2566,6 +2622,7 @@ static void stream_dec(Stream* s, const void* in, float* y, const float* noise_u
 extern "C" int rave_stream_encode(rave_stream* h, const float* x, float* z, void* stream) {
     return guarded([&] {
         Stream* s = stream_of(h);
+        s->m->coop_check();
         if (!x || !z) fail(RAVE_ERR_ARG, "stream encode: null tensor");
         if (s->codes) fail(RAVE_ERR_ARG, "discrete config: stream with rave_stream_encode_codes");
         stream_enc(s, x, z, as_stream(stream));
@@ -2575,6 +2632,7 @@ extern "C" int rave_stream_encode(rave_stream* h, const float* x, float* z, void
 extern "C" int rave_stream_decode(rave_stream* h, const float* z, float* y, const float* noise_u, void* stream) {
     return guarded([&] {
         Stream* s = stream_of(h);
+        s->m->coop_check();
         if (!z || !y) fail(RAVE_ERR_ARG, "stream decode: null tensor");
         if (s->codes) fail(RAVE_ERR_ARG, "discrete config: stream with rave_stream_decode_codes");
         stream_dec(s, z, y, noise_u, as_stream(stream));
@@ -2584,6 +2642,7 @@ extern "C" int rave_stream_decode(rave_stream* h, const float* z, float* y, cons
 extern "C" int rave_stream_encode_codes(rave_stream* h, const float* x, int64_t* idx, void* stream) {
     return guarded([&] {
         Stream* s = stream_of(h);
+        s->m->coop_check();
         if (!x || !idx) fail(RAVE_ERR_ARG, "stream encode_codes: null tensor");
         if (!s->codes) fail(RAVE_ERR_ARG, "encode_codes needs a discrete (RVQ) config");
         stream_enc(s, x, idx, as_stream(stream));
@@ -2594,6 +2653,7 @@ extern "C" int rave_stream_decode_codes(rave_stream* h, const int64_t* idx, floa
                                         void* stream) {
     return guarded([&] {
         Stream* s = stream_of(h);
+        s->m->coop_check();
         if (!idx || !y) fail(RAVE_ERR_ARG, "stream decode_codes: null tensor");
         if (!s->codes) fail(RAVE_ERR_ARG, "decode_codes needs a discrete (RVQ) config");
         stream_dec(s, idx, y, noise_u, as_stream(stream));

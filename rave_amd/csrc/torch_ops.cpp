@@ -234,6 +234,11 @@ struct Engine : torch::CustomClassHolder {
         // return is stream-ordered after the copy
         speaker = emb.detach().cpu().to(at::kFloat).reshape({-1}).clone();    // travels with the pickle
     }
+    // cooperative-unit give-ups of the calls queued so far (rave_model_check; waits for
+    // the current stream); encode / decode / stream calls also raise them on entry
+    void check_status() { check(rave_model_check(m, 1, cur()), "check"); }
+    // launch choices (RAVE.tuning() text: "key value ms" per line), e.g. a pinned plan
+    void set_tuning(const std::string& text) { check(rave_model_tuning_set(m, text.c_str()), "tuning_set"); }
     int64_t get_hop() const { return hop; }
     int64_t latent_channels() const { return zc(); }
     int64_t block() const { return stream_block; }
@@ -403,23 +408,136 @@ at::Tensor pqmf_analysis_op(at::Tensor x, at::Tensor hkf, int64_t n_out_bands, i
 // rave_amd::pqmf_synthesis -- CachedPQMF.inverse (rave/pqmf.py:275-284): x (B, n_band, F)
 // -> (B, 1, F * n_band); hki (n_band, n_band, taps).  x_len > F: x carries
 // cached history columns before the F frames (streaming, pad_left 0).
+// mode 1 / 2: GeneratorV2's epilogue fused in front (rave/blocks.py:699-707):
+// x holds 2 n_band channels (waveform, amplitude) and the input is
+// tanh(x[:n] * sigmoid(x[n:]) + noise) (mode 1) or tanh(x + noise) (mode 2);
+// noise (B, n_band, x_len) or None.
 at::Tensor pqmf_synthesis_op(at::Tensor x, at::Tensor hki, int64_t pad_left, int64_t frames, int64_t frame0,
-                             int64_t precision) {
+                             int64_t precision, int64_t mode, c10::optional<at::Tensor> noise) {
     seam_tensor(x, "x");
     c10::hip::HIPGuard g((c10::DeviceIndex)x.get_device());
     at::Tensor h = hki.to(x.device(), at::kFloat).contiguous();
     const int64_t nb = h.size(0), B = x.size(0), XL = x.size(2);
-    TORCH_CHECK_VALUE(x.size(1) == nb, "x must have n_band channels");
+    TORCH_CHECK_VALUE(mode >= 0 && mode <= 2, "mode must be 0 (plain), 1 (amplitude modulation) or 2 (tanh)");
+    TORCH_CHECK_VALUE(x.size(1) == (mode == 1 ? 2 * nb : nb), "x must have ", mode == 1 ? 2 * nb : nb, " channels");
+    TORCH_CHECK_VALUE(mode != 0 || !noise.has_value(), "noise needs an epilogue mode");
     const int64_t F = frames > 0 ? frames : XL;
     at::Tensor y = at::empty({B, 1, F * nb}, x.options());
     rave_pqmf_synthesis_args a{};
     a.n_band = (int)nb; a.taps = (int)h.size(2); a.batch = (int)B; a.t_in = (int)F; a.pad_left = (int)pad_left;
-    a.mode = 0; a.frame0 = (int)frame0; a.x_len = (int)XL;
+    a.mode = (int)mode; a.frame0 = (int)frame0; a.x_len = (int)XL;
     a.x = x.data_ptr<float>(); a.x_sb = x.stride(0); a.x_sc = x.stride(1);
+    at::Tensor nz;
+    if (noise.has_value()) {
+        nz = *noise;
+        seam_tensor(nz, "noise");
+        TORCH_CHECK_VALUE(nz.dim() == 3 && nz.size(0) == B && nz.size(1) == nb && nz.size(2) == XL && nz.stride(2) == 1,
+                          "noise must be (B, n_band, x_len), time contiguous");
+        a.noise = nz.data_ptr<float>(); a.n_sb = nz.stride(0); a.n_sc = nz.stride(1);
+    }
     a.y = y.data_ptr<float>(); a.y_sb = y.stride(0);
     a.hki = h.data_ptr<float>(); a.precision = (int)precision;
     check(rave_pqmf_synthesis(&a, cur_stream(x)), "pqmf_synthesis");
     return y;
+}
+
+// rave_amd::adain -- AdaptiveInstanceNormalization.forward in eval mode
+// (rave/blocks.py:856-919) on rave_adain over the module's own buffers
+// (mean_x / std_x / mean_y / std_y (max_batch, C, 1), num_update_x / _y (1,)):
+// mode 0 transfer (when both counters are set), 1 learn_x then transfer,
+// 2 learn_y; a learning mode writes the updated statistics back.
+at::Tensor adain_op(at::Tensor x, at::Tensor mean_x, at::Tensor std_x, at::Tensor mean_y, at::Tensor std_y,
+                    at::Tensor num_update_x, at::Tensor num_update_y, int64_t mode) {
+    seam_tensor(x, "x");
+    TORCH_CHECK_VALUE(x.dim() == 3, "x must be (B, C, T)");
+    TORCH_CHECK_VALUE(mode >= 0 && mode <= 2, "mode must be 0 (transfer), 1 (learn_x) or 2 (learn_y)");
+    c10::hip::HIPGuard g((c10::DeviceIndex)x.get_device());
+    const int64_t B = x.size(0), C = x.size(1), T = x.size(2), mb = mean_x.size(0);
+    for (const at::Tensor* t : {&mean_x, &std_x, &mean_y, &std_y})
+        TORCH_CHECK_VALUE(t->dim() == 3 && t->size(0) == mb && t->size(1) == C && t->size(2) == 1,
+                          "AdaIN statistics must be (max_batch, C, 1)");
+    TORCH_CHECK_VALUE(B <= mb, "batch exceeds the AdaIN buffers' max_batch");
+    TORCH_CHECK_VALUE(T >= 2 || mode == 0, "learning needs at least 2 samples (unbiased std)");
+    at::Tensor xc = x.contiguous();
+    at::Tensor stats = at::stack({mean_x, std_x, mean_y, std_y}).to(x.device(), at::kFloat).reshape({4, mb, C})
+                           .contiguous();
+    at::Tensor cnt = at::cat({num_update_x.reshape({1}), num_update_y.reshape({1})}).to(x.device(), at::kFloat)
+                         .contiguous();
+    at::Tensor ticket = at::zeros({1}, x.options().dtype(at::kInt));
+    at::Tensor y = at::empty_like(xc);
+    rave_adain_args a{};
+    a.batch = (int)B; a.channels = (int)C; a.t_len = (int)T; a.mode = (int)mode; a.max_batch = (int)mb; a.row0 = 0;
+    a.x = xc.data_ptr<float>(); a.x_sb = xc.stride(0); a.x_sc = xc.stride(1);
+    a.y = y.data_ptr<float>(); a.y_sb = y.stride(0); a.y_sc = y.stride(1);
+    a.stats = stats.data_ptr<float>();
+    a.counters = cnt.data_ptr<float>();
+    a.ticket = reinterpret_cast<uint32_t*>(ticket.data_ptr<int32_t>());
+    check(rave_adain(&a, cur_stream(x)), "adain");
+    if (mode == 1) {
+        mean_x.copy_(stats[0].reshape(mean_x.sizes()));
+        std_x.copy_(stats[1].reshape(std_x.sizes()));
+        num_update_x.copy_(cnt.narrow(0, 0, 1).reshape(num_update_x.sizes()));
+    } else if (mode == 2) {
+        mean_y.copy_(stats[2].reshape(mean_y.sizes()));
+        std_y.copy_(stats[3].reshape(std_y.sizes()));
+        num_update_y.copy_(cnt.narrow(0, 1, 1).reshape(num_update_y.sizes()));
+    }
+    return y;
+}
+
+// rave_amd::noise_synth -- NoiseGeneratorV2's filter stage after its conv stack
+// (rave/blocks.py:281-291, rave/core.py:66-129) on rave_noise_synth: amp
+// (B, n_band * noise_bands, F) pre-sigmoid, u (B, F, n_band, target) U[0,1)
+// (torch.rand_like(ir)) -> noise (B, n_band, F * target).
+at::Tensor noise_synth_op(at::Tensor amp, at::Tensor u, int64_t n_band, int64_t noise_bands) {
+    seam_tensor(amp, "amp");
+    seam_tensor(u, "u");
+    c10::hip::HIPGuard g((c10::DeviceIndex)amp.get_device());
+    TORCH_CHECK_VALUE(amp.dim() == 3 && amp.size(1) == n_band * noise_bands, "amp must be (B, n_band * noise_bands, F)");
+    const int64_t B = amp.size(0), F = amp.size(2);
+    TORCH_CHECK_VALUE(u.dim() == 4 && u.size(0) == B && u.size(1) == F && u.size(2) == n_band,
+                      "u must be (B, F, n_band, target)");
+    const int64_t target = u.size(3);
+    at::Tensor ac = amp.contiguous(), uc = u.contiguous();
+    at::Tensor y = at::empty({B, n_band, F * target}, amp.options());
+    rave_noise_args a{};
+    a.batch = (int)B; a.frames = (int)F; a.n_band = (int)n_band; a.noise_bands = (int)noise_bands;
+    a.target = (int)target;
+    a.amp = ac.data_ptr<float>(); a.a_sb = ac.stride(0); a.a_sc = ac.stride(1);
+    a.u = uc.data_ptr<float>(); a.u_sb = uc.stride(0);
+    a.y = y.data_ptr<float>(); a.y_sb = y.stride(0); a.y_sc = y.stride(1);
+    check(rave_noise_synth(&a, cur_stream(amp)), "noise_synth");
+    return y;
+}
+
+// rave_amd::delay_line -- cached_conv's CachedPadding1d on rave_copy: returns
+// [state[:B] | x] (B, C, P + T), or its first T columns when `crop` (a pure
+// P-sample delay), and keeps the newest P columns in `state` (max_batch, C, P).
+at::Tensor delay_line_op(at::Tensor x, at::Tensor state, bool crop) {
+    seam_tensor(x, "x");
+    seam_tensor(state, "state");
+    c10::hip::HIPGuard g((c10::DeviceIndex)x.get_device());
+    TORCH_CHECK_VALUE(x.dim() == 3 && state.dim() == 3 && state.size(1) == x.size(1) && state.size(0) >= x.size(0) &&
+                          state.is_contiguous(),
+                      "state must be a contiguous (max_batch, C, P) buffer with x's channels");
+    const int64_t B = x.size(0), C = x.size(1), T = x.size(2), P = state.size(2);
+    at::Tensor xc = x.contiguous();
+    at::Tensor full = at::empty({B, C, P + T}, x.options());
+    void* st = cur_stream(x);
+    auto copy = [&](const float* src, int64_t s_sb, int64_t s_sc, float* dst, int64_t d_sb, int64_t d_sc, int64_t n) {
+        if (n <= 0) return;
+        rave_copy_args a{};
+        a.batch = (int)B; a.channels = (int)C; a.t_len = (int)n;
+        a.x = src; a.x_sb = s_sb; a.x_sc = s_sc;
+        a.y = dst; a.y_sb = d_sb; a.y_sc = d_sc;
+        check(rave_copy(&a, st), "delay_line");
+    };
+    float* f = full.data_ptr<float>();
+    float* sp = state.data_ptr<float>();
+    copy(sp, C * P, P, f, C * (P + T), P + T, P);                                   // history
+    copy(xc.data_ptr<float>(), xc.stride(0), xc.stride(1), f + P, C * (P + T), P + T, T);   // block
+    copy(f + T, C * (P + T), P + T, sp, C * P, P, P);                               // newest P -> state
+    return crop ? full.narrow(2, 0, T) : full;
 }
 
 // rave_amd::rvq_encode / rvq_decode -- ResidualVectorQuantization.encode / decode
@@ -475,8 +593,14 @@ TORCH_LIBRARY(rave_amd, lib) {
             "float slope, int precision) -> Tensor", &conv1d_op);
     lib.def("pqmf_analysis(Tensor x, Tensor hkf, int n_out_bands, int pad_left, int precision) -> Tensor",
             &pqmf_analysis_op);
-    lib.def("pqmf_synthesis(Tensor x, Tensor hki, int pad_left, int frames, int frame0, int precision) -> Tensor",
+    lib.def("pqmf_synthesis(Tensor x, Tensor hki, int pad_left, int frames, int frame0, int precision, int mode=0, "
+            "Tensor? noise=None) -> Tensor",
             &pqmf_synthesis_op);
+    lib.def("adain(Tensor x, Tensor(a!) mean_x, Tensor(b!) std_x, Tensor(c!) mean_y, Tensor(d!) std_y, "
+            "Tensor(e!) num_update_x, Tensor(f!) num_update_y, int mode) -> Tensor",
+            &adain_op);
+    lib.def("noise_synth(Tensor amp, Tensor u, int n_band, int noise_bands) -> Tensor", &noise_synth_op);
+    lib.def("delay_line(Tensor x, Tensor(a!) state, bool crop) -> Tensor", &delay_line_op);
     lib.def("rvq_encode(Tensor z, Tensor codebooks) -> Tensor", &rvq_encode_op);
     lib.def("rvq_decode(Tensor idx, Tensor codebooks) -> Tensor", &rvq_decode_op);
     lib.class_<Engine>("Engine")
@@ -494,6 +618,8 @@ TORCH_LIBRARY(rave_amd, lib) {
         .def("stream_reset", &Engine::stream_reset)
         .def("adain_control", &Engine::adain_control)
         .def("set_speaker", &Engine::set_speaker)
+        .def("check", &Engine::check_status)
+        .def("set_tuning", &Engine::set_tuning)
         .def("hop", &Engine::get_hop)
         .def("latent_channels", &Engine::latent_channels)
         .def("block", &Engine::block)

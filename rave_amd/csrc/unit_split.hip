@@ -31,11 +31,17 @@
 // blocks are consecutive in one XCD's dispatch order (blocks b, b + 8, ...): a
 // group is resident together whenever its first member is, and every other
 // resident group completes without waiting on a non-resident one.  The range
-// guard of h is group-wide (members publish their max |h|).  The arithmetic and
-// the K order are those of the one-workgroup form: the results are identical.
+// guard of h is group-wide (members publish their max |h|).  The arithmetic is
+// that of the one-workgroup form, but not its fp32 summation order: each
+// member's phase 2 starts at its own channel block (smap) and alternate K-steps
+// accumulate into two chains (DA), so the two forms agree within tolerance, not
+// bitwise.  The poll is bounded: a member that gives up writes NaN outputs AND
+// sets the workspace's RAVE_SPLITK_STATUS_WORD (sticky), which the owner of the
+// workspace reads back and reports (the engine returns RAVE_ERR_COOP).
 #include "common.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -57,7 +63,7 @@ constexpr int kUSMaxDil = 16;
 #ifndef RAVE_US_RC
 #define RAVE_US_RC 6                // weight ring depth of the cooperative form (4 waves per CU)
 #endif
-constexpr unsigned kUSSpinLimit = 1u << 18;   // cooperative seam: bounded poll (give-up -> NaN outputs)
+constexpr unsigned kUSSpinLimit = 1u << 18;   // cooperative seam: bounded poll (give-up -> status word + NaN)
 template <int V> struct IC {
     static constexpr int value = V;
 };
@@ -78,6 +84,8 @@ __device__ unsigned long long* g_us_stamps = nullptr;
     } while (0)
 #endif
 constexpr unsigned kUSOOB = 0xFFFFFFF0u;
+constexpr int kXcds = 8;                      // gfx950: blocks dealt round-robin over 8 XCDs
+constexpr int kCoopNoFit = 1;                 // us_launch: a group does not fit one XCD
 
 struct USArgs {
     const float* x; float* y; const float* w; const float* rs1; const float* rs2;
@@ -95,6 +103,9 @@ struct USArgs {
     int xv;                  // 16-byte window loads (T % 4 == 0, 16-byte aligned rows)
     unsigned nb_magic;       // ceil(2^24 / window blocks per row)
     int flag_stride;         // counter words per group (cooperative form)
+    unsigned* status;        // optional caller's give-up word (host-mapped: system scope)
+    unsigned spin_limit;     // polls before a member gives up (rave_debug_coop)
+    int force_giveup;        // debug: every group reports a give-up after a normal hand-off
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t us_rsrc(const void* p, int bytes) {
@@ -607,17 +618,21 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
                 const unsigned n = __builtin_amdgcn_readfirstlane(
                     __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                 if (n >= (unsigned)RB) break;
-                if (++spins > kUSSpinLimit) {
+                if (++spins > a.spin_limit) {
                     ok = false;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
+            if (a.force_giveup) ok = false;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) {
                 vote[0] = ok ? 0 : 1;
-                if (!ok) __hip_atomic_store(a.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!ok) {
+                    __hip_atomic_store(a.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         }
         __syncthreads();
@@ -772,6 +787,20 @@ static int us_launch(USArgs k, int B, bool snake, bool f32, hipStream_t st) {
     }
     int grid = k.ntiles * B;
     if constexpr (RB > 1) {
+        // forward progress needs a whole group resident on one XCD at once:
+        // RB workgroups of this geometry must fit that XCD's CUs (else the
+        // caller runs the one-workgroup form)
+        static int fits[4] = {-1, -1, -1, -1};
+        int& f = fits[2 * f32 + snake];
+        if (f < 0) {
+            int per_cu = 0, dev = 0, cus = 0;
+            RAVE_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern),
+                                                                        G::NT, G::LDS));
+            RAVE_CHECK_HIP(hipGetDevice(&dev));
+            RAVE_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            f = (int64_t)per_cu * (cus / kXcds) >= RB ? 1 : 0;
+        }
+        if (!f) return kCoopNoFit;
         k.ngroups = grid;
         grid = ceil_div(grid, 8) * 8 * RB;          // whole groups per XCD slot
     }
@@ -869,6 +898,9 @@ extern "C" int rave_diag_unit_stamps(void* p) {
 #endif
 
 namespace rave {
+// debug overrides of the cooperative hand-off (rave_debug_coop)
+static std::atomic<unsigned> g_coop_spin{kUSSpinLimit};
+static std::atomic<int> g_coop_force{0};
 // Cooperative form (header comment): C = 256 and 512, groups of C/128 workgroups
 // over 32-column slabs.  RAVE_UNIT_COOP=0 keeps one workgroup per slab (A/B).
 static bool coop_enabled() {
@@ -891,10 +923,10 @@ static CoopLayout coop_layout(const rave_unit_args& a) {
     const int64_t ng = (int64_t)ceil_div(a.t_len, kCoopBN) * a.batch;
     const int64_t ngp = ceil_div64(ng, 8) * 8;
     // counters live in the split-K ticket words (zero at rest, as the conv
-    // kernels leave theirs); the last ticket word is the give-up word
-    if (2 * ngp > RAVE_SPLITK_TICKETS - 1) return L;
+    // kernels leave theirs); the reserved last word is the give-up word
+    if (2 * ngp > RAVE_SPLITK_STATUS_WORD) return L;
     // a group's counters on a 128-byte line of their own where the words allow
-    while (L.stride < 32 && 2 * L.stride * ngp <= RAVE_SPLITK_TICKETS - 1) L.stride *= 2;
+    while (L.stride < 32 && 2 * L.stride * ngp <= RAVE_SPLITK_STATUS_WORD) L.stride *= 2;
     const int rb = C / 128;
     L.groups = ng;
     L.xmax = RAVE_SPLITK_TICKETS;
@@ -947,12 +979,17 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
     if (L.rb > 1 && a.workspace) {
         k.flag_stride = L.stride;
         k.flags = reinterpret_cast<unsigned*>(a.workspace);
-        k.tmo = k.flags + RAVE_SPLITK_TICKETS - 1;
+        k.tmo = k.flags + RAVE_SPLITK_STATUS_WORD;
+        k.status = a.status;
+        k.spin_limit = g_coop_spin.load(std::memory_order_relaxed);
+        k.force_giveup = g_coop_force.load(std::memory_order_relaxed);
         k.xmax = a.workspace + L.xmax;
         k.xch = a.workspace + L.xch;
         k.xch_bytes = (int)((L.floats - L.xch) * 4);
-        if (C == 256) return go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<2>{});
-        return go(IC<512>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<4>{});
+        const int rc = C == 256 ? go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<2>{})
+                                : go(IC<512>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<4>{});
+        if (rc != kCoopNoFit) return rc;
+        // (a group does not fit one XCD: the one-workgroup form below)
     }
     // (K-groups, KG = 2, measured slower for every C: 13.3/11.6/19.5 -> 16.8/12.0/21.5 us)
     // (WGN, CB) per C, measured (tools/layer_bench.py unit_*): C=256 with one
@@ -980,6 +1017,14 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
 }
 
 }  // namespace rave
+
+extern "C" int rave_debug_coop(int64_t spin_limit, int force_giveup) {
+    rave::g_coop_spin.store(spin_limit < 0 ? rave::kUSSpinLimit
+                                           : (unsigned)std::min<int64_t>(spin_limit, 0xFFFFFFFFll),
+                            std::memory_order_relaxed);
+    rave::g_coop_force.store(force_giveup ? 1 : 0, std::memory_order_relaxed);
+    return RAVE_OK;
+}
 
 extern "C" int64_t rave_unit_workspace(const rave_unit_args* a) {
     RAVE_CHECK_ARG(a, "unit_workspace: null pointer");

@@ -100,6 +100,15 @@ class RAVE:
             N.lib.rave_model_destroy(h)
             self.handle = None
 
+    # ------------------------------------------------------------ status
+    def check(self, wait: bool = True) -> None:
+        """Raise ``NativeError`` if a cooperative residual unit's in-launch
+        hand-off gave up in a call that has run (its outputs are NaN); with
+        ``wait`` the device's current stream is synchronised first, so every
+        queued call is covered (rave_model_check).  encode / decode / forward
+        also raise pending give-ups when they are called."""
+        N.check(N.lib.rave_model_check(self.handle, int(bool(wait)), _stream(self.device)), "check")
+
     # ------------------------------------------------------------ tuning
     def tuning(self) -> list:
         """The autotuner's choices so far, JSON-serialisable; pass it back as

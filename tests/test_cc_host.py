@@ -11,7 +11,7 @@ from rave_amd.modules import DilatedUnit, RAVEModules, Residual, load_reference_
 from rave_amd.weights import init_params, init_speaker
 
 
-@pytest.mark.parametrize("name", ["v2", "causal", "discrete"])
+@pytest.mark.parametrize("name", ["v2", "causal", "discrete", "v3", "v3_noise"])
 def test_tree_names_match_reference_state_dict(name):
     cfg = rcfg.get_config(name, capacity=8)
     m = RAVEModules(cfg, init_speaker(cfg, 0))
@@ -22,16 +22,20 @@ def test_tree_names_match_reference_state_dict(name):
             continue
         expected.add(k[:-len("_g")] if k.endswith(".weight_g") else k)
     expected = {k for k in expected if not k.endswith(".weight_v")}
-    own = {k for k in m.state_dict() if k not in ("speaker", "pqmf.hk")}
+    buffers = {k for k, _ in m.named_buffers()}
+    own = {k for k in m.state_dict() if k not in ("speaker", "pqmf.hk") and k not in buffers}
     assert own == expected, (sorted(own - expected)[:4], sorted(expected - own)[:4])
+    if cfg.adain:   # AdaIN buffers under the reference's names (rave/blocks.py:858-868)
+        assert "encoder.encoder.net.1.mean_x" in buffers and "decoder.net.3.num_update_y" in buffers
     load_reference_state(m, params)
 
 
+@pytest.mark.parametrize("name", ["causal", "v3_noise"])
 @pytest.mark.parametrize("cached", [False, True])
-def test_tree_scripts(cached):
+def test_tree_scripts(cached, name):
     cc.use_cached_conv(cached)
     try:
-        m = RAVEModules(rcfg.causal(capacity=8))
+        m = RAVEModules(rcfg.get_config(name, capacity=8))
     finally:
         cc.use_cached_conv(False)
     ts = torch.jit.script(m)

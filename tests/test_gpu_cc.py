@@ -143,3 +143,130 @@ def test_cc_conv_module_contract(dev):
     assert maxabs(ct(x).detach().cpu().numpy(), refc) < 1e-5
     with pytest.raises(NotImplementedError):
         cc.ConvTranspose1d(16, 8, 5, stride=2, padding=1)
+
+
+def _set_adain(m, lx, ly, reset=False):
+    """nn~'s learn / reset attributes on every AdaIN module (eager or scripted):
+    the reference's buffer names (rave/blocks.py:858-884)."""
+    vals = {"learn_x": float(lx), "learn_y": float(ly)}
+    if reset:
+        vals.update(mean_x=0.0, std_x=1.0, num_update_x=0.0, mean_y=0.0, std_y=1.0, num_update_y=0.0)
+    n = 0
+    for name, buf in m.named_buffers():
+        leaf = name.rsplit(".", 1)[-1]
+        if leaf in vals and (".net." in name or name.startswith("net.")):
+            buf.fill_(vals[leaf])
+            n += leaf == "learn_x"
+    assert n > 0
+
+
+@pytest.mark.parametrize("precision", ["f32", "split16"])
+def test_cc_v3_noise_tree_per_layer_golden(dev, golden, precision):
+    """The v3 tree with AdaIN, Snake and NoiseGeneratorV2 (capacity 8) on the
+    operator seam, every conv against the reference's per-layer outputs
+    (tests/golden/v3_noise_small_layers.npz: the residual convs, the noise
+    module's three convs, the waveform module), z and y within 1e-4 with the
+    reference's uniform noise injected; the scripted tree equal."""
+    from rave_amd import cc
+    from rave_amd import config as rcfg
+    cfg = rcfg.v3_noise(capacity=8)
+    g = golden("v3_noise_small_layers")
+    m = _tree(cfg, g, golden, dev, precision=precision)
+    got = {}
+    hooks = [mod.register_forward_hook(lambda mod, i, o, n=n: got.__setitem__(n, o.detach().cpu().numpy()))
+             for n, mod in m.named_modules() if isinstance(mod, (cc.Conv1d, cc.ConvTranspose1d))]
+    u = torch.from_numpy(g["noise_u"]).to(dev)
+    with torch.no_grad():
+        z = m.encode(torch.from_numpy(g["x"]).to(dev))
+        y = m.decode(torch.from_numpy(g["z"]).to(dev), u)
+    for h in hooks:
+        h.remove()
+    layers = [k[len("layer/"):] for k in g if k.startswith("layer/")]
+    assert {"decoder.noise_module.net.4", "decoder.waveform_module"} <= set(layers)
+    assert layers and set(layers) <= set(got), sorted(set(layers) - set(got))[:5]
+    worst = 0.0
+    for name in layers:
+        ref = g["layer/" + name]
+        err = maxabs(got[name], ref)
+        worst = max(worst, err / max(1.0, float(np.abs(ref).max())))
+        assert err <= 2e-5 * max(1.0, float(np.abs(ref).max())), (name, err)
+    ez = maxabs(z.cpu().numpy()[:, :cfg.latent_size], g["z"][:, :cfg.latent_size])
+    ey = maxabs(y.cpu().numpy(), g["y"])
+    print(f"\n[cc] v3+noise cap 8 {precision}: {len(layers)} layers, worst rel {worst:.2e}; z {ez:.2e} y {ey:.2e}")
+    assert ez < TOL and ey < TOL
+    ts = torch.jit.script(m)
+    with torch.no_grad():
+        ys = ts.decode(torch.from_numpy(g["z"]).to(dev), u)
+    assert maxabs(ys.cpu().numpy(), y.cpu().numpy()) == 0.0
+
+
+@pytest.mark.parametrize("fixture,causal", [("v3_noise_causal_stream", True), ("v3_noise_stream", False)])
+def test_cc_cached_v3_noise_tree_streams_reference(dev, golden, fixture, causal):
+    """cc.use_cached_conv(True): the v3 + noise + AdaIN tree (capacity 16),
+    scripted, streams 2048-sample blocks against the reference's cached_conv
+    run block for block, AdaIN learning the target, then the source, then
+    transferring (nn~'s learn flags switched between blocks), the reference's
+    per-block uniform noise injected."""
+    from rave_amd import config as rcfg
+    cfg = rcfg.v3_noise(causal=causal, capacity=16)
+    g = golden(fixture)
+    m = torch.jit.script(_tree(cfg, g, golden, dev, cached=True))
+    blk = int(g["block"])
+    Fz = blk // cfg.hop
+    x = torch.from_numpy(g["x"]).to(dev)
+    z = torch.from_numpy(g["z"]).to(dev)
+    u = torch.from_numpy(g["noise_u"]).to(dev)
+    zs, ys = [], []
+    with torch.no_grad():
+        for i, (lx, ly) in enumerate(g["flags"]):
+            _set_adain(m, lx, ly)
+            zs.append(m.encode(x[..., i * blk:(i + 1) * blk]))
+        _set_adain(m, 0, 0, reset=True)
+        for i, (lx, ly) in enumerate(g["flags"]):
+            _set_adain(m, lx, ly)
+            ys.append(m.decode(z[..., i * Fz:(i + 1) * Fz], u[i]))
+    ez = maxabs(torch.cat(zs, -1).cpu().numpy(), g["z_stream"])
+    ey = maxabs(torch.cat(ys, -1).cpu().numpy(), g["y_stream"])
+    print(f"\n[cc] cached v3+noise+AdaIN tree ({'causal' if causal else 'centred'}) vs reference: z {ez:.2e} y {ey:.2e}")
+    assert ez < TOL and ey < TOL
+
+
+def test_cc_adain_modes_match_reference_semantics(dev):
+    """AdaptiveInstanceNormalization on rave_adain against the reference's eval
+    forward restated in torch fp64 (rave/blocks.py:886-919): learn_y updates the
+    y statistics and passes x through, learn_x updates the x statistics and
+    then transfers (once both counters are set), batch rows [:bs] only."""
+    from rave_amd.modules import AdaptiveInstanceNormalization
+    C, T = 16, 300
+    m = AdaptiveInstanceNormalization(C).to(dev).eval()
+    r = {k: v.clone().double() for k, v in m.state_dict().items()}
+
+    def ref_forward(x):
+        bs = x.shape[0]
+        if r["learn_y"].item():
+            for k, v in (("mean_y", x.mean(-1, keepdim=True)), ("std_y", x.std(-1, keepdim=True))):
+                r[k][:bs] += (v - r[k][:bs]) / (r["num_update_y"] + 1)
+            r["num_update_y"] += 1
+            return x
+        if r["learn_x"].item():
+            for k, v in (("mean_x", x.mean(-1, keepdim=True)), ("std_x", x.std(-1, keepdim=True))):
+                r[k][:bs] += (v - r[k][:bs]) / (r["num_update_x"] + 1)
+            r["num_update_x"] += 1
+        if r["num_update_x"].item() and r["num_update_y"].item():
+            x = (x - r["mean_x"][:bs]) / (r["std_x"][:bs] + 1e-5) * r["std_y"][:bs] + r["mean_y"][:bs]
+        return x
+
+    gen = torch.Generator().manual_seed(3)
+    for step, (lx, ly, bs) in enumerate([(0, 1, 3), (0, 1, 3), (1, 0, 3), (1, 0, 2), (0, 0, 3)]):
+        for t in (m, ):
+            t.learn_x.fill_(lx)
+            t.learn_y.fill_(ly)
+        r["learn_x"].fill_(lx)
+        r["learn_y"].fill_(ly)
+        x = (torch.randn(bs, C, T, generator=gen) * (1 + step) + step).to(dev)
+        with torch.no_grad():
+            y = m(x)
+        ref = ref_forward(x.cpu().double())
+        assert maxabs(y.cpu().numpy(), ref.numpy()) < 1e-4, step
+        for k in ("mean_x", "std_x", "mean_y", "std_y", "num_update_x", "num_update_y"):
+            assert maxabs(getattr(m, k).cpu().numpy(), r[k].numpy()) < 1e-5, (step, k)

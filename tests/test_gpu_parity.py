@@ -241,6 +241,44 @@ def test_pqmf_golden(N, dev, golden, causal, precision):
     assert maxabs(out.cpu().numpy(), ref_s) <= 1e-5 * max(1, np.abs(ref_s).max())
 
 
+@pytest.mark.parametrize("precision", ["f32", "split16"])
+@pytest.mark.parametrize("causal", [False, True])
+def test_pqmf_roundtrip_golden(N, dev, golden, causal, precision):
+    """PQMF round trip on the GPU: rave_pqmf_analysis of the fixture audio,
+    then rave_pqmf_synthesis of those device-resident bands (CachedPQMF.forward
+    then .inverse, rave/pqmf.py:269-284), against the reference's own
+    ``roundtrip_{centered,causal}`` outputs, in both arithmetics.  (The fused
+    path edges carry a conv between the two filterbanks, so they have no pure
+    round trip; tests/test_gpu_edges.py checks them against the oracle.)"""
+    prec = N.PRECISION[precision]
+    from oracle.rave_oracle import get_padding
+    from rave_amd.pqmf import kernels
+    g = golden("pqmf")
+    mode = "causal" if causal else "centered"
+    hkf, hki = kernels(g["hk"])
+    hkf_d, hki_d = torch.from_numpy(hkf).to(dev), torch.from_numpy(hki).to(dev)
+    x = torch.from_numpy(g["x"]).to(dev)
+    B, _, T = x.shape
+    F = T // 16
+    bands = torch.empty(B, 16, F, device=dev)
+    out = torch.full((B, 1, T), float("nan"), device=dev)
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    a = N.AnalysisArgs(n_band=16, taps=hkf.shape[-1], n_out_bands=16, batch=B, t_in=T,
+                       pad_left=get_padding(hkf.shape[-1], causal=causal)[0], t_out=F, x=x.data_ptr(), x_sb=T,
+                       y=bands.data_ptr(), y_sb=16 * F, y_sc=F, hkf=hkf_d.data_ptr(), precision=prec)
+    N.check(N.lib.rave_pqmf_analysis(C.byref(a), st))
+    s_ = N.SynthesisArgs(n_band=16, taps=hki.shape[-1], batch=B, t_in=F,
+                         pad_left=get_padding(hki.shape[-1], causal=causal)[0], mode=0, frame0=0, x_len=0,
+                         x=bands.data_ptr(), x_sb=16 * F, x_sc=F, y=out.data_ptr(), y_sb=T,
+                         hki=hki_d.data_ptr(), precision=prec)
+    N.check(N.lib.rave_pqmf_synthesis(C.byref(s_), st))
+    torch.cuda.synchronize()
+    ref = g[f"roundtrip_{mode}"]
+    got = out.cpu().numpy()
+    assert np.isfinite(got).all()
+    assert maxabs(got, ref) <= 1e-5 * max(1, np.abs(ref).max())
+
+
 @pytest.mark.parametrize("case", [
     # (B, frames, mode, noise, pad, x_len, frame0, n_out)  -- offline and streaming shapes
     (3, 300, 1, True, 16, 0, 0, 6), (2, 257, 2, True, 32, 0, 0, 16), (1, 2, 1, False, 0, 34, -32, 6),
