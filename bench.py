@@ -94,15 +94,19 @@ def op_family(kind: int, precision: int) -> str:
     return "other"
 
 
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "traffic.json")
+# committed PMC traffic per arithmetic mode (tools/profile_round.sh -> tools/rocprof_summary.py)
+TRAFFIC_FILES = {"auto": os.path.join(REPO, "profiles", "traffic.json"),
+                 "f32_tuned": os.path.join(REPO, "profiles", "traffic_f32_tuned.json")}
 
 
 def traffic_per_launch(config: str, B: int, T: int, precision: str):
     """HBM bytes per op launch, per kernel family, from the committed rocprofv3
     PMC passes (tools/profile_round.sh -> tools/rocprof_summary.py), for this
     exact workload and precision only; None otherwise."""
+    if precision not in TRAFFIC_FILES:
+        return None
     try:
-        with open(TRAFFIC_FILE) as fh:
+        with open(TRAFFIC_FILES[precision]) as fh:
             t = json.load(fh)
     except (OSError, ValueError):
         return None
@@ -523,8 +527,8 @@ def main():
         }
         if exact and exact.get("roofline"):       # keep the exact-fp32 line compact
             r = exact["roofline"]
-            exact["roofline"] = {k: r[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel",
-                                                   "all_gemm_ops")}
+            exact["roofline"] = {k: r[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                   "kernel", "all_gemm_ops")}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -524,18 +524,31 @@ static bool f32_tile_ok(int ti, int M, int split_row) {
 }
 
 // The launch configuration: args.config when set (validated), else the heuristic.
-static int resolve(const rave_conv1d_args& a, const ConvKArgs& k, LaunchCfg& c) {
+static int resolve(const rave_conv1d_args& a, const ConvKArgs& k, int taps, LaunchCfg& c) {
     if (a.config == 0) {
         c = choose(k.M, k.U, k.B, k.nchunks, k.split_row);
         return RAVE_OK;
     }
     ConfigCode cc;
-    RAVE_CHECK_ARG(decode_config(a.config, cc) && cc.sep == 0 && f32_tile_ok(cc.tile, k.M, k.split_row) &&
+    const bool dec = decode_config(a.config, cc);
+    if (dec && is_gemv_tile(cc.tile)) {   // the skinny-N family (conv_gemv.hip)
+        RAVE_CHECK_ARG(split_count_distinct(cc.S, k.nchunks) && (cc.S > 1 || !cc.sep) &&
+                           gemv_fits(taps, k.U, k.d, k.transposed != 0, ceil_div(k.nchunks, cc.S),
+                                     gemv_nmax(cc.tile)),
+                       "conv1d: gemv config not valid for these args (see rave_conv1d_configs)");
+        c = {0, gemv_nmax(cc.tile), cc.S};
+        c.sep = cc.sep;
+        return RAVE_OK;
+    }
+    RAVE_CHECK_ARG(dec && cc.sep == 0 && f32_tile_ok(cc.tile, k.M, k.split_row) &&
                        split_count_distinct(cc.S, k.nchunks),
                    "conv1d: config not valid for these args (see rave_conv1d_configs)");
     c = {kF32Tiles[cc.tile][0], kF32Tiles[cc.tile][1], cc.S};
     return RAVE_OK;
 }
+
+// K-split counts of the gemv family (more than the MFMA tiles': its row tiles are few)
+constexpr int kGemvSplits[] = {1, 2, 4, 8, 16, 32};
 
 extern "C" int rave_conv1d_configs(const rave_conv1d_args* p, int32_t* cfgs, int max_cfgs) {
     RAVE_CHECK_ARG(p && max_cfgs >= 0, "conv1d_configs: null args");
@@ -557,6 +570,25 @@ extern "C" int rave_conv1d_configs(const rave_conv1d_args* p, int32_t* cfgs, int
             ++n;
         }
     }
+    // skinny-N (gemv) configurations: the smallest column width holding U
+    if (k.U <= kGemvMaxN) {
+        int nmax = 4, tile = 8;
+        while (nmax < k.U) nmax *= 2, ++tile;
+        const int64_t tiles = (int64_t)ceil_div(k.M, 256) * k.B;
+        for (int S : kGemvSplits) {
+            if (!split_count_distinct(S, k.nchunks) || tiles * S > 2048 ||
+                !gemv_fits(taps, k.U, k.d, k.transposed != 0, ceil_div(k.nchunks, S), nmax))
+                continue;
+            if (S == 1 || tiles <= kSplitTicketsUsable) {
+                if (n < max_cfgs && cfgs) cfgs[n] = encode_config(tile, S, 0);
+                ++n;
+            }
+            if (S > 1) {
+                if (n < max_cfgs && cfgs) cfgs[n] = encode_config(tile, S, 1);
+                ++n;
+            }
+        }
+    }
     return n;
 }
 
@@ -568,7 +600,7 @@ extern "C" int64_t rave_conv1d_workspace(const rave_conv1d_args* p) {
     int taps;
     if (prepare(*p, k, taps) != RAVE_OK) return -1;
     LaunchCfg c;
-    if (resolve(*p, k, c) != RAVE_OK) return -1;
+    if (resolve(*p, k, taps, c) != RAVE_OK) return -1;
     if (c.S <= 1) return 0;
     return kSplitTickets + (int64_t)c.S * k.B * (int64_t)k.M * k.U;   // same layout as the split path
 }
@@ -582,12 +614,20 @@ extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
     int rc = prepare(*p, k, taps);
     if (rc != RAVE_OK) return rc;
     LaunchCfg c;
-    rc = resolve(*p, k, c);
+    rc = resolve(*p, k, taps, c);
     if (rc != RAVE_OK) return rc;
     if (c.S > 1 && p->partial == nullptr) c.S = 1;   // no workspace given: single pass
     k.cps = ceil_div(k.nchunks, c.S);
     k.S = ceil_div(k.nchunks, k.cps);                 // no empty splits
     k.partial = p->partial ? p->partial + kSplitTickets : nullptr;   // slabs after the counters
+    if (c.bm == 0) {                                  // skinny-N family (tickets ahead of the slabs)
+        k.tickets = reinterpret_cast<int*>(p->partial);
+        if (!gemv_fits(taps, k.U, k.d, k.transposed != 0, k.cps, c.bn)) {
+            set_error("conv1d(gemv): one K split's window exceeds the staging area (give the workspace)");
+            return RAVE_ERR_UNSUPPORTED;
+        }
+        return conv1d_gemv(k, taps, c.bn, c.sep, as_stream(stream));
+    }
 #ifdef RAVE_STAMPS
     k.stamps = p->stamps;
 #endif

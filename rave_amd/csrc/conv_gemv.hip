@@ -1,0 +1,253 @@
+// Skinny-N convolution ("GEMV" family) in exact fp32 on the VALU: the cached
+// streaming convs at batch 1 (BASELINE configs[2], cached_conv's
+// CachedConv1d / CachedConvTranspose1d at every call site of rave/blocks.py:
+// DilatedUnit :96-106, EncoderV2 :533-584, GeneratorV2 :631-677) produce 2-32
+// output frames per call while reading the layer's whole weight matrix.  The
+// column-tiled MFMA kernels give such a layer a handful of workgroups, each
+// streaming a large share of the weights through one CU.  Here the weight
+// matrix is spread over the whole chip instead:
+//
+//   Y[m, n] = sum_kk W[m, kk] act(X)[kk, n] (+ bias, + residual)   n < U <= NMAX
+//
+//   * grid = (256-row tiles) x (K splits) x batch; a workgroup reads its rows'
+//     share of W exactly once, straight from the exact-fp32 packed image of
+//     conv1d.hip ([chunk][tap][channel][Mpad]: each K-row is Mpad contiguous
+//     floats), one 16-byte load per lane per K-row (lane = 4 consecutive rows,
+//     a wave covers 256 rows: fully coalesced);
+//   * the split's input window (its channels x the U output columns' reach) is
+//     staged once in LDS with the activation applied; every lane reads the
+//     same x values (LDS broadcast) and keeps 4 x NMAX fp32 accumulators
+//     (packed v_pk_fma_f32 over column pairs);
+//   * the 4 waves take interleaved channels of every chunk and are summed
+//     through LDS in wave order; K splits over workgroups write fp32 slabs that
+//     the last-arriving split sums in split order (or a separate reduce launch)
+//     -- fixed orders, bitwise reproducible, no float atomics.
+// ConvTranspose1d runs in conv1d.hip's polyphase form (rows m = (co, phase q),
+// 2 taps, phase group 1 one input column later).
+#include "conv_shared.h"
+
+namespace rave {
+
+typedef float g_f32x2 __attribute__((ext_vector_type(2)));
+typedef float g_f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kGemvRows = 256;                     // GEMM rows per workgroup (64 lanes x 4)
+constexpr int kGemvStage = 12288;                  // staged window floats per workgroup (48 KiB)
+
+// (channels per packed chunk, stride) of conv1d.hip's exact-fp32 families
+template <int KT> struct GFam;
+template <> struct GFam<1> { static constexpr int CIT = 32, ST = 1; };
+template <> struct GFam<2> { static constexpr int CIT = 32, ST = 1; };
+template <> struct GFam<3> { static constexpr int CIT = 16, ST = 1; };
+template <> struct GFam<4> { static constexpr int CIT = 16, ST = 2; };
+template <> struct GFam<7> { static constexpr int CIT = 8, ST = 1; };
+template <> struct GFam<8> { static constexpr int CIT = 8, ST = 4; };
+
+// window columns a split stages: every output column's reach, plus one column
+// for ConvT phase group 1 (its taps start one input column later)
+__host__ __device__ inline int gemv_xw(int KT, int ST, int U, int d, bool transposed) {
+    return (U - 1) * ST + (KT - 1) * d + 1 + (transposed ? 1 : 0);
+}
+
+template <int KT, int NMAX, bool SNAKE>
+__global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
+    constexpr int CIT = GFam<KT>::CIT, ST = GFam<KT>::ST, NP = NMAX / 2;
+    constexpr unsigned kOOB = 0xFFFFFFF0u;
+    extern __shared__ __attribute__((aligned(16))) float gsm[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int MT = ceil_div(a.M, kGemvRows);
+    // splits of one row tile on consecutive blocks of one XCD (blocks b, b+8, ...)
+    int lg = blockIdx.x;
+    if ((gridDim.x & 7) == 0) lg = (lg & 7) * (gridDim.x >> 3) + (lg >> 3);
+    lg = __builtin_amdgcn_readfirstlane(lg);
+    const int split = lg % a.S;
+    const int tile = lg / a.S;                       // b * MT + mt (ticket index)
+    const int mt = tile % MT, b = tile / MT;
+    const int m0 = mt * kGemvRows;
+    const int c_begin = split * a.cps, c_end = min(a.nchunks, c_begin + a.cps);
+    const int nch = (c_end - c_begin) * CIT;         // staged channels
+    const int U = a.U, XW = a.XW;
+    const int t0 = -a.pad_l;                         // input time of window column 0
+    const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
+
+    // ---------------------------------------------------------------- window
+    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);
+    for (int e = tid; e < nch * XW; e += 256) {
+        const int cl = e / XW, w = e - cl * XW;
+        const int ci = c_begin * CIT + cl, t = t0 + w;
+        const bool ok = ci < a.c_in && t >= 0 && t < a.t_in;
+        float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+            xrs, ok ? (unsigned)(ci * a.x_sc + t) * 4u : kOOB, 0, 0));
+        if constexpr (SNAKE) {
+            const float al = a.alpha[min(ci, a.c_in - 1)];
+            v = v + (1.0f / (al + 1e-9f)) * sin_squared(al * v);
+        } else {
+            v = v > 0.f ? v : v * slope;
+        }
+        gsm[cl * XW + w] = ok ? v : 0.f;
+    }
+    __syncthreads();
+
+    // ---------------------------------------------------------------- K loop
+    // lane: rows m0 + 4 lane .. + 3; ConvT rows of phase group 1 read one column later
+    const int mrow = m0 + 4 * lane;
+    const int goff = (a.transposed && mrow >= a.split_row) ? 1 : 0;
+    const bool rows_ok = mrow < a.Mpad;
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, a.w_bytes);
+    g_f32x2 acc[4][NP];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) acc[r][p] = g_f32x2{0.f, 0.f};
+    for (int c = c_begin; c < c_end; ++c) {
+#pragma unroll
+        for (int j = 0; j < KT; ++j) {
+            const int col0 = goff + j * a.d;
+            // this wave's channels of the chunk: wave, wave + 4, ...
+#pragma unroll 2
+            for (int cl = wave; cl < CIT; cl += 4) {
+                const unsigned kk = (unsigned)((c * KT + j) * CIT + cl);
+                const g_f32x4 w4 = __builtin_bit_cast(g_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                    wrs, rows_ok ? (kk * (unsigned)a.Mpad + (unsigned)mrow) * 4u : kOOB, 0, 0));
+                const float* xr = gsm + ((c - c_begin) * CIT + cl) * XW + col0;
+#pragma unroll
+                for (int p = 0; p < NP; ++p) {
+                    const g_f32x2 xv = {xr[(2 * p) * ST], xr[(2 * p + 1) * ST]};
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[r][p] = __builtin_elementwise_fma(g_f32x2{w4[r], w4[r]}, xv, acc[r][p]);
+                }
+            }
+        }
+    }
+    __syncthreads();                                  // window dead: the reduction area
+
+    // ---------------------------------------------------------------- wave sum (fixed order)
+    float* red = gsm;                                 // [wave][row 0..255][NMAX]
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+            *reinterpret_cast<g_f32x2*>(red + ((wave * kGemvRows + 4 * lane + r) * NMAX + 2 * p)) = acc[r][p];
+    __syncthreads();
+    const int m = m0 + tid;                           // this thread's row from here on
+    float v[NMAX];
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) s += red[(w * kGemvRows + tid) * NMAX + n];
+        v[n] = s;
+    }
+
+    // ---------------------------------------------------------------- K splits
+    if (a.S > 1) {
+        const int64_t total = (int64_t)a.B * a.M * U;
+        float* slab = a.partial + (int64_t)split * total + ((int64_t)b * a.M + m) * U;
+        if (m < a.M)
+#pragma unroll
+            for (int n = 0; n < NMAX; ++n)
+                if (n < U) slab[n] = v[n];
+        if (!a.inlaunch) return;                      // a separate reduce launch sums the slabs
+        // in-launch combine: publish with an agent-scope release, draw the row
+        // tile's ticket; the split drawing S - 1 acquires and sums every slab in
+        // split order (conv_split.hip's pattern)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every thread's slab stores performed
+        __syncthreads();
+        __shared__ int last_s;
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            const int prev = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = prev == a.S - 1;
+            if (last) {
+                __hip_atomic_store(a.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+            last_s = last;
+        }
+        __syncthreads();
+        if (!last_s) return;
+        if (m >= a.M) return;
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n) v[n] = 0.f;
+        for (int s = 0; s < a.S; ++s) {
+            const float* sl = a.partial + (int64_t)s * total + ((int64_t)b * a.M + m) * U;
+#pragma unroll
+            for (int n = 0; n < NMAX; ++n)
+                if (n < U) v[n] += sl[n];
+        }
+    }
+    if (m >= a.M) return;
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n)
+        if (n < U) store_out(a, b, m, n, v[n]);
+}
+
+template <int KT, int NMAX>
+static int gemv_go(ConvKArgs k, hipStream_t st) {
+    const int MT = ceil_div(k.M, kGemvRows);
+    const int grid = MT * k.S * k.B;
+    // (+ slack: lanes read all NMAX columns of a window row, the ones past U unused)
+    const size_t lds = (size_t)std::max(ceil_div(k.cps * GFam<KT>::CIT * k.XW, 4) * 4 + NMAX * GFam<KT>::ST + 16,
+                                        4 * kGemvRows * NMAX) * 4;
+    auto kern = k.act == RAVE_ACT_SNAKE ? conv1d_gemv_kernel<KT, NMAX, true> : conv1d_gemv_kernel<KT, NMAX, false>;
+    if (lds > 64 * 1024) {
+        static bool done[2] = {false, false};
+        bool& d = done[k.act == RAVE_ACT_SNAKE];
+        if (!d) {
+            RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            d = true;
+        }
+    }
+    launch(kern, dim3(grid), dim3(256), (uint32_t)lds, st, k);
+    return launch_status("conv1d_gemv_kernel");
+}
+
+template <int KT>
+static int gemv_family(const ConvKArgs& k, int nmax, hipStream_t st) {
+    switch (nmax) {
+        case 4: return gemv_go<KT, 4>(k, st);
+        case 8: return gemv_go<KT, 8>(k, st);
+        case 16: return gemv_go<KT, 16>(k, st);
+        default: return gemv_go<KT, 32>(k, st);
+    }
+}
+
+bool gemv_fits(int taps, int U, int d, bool transposed, int cps, int nmax) {
+    if (U > nmax || nmax > kGemvMaxN) return false;
+    const int cit = taps == 1 || taps == 2 ? 32 : taps == 3 || taps == 4 ? 16 : 8;
+    const int st = taps == 4 ? 2 : taps == 8 ? 4 : 1;
+    return (int64_t)cps * cit * gemv_xw(taps, st, U, d, transposed) <= kGemvStage;
+}
+
+int conv1d_gemv(ConvKArgs k, int taps, int nmax, int sep, hipStream_t st) {
+    const int cit = taps == 1 || taps == 2 ? 32 : taps == 3 || taps == 4 ? 16 : 8;
+    const int stv = taps == 4 ? 2 : taps == 8 ? 4 : 1;
+    (void)cit;
+    k.XW = gemv_xw(taps, stv, k.U, k.d, k.transposed != 0);
+    if (!gemv_fits(taps, k.U, k.d, k.transposed != 0, k.cps, nmax)) {
+        set_error("conv1d(gemv): window of one K split exceeds the staging area, or too many columns");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    const int tiles = ceil_div(k.M, kGemvRows) * k.B;
+    k.inlaunch = (k.S > 1 && !sep && k.partial && tiles <= kSplitTicketsUsable) ? 1 : 0;
+    RAVE_CHECK_ARG(k.S <= 1 || k.partial, "conv1d(gemv): K splits need the workspace");
+    int rc;
+    switch (taps) {
+        case 1: rc = gemv_family<1>(k, nmax, st); break;
+        case 2: rc = gemv_family<2>(k, nmax, st); break;
+        case 3: rc = gemv_family<3>(k, nmax, st); break;
+        case 4: rc = gemv_family<4>(k, nmax, st); break;
+        case 7: rc = gemv_family<7>(k, nmax, st); break;
+        case 8: rc = gemv_family<8>(k, nmax, st); break;
+        default: set_error("conv1d(gemv): unsupported kernel size"); return RAVE_ERR_UNSUPPORTED;
+    }
+    if (rc != RAVE_OK || k.S <= 1 || k.inlaunch) return rc;
+    const int64_t total = (int64_t)k.B * k.M * k.U;
+    const int blocks = (int)std::min<int64_t>(ceil_div64(total, 256), 4096);
+    launch(conv1d_splitk_reduce_kernel<1>, dim3(blocks), dim3(256), 0, st, k);
+    return launch_status("conv1d_splitk_reduce_kernel");
+}
+
+}  // namespace rave

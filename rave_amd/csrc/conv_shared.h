@@ -116,7 +116,17 @@ static inline int convt_group1_row(int c_out, int R, int q0) {
 
 struct LaunchCfg {
     int bm, bn, S;
+    int sep = 0;          // gemv (bm == 0, bn = NMAX): the K-split slabs summed by a separate launch
 };
+
+// Skinny-N fp32 family (conv_gemv.hip): weights spread over the chip, all
+// output columns (U <= NMAX) per workgroup.  Launch-config tiles 8..11 of the
+// exact-fp32 precision select it with NMAX = 4 << (tile - 8).
+constexpr int kGemvMaxN = 32;
+inline bool is_gemv_tile(int t) { return t >= 8 && t <= 11; }
+inline int gemv_nmax(int t) { return 4 << (t - 8); }
+bool gemv_fits(int taps, int U, int d, bool transposed, int cps, int nmax);
+int conv1d_gemv(ConvKArgs k, int taps, int nmax, int sep, hipStream_t st);
 
 // rave_conv1d_args.config: 0 = heuristic, else 1 + tile + 16 (S - 1) + 512 sep
 // (tile: index into the precision's tile table; S: K-splits; sep: split-K

@@ -25,6 +25,21 @@ def dev():
     return torch.device("cuda:0")
 
 
+def _conv_hooks(m, got):
+    """Forward hooks recording every cc conv's output under its module name.  A
+    conv that carries its Residual's sum in its epilogue (``forward(h,
+    residual, ...)``: each DilatedUnit's last conv) reports the conv alone --
+    output minus the residual it was given -- which is what the reference's
+    hook on that nn.Conv1d saw (rave/blocks.py:44-46 adds after the module)."""
+    from rave_amd import cc
+
+    def hook(mod, i, o, n):
+        r = i[1] if len(i) > 1 else None
+        got[n] = (o - r if r is not None else o).detach().cpu().numpy()
+    return [mod.register_forward_hook(lambda mod, i, o, n=n: hook(mod, i, o, n))
+            for n, mod in m.named_modules() if isinstance(mod, (cc.Conv1d, cc.ConvTranspose1d))]
+
+
 def _tree(cfg, g, golden, dev, cached=False, precision="f32"):
     from rave_amd import cc
     from rave_amd.modules import RAVEModules, load_reference_state
@@ -45,14 +60,12 @@ def test_cc_tree_per_layer_golden(dev, golden, precision):
     """Every conv of the v2 tree (capacity 8) against the reference's per-layer
     outputs (tests/golden/v2_small_layers.npz, forward hooks on the reference
     modules of the same names); z and y within 1e-4; the scripted tree equal."""
-    from rave_amd import cc
     from rave_amd import config as rcfg
     cfg = rcfg.v2(capacity=8)
     g = golden("v2_small_layers")
     m = _tree(cfg, g, golden, dev, precision=precision)
     got = {}
-    hooks = [mod.register_forward_hook(lambda mod, i, o, n=n: got.__setitem__(n, o.detach().cpu().numpy()))
-             for n, mod in m.named_modules() if isinstance(mod, (cc.Conv1d, cc.ConvTranspose1d))]
+    hooks = _conv_hooks(m, got)
     with torch.no_grad():
         z = m.encode(torch.from_numpy(g["x"]).to(dev))
         y = m.decode(torch.from_numpy(g["z"]).to(dev))
@@ -167,14 +180,12 @@ def test_cc_v3_noise_tree_per_layer_golden(dev, golden, precision):
     (tests/golden/v3_noise_small_layers.npz: the residual convs, the noise
     module's three convs, the waveform module), z and y within 1e-4 with the
     reference's uniform noise injected; the scripted tree equal."""
-    from rave_amd import cc
     from rave_amd import config as rcfg
     cfg = rcfg.v3_noise(capacity=8)
     g = golden("v3_noise_small_layers")
     m = _tree(cfg, g, golden, dev, precision=precision)
     got = {}
-    hooks = [mod.register_forward_hook(lambda mod, i, o, n=n: got.__setitem__(n, o.detach().cpu().numpy()))
-             for n, mod in m.named_modules() if isinstance(mod, (cc.Conv1d, cc.ConvTranspose1d))]
+    hooks = _conv_hooks(m, got)
     u = torch.from_numpy(g["noise_u"]).to(dev)
     with torch.no_grad():
         z = m.encode(torch.from_numpy(g["x"]).to(dev))

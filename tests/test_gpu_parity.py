@@ -193,6 +193,46 @@ def test_conv_every_config(N, dev, case, precision):
         assert np.isfinite(got).all() and err <= 2e-5 * max(1.0, np.abs(ref).max()), (cfg, err)
 
 
+GEMV_CASES = [
+    # c_in, c_out, k, s, d, transposed, act, residual, B, T   -- the streaming shapes (U <= 32)
+    (1024, 64, 3, 1, 1, 0, "leaky", False, 1, 4),
+    (512, 512, 3, 1, 9, 0, "snake", True, 1, 4),
+    (512, 1024, 4, 2, 1, 0, "leaky", False, 1, 8),
+    (128, 256, 8, 4, 1, 0, "snake", False, 2, 128),
+    (1024, 512, 4, 2, 1, 1, "leaky", False, 1, 4),
+    (256, 128, 8, 4, 1, 1, "snake", False, 2, 8),
+    (64, 32, 7, 1, 1, 0, "snake", False, 1, 32),
+    (128, 128, 1, 1, 1, 0, "leaky", True, 1, 32),
+    (320, 1024, 3, 1, 1, 0, "none", False, 1, 2),
+    (96, 200, 3, 1, 3, 0, "leaky", True, 3, 13),
+]
+
+
+@pytest.mark.parametrize("case", GEMV_CASES, ids=[str(c[:8]) for c in GEMV_CASES])
+def test_conv_gemv_configs(N, dev, case):
+    """The skinny-N exact-fp32 family (conv_gemv.hip: weights spread over the
+    chip, all output columns per workgroup), every configuration
+    rave_conv1d_configs lists for it (column width x K splits x in-launch or
+    separate combine), against the float64 oracle at the layer tolerance: k1 /
+    k3 dilated / k7 / strided k4 s2 and k8 s4 / ConvT (both phase groups),
+    LeakyReLU / Snake / none, residual, batch > 1, ragged channel counts."""
+    c_in, c_out, k, s, d, transposed, act, has_res, B, T = case
+    x, w, b, alpha, res, pad, ref = conv_case(case)
+    t_out = ref.shape[-1]
+    a = N.ConvArgs(c_in=c_in, c_out=c_out, kernel=k, stride=s, dilation=d,
+                   pad_left=0 if transposed else pad[0], pad_right=0 if transposed else pad[1],
+                   transposed=transposed, out_shift=s // 2 if transposed else 0, act=N.ACT[act],
+                   batch=B, t_in=T, t_out=t_out, precision=N.PREC_F32, x=16, y=16, weight=16,
+                   alpha=16 if alpha is not None else None, residual=16 if res is not None else None)
+    gemv = [c for c in N.conv_configs(a) if 8 <= ((c - 1) & 15) <= 11]
+    assert gemv, "no skinny-N configurations listed"
+    for cfg in gemv:
+        got = run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act, True,
+                       N.PREC_F32, config=cfg)
+        err = maxabs(got, ref)
+        assert np.isfinite(got).all() and err <= 2e-5 * max(1.0, np.abs(ref).max()), (cfg, err)
+
+
 def test_conv_ring_refuses_unaligned(N, dev):
     """RAVE_PREC_F32_RING refuses rows it cannot DMA in 16-byte pieces (the
     autotuner then keeps the register-staged fp32 kernel for that op)."""
