@@ -284,9 +284,13 @@ def run_mode(a, cfg, params, spk, precision, x, dev, world, rank, log_ops):
     if not torch.isfinite(y).all():
         raise RuntimeError("non-finite output")
     model.check()     # a cooperative-unit give-up in any timed step is an error, not a number
+    # the exchange checked end to end, outside the timed region: every rank's
+    # rows of the gathered latents against that rank's own (raises on mismatch)
+    gather_check = runner.verify(x)
     value = world * B * T * a.steps / el
     res = {"value": round(value, 1), "ms_per_step": round(1e3 * el / a.steps, 4),
-           "x_realtime": round(value / SR, 1), "dtype": DTYPE[precision], "tuning": tuning_info}
+           "x_realtime": round(value / SR, 1), "dtype": DTYPE[precision], "tuning": tuning_info,
+           "gather_check": gather_check}
     if a.pipeline > 1 and world == 1 and precision == a.precision:
         res["pipelined"] = pipelined(a, cfg, params, spk, precision, model, x, dev)
     launches = {}
@@ -520,6 +524,7 @@ def main():
             "per_gpu_samples_per_s": round(head["value"] / world, 1),
             "gemm_launches_by_family": head["gemm_launches_by_family"],
             "tuning": head["tuning"],
+            "gather_check": head["gather_check"],
             "roofline": head.get("roofline"),
             "pipelined": head.get("pipelined"),
             "f32_exact": exact,

@@ -491,7 +491,7 @@ at::Tensor adain_op(at::Tensor x, at::Tensor mean_x, at::Tensor std_x, at::Tenso
 // (torch.rand_like(ir)) -> noise (B, n_band, F * target).
 at::Tensor noise_synth_op(at::Tensor amp, at::Tensor u, int64_t n_band, int64_t noise_bands) {
     seam_tensor(amp, "amp");
-    seam_tensor(u, "u");
+    TORCH_CHECK_VALUE(u.is_cuda() && u.scalar_type() == at::kFloat, "u must be a float32 GPU tensor");
     c10::hip::HIPGuard g((c10::DeviceIndex)amp.get_device());
     TORCH_CHECK_VALUE(amp.dim() == 3 && amp.size(1) == n_band * noise_bands, "amp must be (B, n_band * noise_bands, F)");
     const int64_t B = amp.size(0), F = amp.size(2);

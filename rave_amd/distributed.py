@@ -123,6 +123,51 @@ class ShardedRunner:
             out = torch.cat([out[r * bmax:r * bmax + n] for r, n in enumerate(sizes)], 0)
         return out.view(torch.int16).to(t.dtype) if narrow else out
 
+    def verify(self, x_local: torch.Tensor) -> dict:
+        """One step's exchange checked end to end (call it outside any timed
+        region): this rank's rows of the gathered tensor equal its own encode
+        output bitwise, and every rank's rows match that rank's own checksum
+        (float64 sum and abs-sum, all-gathered separately).  The verdict is
+        reduced over ranks (MIN), so every rank returns the global result; a
+        mismatch raises.  The latents are what the all-gather delivers to every
+        rank, so this is what makes a wrong collective visible at N > 1."""
+        rank, size = world()
+        if self.mode == "decode":
+            return {"checked": False, "reason": "decode mode has no exchange"}
+        sizes = self.sizes(x_local.shape[0], x_local.device)
+        local = self.model.encode_codes(x_local) if self.mode == "codes" else self.model.encode(x_local)
+        allt = self._gather(local, sizes)
+        off = sum(sizes[:rank])
+        own = bool(torch.equal(allt[off:off + local.shape[0]], local))
+        ld = local.double()
+        mine = torch.stack([ld.sum(), ld.abs().sum()])
+        if size > 1:
+            dev = local.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+            sums = torch.empty(2 * size, dtype=torch.float64, device=dev)
+            dist.all_gather_into_tensor(sums, mine.to(dev), group=self.group)
+            sums = sums.view(size, 2).to(local.device)
+        else:
+            sums = mine.view(1, 2)
+        worst = 0.0
+        o = 0
+        for r, n in enumerate(sizes):
+            got = allt[o:o + n].double()
+            ref = sums[r]
+            err = torch.abs(torch.stack([got.sum(), got.abs().sum()]) - ref) / torch.clamp(ref[1].abs(), min=1.0)
+            worst = max(worst, float(err.max()))
+            o += n
+        ok = own and worst <= 1e-12
+        if size > 1:
+            dev = local.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+            ok = bool(flag.item())
+        res = {"checked": True, "ranks": size, "rows": int(sum(sizes)), "own_rows_bitwise": own,
+               "max_rel_checksum_err": worst, "ok": ok}
+        if not ok:
+            raise RuntimeError(f"all-gather check failed: {res}")
+        return res
+
     def step(self, x_local: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """(what every rank holds after the exchange, this rank's decoded audio)."""
         if self.mode == "decode":

@@ -71,6 +71,8 @@ def _worker(rank, size, port, x_all, q, mode="latent", fixed_sizes=False):
         sizes = [h - l for l, h in spans] if fixed_sizes else None
         runner = ShardedRunner(model, mode=mode, shard_sizes=sizes)
         z_all, y = runner.step(x_all[lo:hi])
+        chk = runner.verify(x_all[lo:hi])          # the exchange self-check bench.py runs
+        assert chk["ok"] and chk["ranks"] == size and chk["rows"] == x_all.shape[0], chk
         q.put((rank, z_all.numpy(), y.numpy()))
     finally:
         dist.destroy_process_group()

@@ -60,6 +60,8 @@ def test_rccl_latent_gather(nccl_group):
     z = m.encode(x)
     assert torch.equal(z_all, z)
     assert torch.equal(y, m.decode(z))
+    chk = runner.verify(x)                    # bench.py's exchange self-check, through RCCL
+    assert chk["ok"] and chk["own_rows_bitwise"] and chk["max_rel_checksum_err"] == 0.0
 
 
 def test_rccl_codes_gather_int16(nccl_group):
@@ -78,4 +80,5 @@ def test_rccl_codes_gather_int16(nccl_group):
     assert runner._all.dtype == torch.uint8                 # int16 codes carried as bytes over RCCL
     idx = m.encode_codes(x)
     assert idx_all.dtype == idx.dtype and torch.equal(idx_all, idx)
+    assert runner.verify(x)["ok"]
     assert torch.equal(y, m.decode_codes(idx))

@@ -241,3 +241,32 @@ def test_edge_precision_and_f32_filter_images(golden):
     trows = timg[:16 * 552].reshape(16, 552)
     h3 = np.asarray(hki, np.float32).reshape(16, 16, -1)
     np.testing.assert_array_equal(trows[3, 5 * 16 + 2], h3[3, 2, 5])
+
+
+def test_gemv_configs_listing():
+    """The skinny-N family (conv_gemv.hip) is listed for the exact-fp32
+    precision when the output has at most 32 columns: the narrowest column
+    width that holds them, K splits that each stage a bounded window, in-launch
+    and separate combines; its workspace is the tickets plus S fp32 slabs.
+    Wider outputs list none (host logic only; config codes are per precision:
+    the split-f16 tile table has its own tiles 8..11)."""
+    def args(T, t_out, prec=N.PREC_F32, c_in=512, c_out=512, k=3, d=3, B=1):
+        return N.ConvArgs(c_in=c_in, c_out=c_out, kernel=k, stride=1, dilation=d, pad_left=0, pad_right=0,
+                          batch=B, t_in=T, t_out=t_out, precision=prec, x=16, y=16, weight=16)
+
+    def tile(c):
+        return (c - 1) & 15
+
+    a = args(10, 4)
+    gemv = [c for c in N.conv_configs(a) if 8 <= tile(c) <= 11]
+    assert gemv and all(tile(c) == 8 for c in gemv)              # NMAX 4 holds 4 columns
+    assert any(((c - 1) >> 9) & 1 for c in gemv) and any(not ((c - 1) >> 9) & 1 for c in gemv)
+    for c in gemv:
+        a.config = c
+        S = (((c - 1) >> 4) & 31) + 1
+        want = 0 if S == 1 else N.SPLITK_TICKETS + S * 1 * 512 * 4
+        assert N.lib.rave_conv1d_workspace(C.byref(a)) == want, c
+    b = args(23, 17)
+    assert {tile(c) for c in N.conv_configs(b) if 8 <= tile(c) <= 11} == {11}   # 17 columns: NMAX 32
+    wide = args(40, 34)
+    assert not [c for c in N.conv_configs(wide) if 8 <= tile(c) <= 11]
