@@ -72,20 +72,37 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
     const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
 
     // ---------------------------------------------------------------- window
+    // (WB loads in flight per thread before any is used: a load-then-use loop
+    // waits out one memory round trip per element)
+    constexpr int WB = 8;
     const __amdgpu_buffer_rsrc_t xrs = make_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);
-    for (int e = tid; e < nch * XW; e += 256) {
-        const int cl = e / XW, w = e - cl * XW;
-        const int ci = c_begin * CIT + cl, t = t0 + w;
-        const bool ok = ci < a.c_in && t >= 0 && t < a.t_in;
-        float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-            xrs, ok ? (unsigned)(ci * a.x_sc + t) * 4u : kOOB, 0, 0));
-        if constexpr (SNAKE) {
-            const float al = a.alpha[min(ci, a.c_in - 1)];
-            v = v + (1.0f / (al + 1e-9f)) * sin_squared(al * v);
-        } else {
-            v = v > 0.f ? v : v * slope;
+    for (int e0 = tid; e0 < nch * XW; e0 += 256 * WB) {
+        float rv[WB];
+#pragma unroll
+        for (int i = 0; i < WB; ++i) {
+            const int e = e0 + i * 256;
+            const int cl = e / XW, w = e - cl * XW;
+            const int ci = c_begin * CIT + cl, t = t0 + w;
+            const bool ok = e < nch * XW && ci < a.c_in && t >= 0 && t < a.t_in;
+            rv[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                xrs, ok ? (unsigned)(ci * a.x_sc + t) * 4u : kOOB, 0, 0));
         }
-        gsm[cl * XW + w] = ok ? v : 0.f;
+#pragma unroll
+        for (int i = 0; i < WB; ++i) {
+            const int e = e0 + i * 256;
+            if (e >= nch * XW) break;
+            const int cl = e / XW, w = e - cl * XW;
+            const int ci = c_begin * CIT + cl, t = t0 + w;
+            const bool ok = ci < a.c_in && t >= 0 && t < a.t_in;
+            float v = rv[i];
+            if constexpr (SNAKE) {
+                const float al = a.alpha[min(ci, a.c_in - 1)];
+                v = v + (1.0f / (al + 1e-9f)) * sin_squared(al * v);
+            } else {
+                v = v > 0.f ? v : v * slope;
+            }
+            gsm[cl * XW + w] = ok ? v : 0.f;
+        }
     }
     __syncthreads();
 
@@ -100,23 +117,34 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int p = 0; p < NP; ++p) acc[r][p] = g_f32x2{0.f, 0.f};
-    for (int c = c_begin; c < c_end; ++c) {
+    // this wave's K-rows: every (chunk, tap) and channels wave, wave + 4, ... of
+    // the chunk, walked in batches of QB whose weight loads are all in flight
+    // before the first FMA (a load-then-use loop is one round trip per K-row)
+    constexpr int QC = CIT / 4, PER_C = KT * QC, QB = NMAX <= 8 ? 16 : 8;
+    const int nq = (c_end - c_begin) * PER_C;
+    for (int q0 = 0; q0 < nq; q0 += QB) {
+        g_f32x4 wv[QB];
+        int xo[QB];
 #pragma unroll
-        for (int j = 0; j < KT; ++j) {
-            const int col0 = goff + j * a.d;
-            // this wave's channels of the chunk: wave, wave + 4, ...
-#pragma unroll 2
-            for (int cl = wave; cl < CIT; cl += 4) {
-                const unsigned kk = (unsigned)((c * KT + j) * CIT + cl);
-                const g_f32x4 w4 = __builtin_bit_cast(g_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                    wrs, rows_ok ? (kk * (unsigned)a.Mpad + (unsigned)mrow) * 4u : kOOB, 0, 0));
-                const float* xr = gsm + ((c - c_begin) * CIT + cl) * XW + col0;
+        for (int i = 0; i < QB; ++i) {
+            const int q = q0 + i;
+            const int cc = q / PER_C, rem = q - cc * PER_C;
+            const int j = rem / QC, cl = wave + 4 * (rem - j * QC);
+            const unsigned kk = (unsigned)(((c_begin + cc) * KT + j) * CIT + cl);
+            const bool ok = q < nq && rows_ok;
+            wv[i] = __builtin_bit_cast(g_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                wrs, ok ? (kk * (unsigned)a.Mpad + (unsigned)mrow) * 4u : kOOB, 0, 0));
+            xo[i] = q < nq ? (cc * CIT + cl) * XW + goff + j * a.d : 0;   // (past nq: zero weights)
+        }
 #pragma unroll
-                for (int p = 0; p < NP; ++p) {
-                    const g_f32x2 xv = {xr[(2 * p) * ST], xr[(2 * p + 1) * ST]};
+        for (int i = 0; i < QB; ++i) {
+            const float* xr = gsm + xo[i];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[r][p] = __builtin_elementwise_fma(g_f32x2{w4[r], w4[r]}, xv, acc[r][p]);
-                }
+            for (int p = 0; p < NP; ++p) {
+                const g_f32x2 xv = {xr[(2 * p) * ST], xr[(2 * p + 1) * ST]};
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    acc[r][p] = __builtin_elementwise_fma(g_f32x2{wv[i][r], wv[i][r]}, xv, acc[r][p]);
             }
         }
     }
@@ -170,11 +198,24 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
         if (m >= a.M) return;
 #pragma unroll
         for (int n = 0; n < NMAX; ++n) v[n] = 0.f;
-        for (int s = 0; s < a.S; ++s) {
-            const float* sl = a.partial + (int64_t)s * total + ((int64_t)b * a.M + m) * U;
+        // slabs summed in split order; SB splits' loads in flight at once
+        constexpr int SB = NMAX <= 8 ? 8 : 4;
+        const __amdgpu_buffer_rsrc_t prs = make_rsrc(a.partial, 0x7FFFFFF0);
+        for (int s0 = 0; s0 < a.S; s0 += SB) {
+            float t[SB][NMAX];
 #pragma unroll
-            for (int n = 0; n < NMAX; ++n)
-                if (n < U) v[n] += sl[n];
+            for (int i = 0; i < SB; ++i)
+#pragma unroll
+                for (int n = 0; n < NMAX; ++n) {
+                    const int64_t off = (int64_t)(s0 + i) * total + ((int64_t)b * a.M + m) * U + n;
+                    t[i][n] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        prs, (s0 + i < a.S && n < U) ? (unsigned)(off * 4) : kOOB, 0, 0));
+                }
+#pragma unroll
+            for (int i = 0; i < SB; ++i)
+                if (s0 + i < a.S)
+#pragma unroll
+                    for (int n = 0; n < NMAX; ++n) v[n] += t[i][n];
         }
     }
     if (m >= a.M) return;

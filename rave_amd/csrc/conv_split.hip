@@ -354,6 +354,17 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
             const int g = (int)(((unsigned)e * a.xw_magic) >> 24);
             const int w = e - g * XW;
             if (e < ntask) {
+#ifdef RAVE_EXP_NOCVT
+                // timing-only A/B variant (wrong results, never shipped): the planes
+                // arrive ready-made, as a producer-side split would deliver them --
+                // one 16-byte copy per plane row piece instead of act + split
+                if constexpr (!F32) {
+                    const s_h8 r8 = *reinterpret_cast<const s_h8*>(raw + (g * 8 / S) * RS + off0 + w * S);
+                    *reinterpret_cast<s_h8*>(xh + w * PH + g * 8) = r8;
+                    *reinterpret_cast<s_h8*>(xl + w * PH + g * 8) = r8;
+                    return m;
+                }
+#endif
                 s_f32x8 v8;
 #pragma unroll
                 for (int v = 0; v < 8; ++v) {

@@ -250,7 +250,7 @@ def test_cc_adain_modes_match_reference_semantics(dev):
     from rave_amd.modules import AdaptiveInstanceNormalization
     C, T = 16, 300
     m = AdaptiveInstanceNormalization(C).to(dev).eval()
-    r = {k: v.clone().double() for k, v in m.state_dict().items()}
+    r = {k: v.detach().cpu().double() for k, v in m.state_dict().items()}
 
     def ref_forward(x):
         bs = x.shape[0]
