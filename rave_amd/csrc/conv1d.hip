@@ -574,7 +574,7 @@ extern "C" int rave_conv1d_configs(const rave_conv1d_args* p, int32_t* cfgs, int
     if (k.U <= kGemvMaxN) {
         int nmax = 4, tile = 8;
         while (nmax < k.U) nmax *= 2, ++tile;
-        const int64_t tiles = (int64_t)ceil_div(k.M, 256) * k.B;
+        const int64_t tiles = (int64_t)ceil_div(k.M, gemv_rows(nmax)) * k.B;
         for (int S : kGemvSplits) {
             if (!split_count_distinct(S, k.nchunks) || tiles * S > 2048 ||
                 !gemv_fits(taps, k.U, k.d, k.transposed != 0, ceil_div(k.nchunks, S), nmax))

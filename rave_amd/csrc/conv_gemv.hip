@@ -31,7 +31,6 @@ namespace rave {
 typedef float g_f32x2 __attribute__((ext_vector_type(2)));
 typedef float g_f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kGemvRows = 256;                     // GEMM rows per workgroup (64 lanes x 4)
 constexpr int kGemvStage = 12288;                  // staged window floats per workgroup (48 KiB)
 
 // (channels per packed chunk, stride) of conv1d.hip's exact-fp32 families
@@ -49,14 +48,22 @@ __host__ __device__ inline int gemv_xw(int KT, int ST, int U, int d, bool transp
     return (U - 1) * ST + (KT - 1) * d + 1 + (transposed ? 1 : 0);
 }
 
+// GR<NMAX>: rows per lane (4 x NMAX accumulators at most 128 floats), rows
+// per workgroup, threads per output row in the epilogue and columns per thread
+template <int NMAX> struct GR {
+    static constexpr int R = NMAX <= 32 ? 4 : NMAX == 64 ? 2 : 1;
+    static constexpr int BM = 64 * R, TPR = 256 / BM, NC = NMAX / TPR;
+};
+
 template <int KT, int NMAX, bool SNAKE>
 __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
     constexpr int CIT = GFam<KT>::CIT, ST = GFam<KT>::ST, NP = NMAX / 2;
+    constexpr int R = GR<NMAX>::R, BM = GR<NMAX>::BM, TPR = GR<NMAX>::TPR, NC = GR<NMAX>::NC;
     constexpr unsigned kOOB = 0xFFFFFFF0u;
     extern __shared__ __attribute__((aligned(16))) float gsm[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int MT = ceil_div(a.M, kGemvRows);
+    const int MT = ceil_div(a.M, BM);
     // splits of one row tile on consecutive blocks of one XCD (blocks b, b+8, ...)
     int lg = blockIdx.x;
     if ((gridDim.x & 7) == 0) lg = (lg & 7) * (gridDim.x >> 3) + (lg >> 3);
@@ -64,7 +71,7 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
     const int split = lg % a.S;
     const int tile = lg / a.S;                       // b * MT + mt (ticket index)
     const int mt = tile % MT, b = tile / MT;
-    const int m0 = mt * kGemvRows;
+    const int m0 = mt * BM;
     const int c_begin = split * a.cps, c_end = min(a.nchunks, c_begin + a.cps);
     const int nch = (c_end - c_begin) * CIT;         // staged channels
     const int U = a.U, XW = a.XW;
@@ -107,14 +114,14 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
     __syncthreads();
 
     // ---------------------------------------------------------------- K loop
-    // lane: rows m0 + 4 lane .. + 3; ConvT rows of phase group 1 read one column later
-    const int mrow = m0 + 4 * lane;
+    // lane: rows m0 + R lane .. + R-1; ConvT rows of phase group 1 read one column later
+    const int mrow = m0 + R * lane;
     const int goff = (a.transposed && mrow >= a.split_row) ? 1 : 0;
     const bool rows_ok = mrow < a.Mpad;
     const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, a.w_bytes);
-    g_f32x2 acc[4][NP];
+    g_f32x2 acc[R][NP];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int p = 0; p < NP; ++p) acc[r][p] = g_f32x2{0.f, 0.f};
     // this wave's K-rows: every (chunk, tap) and channels wave, wave + 4, ... of
@@ -123,7 +130,7 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
     constexpr int QC = CIT / 4, PER_C = KT * QC, QB = NMAX <= 8 ? 16 : 8;
     const int nq = (c_end - c_begin) * PER_C;
     for (int q0 = 0; q0 < nq; q0 += QB) {
-        g_f32x4 wv[QB];
+        float wv[QB][R];
         int xo[QB];
 #pragma unroll
         for (int i = 0; i < QB; ++i) {
@@ -132,8 +139,18 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
             const int j = rem / QC, cl = wave + 4 * (rem - j * QC);
             const unsigned kk = (unsigned)(((c_begin + cc) * KT + j) * CIT + cl);
             const bool ok = q < nq && rows_ok;
-            wv[i] = __builtin_bit_cast(g_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                wrs, ok ? (kk * (unsigned)a.Mpad + (unsigned)mrow) * 4u : kOOB, 0, 0));
+            const unsigned off = ok ? (kk * (unsigned)a.Mpad + (unsigned)mrow) * 4u : kOOB;
+            if constexpr (R == 4) {
+                const g_f32x4 w4 = __builtin_bit_cast(g_f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) wv[i][r] = w4[r];
+            } else if constexpr (R == 2) {
+                const g_f32x2 w2 = __builtin_bit_cast(g_f32x2, __builtin_amdgcn_raw_buffer_load_b64(wrs, off, 0, 0));
+                wv[i][0] = w2[0];
+                wv[i][1] = w2[1];
+            } else {
+                wv[i][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wrs, off, 0, 0));
+            }
             xo[i] = q < nq ? (cc * CIT + cl) * XW + goff + j * a.d : 0;   // (past nq: zero weights)
         }
 #pragma unroll
@@ -143,7 +160,7 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
             for (int p = 0; p < NP; ++p) {
                 const g_f32x2 xv = {xr[(2 * p) * ST], xr[(2 * p + 1) * ST]};
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
+                for (int r = 0; r < R; ++r)
                     acc[r][p] = __builtin_elementwise_fma(g_f32x2{wv[i][r], wv[i][r]}, xv, acc[r][p]);
             }
         }
@@ -151,20 +168,22 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
     __syncthreads();                                  // window dead: the reduction area
 
     // ---------------------------------------------------------------- wave sum (fixed order)
-    float* red = gsm;                                 // [wave][row 0..255][NMAX]
+    float* red = gsm;                                 // [wave][row 0..BM-1][NMAX]
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int p = 0; p < NP; ++p)
-            *reinterpret_cast<g_f32x2*>(red + ((wave * kGemvRows + 4 * lane + r) * NMAX + 2 * p)) = acc[r][p];
+            *reinterpret_cast<g_f32x2*>(red + ((wave * BM + R * lane + r) * NMAX + 2 * p)) = acc[r][p];
     __syncthreads();
-    const int m = m0 + tid;                           // this thread's row from here on
-    float v[NMAX];
+    // from here on a thread owns row m0 + tid % BM, columns [n0, n0 + NC)
+    const int rl = tid % BM, n0 = (tid / BM) * NC;
+    const int m = m0 + rl;
+    float v[NC];
 #pragma unroll
-    for (int n = 0; n < NMAX; ++n) {
+    for (int n = 0; n < NC; ++n) {
         float s = 0.f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) s += red[(w * kGemvRows + tid) * NMAX + n];
+        for (int w = 0; w < 4; ++w) s += red[(w * BM + rl) * NMAX + n0 + n];
         v[n] = s;
     }
 
@@ -174,8 +193,8 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
         float* slab = a.partial + (int64_t)split * total + ((int64_t)b * a.M + m) * U;
         if (m < a.M)
 #pragma unroll
-            for (int n = 0; n < NMAX; ++n)
-                if (n < U) slab[n] = v[n];
+            for (int n = 0; n < NC; ++n)
+                if (n0 + n < U) slab[n0 + n] = v[n];
         if (!a.inlaunch) return;                      // a separate reduce launch sums the slabs
         // in-launch combine: publish with an agent-scope release, draw the row
         // tile's ticket; the split drawing S - 1 acquires and sums every slab in
@@ -197,40 +216,40 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
         if (!last_s) return;
         if (m >= a.M) return;
 #pragma unroll
-        for (int n = 0; n < NMAX; ++n) v[n] = 0.f;
+        for (int n = 0; n < NC; ++n) v[n] = 0.f;
         // slabs summed in split order; SB splits' loads in flight at once
-        constexpr int SB = NMAX <= 8 ? 8 : 4;
+        constexpr int SB = NC <= 8 ? 8 : 4;
         const __amdgpu_buffer_rsrc_t prs = make_rsrc(a.partial, 0x7FFFFFF0);
         for (int s0 = 0; s0 < a.S; s0 += SB) {
-            float t[SB][NMAX];
+            float t[SB][NC];
 #pragma unroll
             for (int i = 0; i < SB; ++i)
 #pragma unroll
-                for (int n = 0; n < NMAX; ++n) {
-                    const int64_t off = (int64_t)(s0 + i) * total + ((int64_t)b * a.M + m) * U + n;
+                for (int n = 0; n < NC; ++n) {
+                    const int64_t off = (int64_t)(s0 + i) * total + ((int64_t)b * a.M + m) * U + n0 + n;
                     t[i][n] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                        prs, (s0 + i < a.S && n < U) ? (unsigned)(off * 4) : kOOB, 0, 0));
+                        prs, (s0 + i < a.S && n0 + n < U) ? (unsigned)(off * 4) : kOOB, 0, 0));
                 }
 #pragma unroll
             for (int i = 0; i < SB; ++i)
                 if (s0 + i < a.S)
 #pragma unroll
-                    for (int n = 0; n < NMAX; ++n) v[n] += t[i][n];
+                    for (int n = 0; n < NC; ++n) v[n] += t[i][n];
         }
     }
     if (m >= a.M) return;
 #pragma unroll
-    for (int n = 0; n < NMAX; ++n)
-        if (n < U) store_out(a, b, m, n, v[n]);
+    for (int n = 0; n < NC; ++n)
+        if (n0 + n < U) store_out(a, b, m, n0 + n, v[n]);
 }
 
 template <int KT, int NMAX>
 static int gemv_go(ConvKArgs k, hipStream_t st) {
-    const int MT = ceil_div(k.M, kGemvRows);
+    const int MT = ceil_div(k.M, GR<NMAX>::BM);
     const int grid = MT * k.S * k.B;
     // (+ slack: lanes read all NMAX columns of a window row, the ones past U unused)
     const size_t lds = (size_t)std::max(ceil_div(k.cps * GFam<KT>::CIT * k.XW, 4) * 4 + NMAX * GFam<KT>::ST + 16,
-                                        4 * kGemvRows * NMAX) * 4;
+                                        4 * GR<NMAX>::BM * NMAX) * 4;
     auto kern = k.act == RAVE_ACT_SNAKE ? conv1d_gemv_kernel<KT, NMAX, true> : conv1d_gemv_kernel<KT, NMAX, false>;
     if (lds > 64 * 1024) {
         static bool done[2] = {false, false};
@@ -251,7 +270,9 @@ static int gemv_family(const ConvKArgs& k, int nmax, hipStream_t st) {
         case 4: return gemv_go<KT, 4>(k, st);
         case 8: return gemv_go<KT, 8>(k, st);
         case 16: return gemv_go<KT, 16>(k, st);
-        default: return gemv_go<KT, 32>(k, st);
+        case 32: return gemv_go<KT, 32>(k, st);
+        case 64: return gemv_go<KT, 64>(k, st);
+        default: return gemv_go<KT, 128>(k, st);
     }
 }
 
@@ -271,7 +292,8 @@ int conv1d_gemv(ConvKArgs k, int taps, int nmax, int sep, hipStream_t st) {
         set_error("conv1d(gemv): window of one K split exceeds the staging area, or too many columns");
         return RAVE_ERR_UNSUPPORTED;
     }
-    const int tiles = ceil_div(k.M, kGemvRows) * k.B;
+    const int rows = gemv_rows(nmax);                                 // GR<NMAX>::BM
+    const int tiles = ceil_div(k.M, rows) * k.B;
     k.inlaunch = (k.S > 1 && !sep && k.partial && tiles <= kSplitTicketsUsable) ? 1 : 0;
     RAVE_CHECK_ARG(k.S <= 1 || k.partial, "conv1d(gemv): K splits need the workspace");
     int rc;

@@ -120,10 +120,11 @@ struct LaunchCfg {
 };
 
 // Skinny-N fp32 family (conv_gemv.hip): weights spread over the chip, all
-// output columns (U <= NMAX) per workgroup.  Launch-config tiles 8..11 of the
-// exact-fp32 precision select it with NMAX = 4 << (tile - 8).
-constexpr int kGemvMaxN = 32;
-inline bool is_gemv_tile(int t) { return t >= 8 && t <= 11; }
+// output columns (U <= NMAX) per workgroup.  Launch-config tiles 8..13 of the
+// exact-fp32 precision select it with NMAX = 4 << (tile - 8) (4 ... 128).
+constexpr int kGemvMaxN = 128;
+inline bool is_gemv_tile(int t) { return t >= 8 && t <= 13; }
+inline int gemv_rows(int nmax) { return nmax <= 32 ? 256 : nmax == 64 ? 128 : 64; }   // rows per workgroup
 inline int gemv_nmax(int t) { return 4 << (t - 8); }
 bool gemv_fits(int taps, int U, int d, bool transposed, int cps, int nmax);
 int conv1d_gemv(ConvKArgs k, int taps, int nmax, int sep, hipStream_t st);

@@ -205,6 +205,10 @@ GEMV_CASES = [
     (128, 128, 1, 1, 1, 0, "leaky", True, 1, 32),
     (320, 1024, 3, 1, 1, 0, "none", False, 1, 2),
     (96, 200, 3, 1, 3, 0, "leaky", True, 3, 13),
+    (64, 64, 3, 1, 9, 0, "leaky", False, 1, 128),        # 128 columns: one row per lane
+    (64, 64, 1, 1, 1, 0, "snake", True, 1, 128),
+    (128, 128, 3, 1, 3, 0, "leaky", True, 2, 50),        # 64 columns: two rows per lane
+    (128, 64, 8, 4, 1, 1, "leaky", False, 1, 32),        # ConvT to 128 columns
 ]
 
 
@@ -224,7 +228,7 @@ def test_conv_gemv_configs(N, dev, case):
                    transposed=transposed, out_shift=s // 2 if transposed else 0, act=N.ACT[act],
                    batch=B, t_in=T, t_out=t_out, precision=N.PREC_F32, x=16, y=16, weight=16,
                    alpha=16 if alpha is not None else None, residual=16 if res is not None else None)
-    gemv = [c for c in N.conv_configs(a) if 8 <= ((c - 1) & 15) <= 11]
+    gemv = [c for c in N.conv_configs(a) if 8 <= ((c - 1) & 15) <= 13]
     assert gemv, "no skinny-N configurations listed"
     for cfg in gemv:
         got = run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act, True,

@@ -245,7 +245,7 @@ def test_edge_precision_and_f32_filter_images(golden):
 
 def test_gemv_configs_listing():
     """The skinny-N family (conv_gemv.hip) is listed for the exact-fp32
-    precision when the output has at most 32 columns: the narrowest column
+    precision when the output has at most 128 columns: the narrowest column
     width that holds them, K splits that each stage a bounded window, in-launch
     and separate combines; its workspace is the tickets plus S fp32 slabs.
     Wider outputs list none (host logic only; config codes are per precision:
@@ -268,5 +268,6 @@ def test_gemv_configs_listing():
         assert N.lib.rave_conv1d_workspace(C.byref(a)) == want, c
     b = args(23, 17)
     assert {tile(c) for c in N.conv_configs(b) if 8 <= tile(c) <= 11} == {11}   # 17 columns: NMAX 32
-    wide = args(40, 34)
-    assert not [c for c in N.conv_configs(wide) if 8 <= tile(c) <= 11]
+    assert {tile(c) for c in N.conv_configs(args(40, 34)) if 8 <= tile(c) <= 13} == {12}   # NMAX 64
+    assert {tile(c) for c in N.conv_configs(args(130, 128, d=1)) if 8 <= tile(c) <= 13} == {13}   # 128
+    assert not [c for c in N.conv_configs(args(140, 134)) if 8 <= tile(c) <= 13]                  # > 128
