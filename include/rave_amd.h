@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 14
+#define RAVE_ABI_VERSION 15
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 /* The last of those words is reserved: no conv ticket uses it.  A cooperative
@@ -329,6 +329,11 @@ typedef struct rave_unit_args {
     uint32_t* status;   /* optional (cooperative form): a group whose hand-off gave up also sets
                            this word to 1 (system-scope store: host-mapped memory works), beside
                            the workspace's RAVE_SPLITK_STATUS_WORD; the caller clears it */
+    int32_t x_len;      /* valid input columns (0: t_len).  Cached (streaming) form: x starts at
+                           the history, pad_left = 0, x_len = 2*dilation + t_len, and no column
+                           past x_len is padding (the one-shot form pads past t_len with zeros) */
+    int32_t res_shift;  /* the residual of output column n is x column n + res_shift (0 one-shot;
+                           cached: 2*dilation - the identity branch's delay, rave/blocks.py:32-46) */
 } rave_unit_args;
 int64_t rave_unit_packed_size(int channels);
 int rave_unit_pack_weight(const float* w1, const float* w2, int channels, float* packed);

@@ -58,7 +58,7 @@ template <int NMAX> struct GR {
 template <int KT, int NMAX, bool SNAKE>
 __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
     constexpr int CIT = GFam<KT>::CIT, ST = GFam<KT>::ST, NP = NMAX / 2;
-    constexpr int R = GR<NMAX>::R, BM = GR<NMAX>::BM, TPR = GR<NMAX>::TPR, NC = GR<NMAX>::NC;
+    constexpr int R = GR<NMAX>::R, BM = GR<NMAX>::BM, NC = GR<NMAX>::NC;
     constexpr unsigned kOOB = 0xFFFFFFF0u;
     extern __shared__ __attribute__((aligned(16))) float gsm[];
     const int tid = threadIdx.x, lane = tid & 63;

@@ -405,7 +405,8 @@ struct Model {
     bool fuse_unit(const Node& k3, const Node& k1, int B, int T);
     double unit_best_ms(const Node& k3, const Node& k1, int B, int T);
     rave_unit_args unit_desc(const Node& k3, const Node& k1, int B, int T, int prec) const;
-    void unit_op(Plan& p, const Node& k3, const Node& k1, int B, int T, const View& src, const View& dst);
+    void unit_op(Plan& p, const Node& k3, const Node& k1, int B, int T, const View& src, const View& dst,
+                 int x_len = 0, int res_shift = 0);
     rave_stack_args stack_desc(const std::vector<std::pair<const Node*, const Node*>>& run, int B, int T) const;
     bool use_stack(const std::vector<std::pair<const Node*, const Node*>>& run, int B, int T);
     void stack_op(Plan& p, const std::vector<std::pair<const Node*, const Node*>>& run, int B, int T,
@@ -757,9 +758,16 @@ double Model::unit_best_ms(const Node& k3, const Node& k1, int B, int T) {
     return unit_time(k3, k1, B, T);
 }
 
-void Model::unit_op(Plan& p, const Node& k3, const Node& k1, int B, int T, const View& src, const View& dst) {
+void Model::unit_op(Plan& p, const Node& k3, const Node& k1, int B, int T, const View& src, const View& dst,
+                    int x_len, int res_shift) {
     const int pr = unit_pick(k3, B, T, false);
     rave_unit_args u = unit_desc(k3, k1, B, T, pr);
+    if (x_len > 0) {
+        // cached form: x from the history start, no zero padding, residual shifted
+        u.pad_left = 0;
+        u.x_len = x_len;
+        u.res_shift = res_shift;
+    }
     u.x_sb = src.sb;
     u.x_sc = src.sc;
     u.y_sb = dst.sb;
@@ -2261,6 +2269,45 @@ static void conv_stream(Model* m, Plan& p, const Node& n, int B, std::map<std::s
     o.prec = pc.first;
 }
 
+// The cached conv sequence of one stream plan.  A Residual(DilatedUnit) whose
+// fused kernel is timed faster than its two convs (Model::fuse_unit, the
+// one-shot decision at the block's length) runs as ONE cached unit launch: the
+// k=3 window reads the input's history (pad_left 0, x_len = need + T) and the
+// residual is the same buffer shifted by need - delay (AlignBranches,
+// rave/blocks.py:32-46); the intermediate tensor is never written.
+// RAVE_STREAM_UNITS=0 keeps every conv separate (A/B).
+static void stream_convs(Model* m, Plan& p, const std::vector<const Node*>& nodes, int B,
+                         std::map<std::string, StreamBuf>& bufs, std::vector<int>& adain_ops) {
+    static const bool units_on = [] {
+        const char* e = std::getenv("RAVE_STREAM_UNITS");
+        return !(e && e[0] == '0');
+    }();
+    std::map<std::string, const Node*> fused;
+    if (m->cfg.fuse_units && units_on)
+        for (auto& pr : m->unit_pairs(nodes))
+            if (m->unit_ok.count(pr.first->name) && pr.second->adain.empty()) fused[pr.first->name] = pr.second;
+    std::set<std::string> skip;
+    for (const Node* n : nodes) {
+        if (skip.count(n->name)) continue;
+        auto fu = fused.find(n->name);
+        const StreamBuf& src = bufs.at(n->src);
+        if (fu != fused.end() && m->fuse_unit(*n, *fu->second, B, src.t)) {
+            const Node& k1 = *fu->second;
+            skip.insert(k1.name);
+            if (!n->adain.empty() && !m->ad_index.empty()) {
+                adain_ops.push_back((int)p.ops.size());
+                m->adain_op(p, n->adain, B, n->c_in, src.t, src.v.at(src.h));
+            }
+            const int need = stream_need(*n);
+            const StreamBuf& dst = bufs.at(k1.dst);
+            const View y = dst.v.p.kind == PRef::WS ? dst.v.at(dst.h) : dst.v;
+            m->unit_op(p, *n, k1, B, src.t, src.v.at(src.h - need), y, need + src.t, need - k1.res_delay);
+            continue;
+        }
+        conv_stream(m, p, *n, B, bufs, adain_ops);
+    }
+}
+
 static void shift_all(Plan& p, int B, const std::map<std::string, StreamBuf>& bufs) {
     for (auto& kv : bufs) {
         const StreamBuf& b = kv.second;
@@ -2331,7 +2378,7 @@ static void build_stream(Stream& s) {
         copy_op(p, B, 1, s.block, io_view(0, s.block, s.block), a.v.at(a.h));
         const StreamBuf& e = s.enc_bufs.at("enc_in");
         m->analysis_op(p, B, s.block, a.v, e.v.at(e.h), cfg.enc_bands, 0, ha + s.block);
-        for (const Node* n : nodes) conv_stream(m, p, *n, B, s.enc_bufs, s.enc_adain);
+        stream_convs(m, p, nodes, B, s.enc_bufs, s.enc_adain);
         if (s.codes) m->rvq_encode_op(p, B, s.Fz, lat.v, io_view(1, 0, 0));
         else m->fill_speaker(p, B, s.Fz, io_view(1, (int64_t)zc * s.Fz, s.Fz).at((int64_t)cfg.latent_size * s.Fz));
         shift_all(p, B, s.enc_bufs);
@@ -2359,7 +2406,7 @@ static void build_stream(Stream& s) {
         } else {
             copy_op(p, B, m->dec_in, s.Fz, io_view(0, (int64_t)m->dec_in * s.Fz, s.Fz), z.v.at(z.h));
         }
-        for (const Node* n : nodes) conv_stream(m, p, *n, B, s.dec_bufs, s.dec_adain);
+        stream_convs(m, p, nodes, B, s.dec_bufs, s.dec_adain);
         const StreamBuf& w = s.dec_bufs.at("wave");
         View noise_v;
         if (cfg.noise) {

@@ -41,6 +41,7 @@ struct UnitKArgs {
     const float* b1; const float* b2; const float* a0; const float* a2;
     int64_t x_sb, x_sc, y_sb, y_sc;
     int T, d, pad_l, ntiles, W, XWS, HS;
+    int XL, rsh;             // valid input columns; residual column shift (cached form)
     int x_bytes, y_bytes, w_bytes, bias_bytes;
     int act;
     float slope;
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(kUnitThreads) void residual_unit_kernel(UnitKArgs a
                 const int c = wave + r * kUnitWaves;
                 const int w = ch * 64 + lane;
                 const int t = t0 + w;
-                const bool ok = w < a.W && t >= 0 && t < a.T;
+                const bool ok = w < a.W && t >= 0 && t < a.XL;
                 v[r][ch] = ld1(xrs, ok ? (unsigned)(c * a.x_sc + t) * 4u : kUnitOOB);
             }
 #pragma unroll
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(kUnitThreads) void residual_unit_kernel(UnitKArgs a
 #pragma unroll
             for (int r = 0; r < M::ACC; ++r) {
                 const int m = m0 + M::row(lane, r);
-                res[r] = ld1(xrs, nok ? (unsigned)(m * a.x_sc + n) * 4u : kUnitOOB) +
+                res[r] = ld1(xrs, nok ? (unsigned)(m * a.x_sc + n + a.rsh) * 4u : kUnitOOB) +
                          ld1(brs, (unsigned)m * 4u);
             }
 #pragma unroll
@@ -370,6 +371,13 @@ extern "C" int rave_residual_unit(const rave_unit_args* p, void* stream) {
                    "residual_unit: bad activation");
     RAVE_CHECK_ARG(a.act != RAVE_ACT_SNAKE || (a.alpha0 && a.alpha2), "residual_unit: snake needs alphas");
     RAVE_CHECK_ARG(a.x != a.y, "residual_unit: y must not alias x (other slabs still read it)");
+    {
+        // cached form: the window and the shifted residual stay inside x's valid columns
+        const int xl = a.x_len > 0 ? a.x_len : a.t_len;
+        RAVE_CHECK_ARG(xl >= a.t_len && a.res_shift >= 0 && a.t_len + a.res_shift <= xl,
+                       "residual_unit: x_len / res_shift leave the residual outside x");
+        RAVE_CHECK_ARG(a.x_len <= 0 || a.x_sc >= xl, "residual_unit: x_len exceeds the row stride");
+    }
     if (a.precision == RAVE_PREC_SPLIT16 || a.precision == RAVE_PREC_F32_RING) return residual_unit_split(a, stream);
     const int C = a.channels;
     UnitKArgs k{};
@@ -377,13 +385,15 @@ extern "C" int rave_residual_unit(const rave_unit_args* p, void* stream) {
     k.b1 = a.bias1; k.b2 = a.bias2; k.a0 = a.alpha0; k.a2 = a.alpha2;
     k.x_sb = a.x_sb; k.x_sc = a.x_sc; k.y_sb = a.y_sb; k.y_sc = a.y_sc;
     k.T = a.t_len; k.d = a.dilation; k.pad_l = a.pad_left;
+    k.XL = a.x_len > 0 ? a.x_len : a.t_len;
+    k.rsh = a.res_shift;
     const int BN = unit_bn(C), MT = unit_mt(C);
     k.ntiles = ceil_div(a.t_len, BN);
     k.W = BN + 2 * a.dilation;
     k.XWS = unit_stride(k.W, MT);
     k.HS = unit_stride(BN, MT);
     k.act = a.act; k.slope = a.leaky_slope;
-    const int64_t xb = ((int64_t)(C - 1) * a.x_sc + a.t_len) * 4;
+    const int64_t xb = ((int64_t)(C - 1) * a.x_sc + k.XL) * 4;
     const int64_t yb = ((int64_t)(C - 1) * a.y_sc + a.t_len) * 4;
     RAVE_CHECK_ARG(xb < (1ll << 31) && yb < (1ll << 31), "residual_unit: tensors beyond 2 GiB per item");
     k.x_bytes = (int)xb; k.y_bytes = (int)yb;

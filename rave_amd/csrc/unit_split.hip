@@ -92,6 +92,7 @@ struct USArgs {
     const float* b1; const float* b2; const float* a0; const float* a2;
     int64_t x_sb, x_sc, y_sb, y_sc;
     int T, d, pad_l, ntiles, XW;
+    int XL, rsh;             // valid input columns; residual column shift (cached form)
     int x_bytes, y_bytes, w_bytes, bias_bytes;
     int act;
     float slope;
@@ -100,7 +101,7 @@ struct USArgs {
     // the give-up word, members' max |h|, the act2(h) exchange [group][BN][C]
     unsigned* flags; unsigned* tmo; float* xmax; float* xch;
     int ngroups, xch_bytes;
-    int xv;                  // 16-byte window loads (T % 4 == 0, 16-byte aligned rows)
+    int xv;                  // 16-byte window loads (XL % 4 == 0, 16-byte aligned rows)
     unsigned nb_magic;       // ceil(2^24 / window blocks per row)
     int flag_stride;         // counter words per group (cooperative form)
     unsigned* status;        // optional caller's give-up word (host-mapped: system scope)
@@ -255,7 +256,7 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
             const int e = tid + i * NT;
             const int g = (int)(((unsigned)e * a.xw_magic) >> 24);
             const int w = e - g * XW;
-            const int t = min(max(t0 + w, 0), a.T - 1);
+            const int t = min(max(t0 + w, 0), a.XL - 1);
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
                 const int c = min(g * 8 + v, C - 1);
@@ -268,7 +269,7 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
             const int e = tid + i * NT;
             const int g = (int)(((unsigned)e * a.xw_magic) >> 24);
             const int w = e - g * XW;
-            const bool ok = (e < ntask) && (t0 + w >= 0) && (t0 + w < a.T);
+            const bool ok = (e < ntask) && (t0 + w >= 0) && (t0 + w < a.XL);
             us_f32x8 v8;
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
@@ -296,7 +297,7 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
     // 4-sample block k), k fastest along the lanes (coalesced rows); 8 b128
     // loads per task, every load of the window in flight at once, then four
     // transposed 8-channel plane rows per task.  Blocks are wholly inside or
-    // wholly outside [0, T) (T % 4 == 0, 4-aligned block starts).
+    // wholly outside [0, XL) (XL % 4 == 0, 4-aligned block starts).
     auto stage_window_v = [&]() __attribute__((always_inline)) {
         constexpr int NBM = (G::XW_MAX + 3) / 4 + 1, XTV = (G8 * NBM + NT - 1) / NT;
         const int ta = t0 & ~3;
@@ -310,7 +311,7 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
             const int g = (int)(((unsigned)e * a.nb_magic) >> 24);
             const int kb = e - g * nb;
             const int t = ta + 4 * kb;
-            const bool ok = (e < ntv) && t >= 0 && t < a.T;
+            const bool ok = (e < ntv) && t >= 0 && t < a.XL;
 #pragma unroll
             for (int v = 0; v < 8; ++v)
                 rx[i][v] = __builtin_bit_cast(us_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -373,8 +374,8 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
             for (int e = tid; e < ntask; e += NT) {
                 const int g = (int)(((unsigned)e * a.xw_magic) >> 24);
                 const int w = e - g * XW;
-                const bool ok = (t0 + w >= 0) && (t0 + w < a.T);
-                const int t = min(max(t0 + w, 0), a.T - 1);
+                const bool ok = (t0 + w >= 0) && (t0 + w < a.XL);
+                const int t = min(max(t0 + w, 0), a.XL - 1);
                 us_f32x8 v8;
 #pragma unroll
                 for (int v = 0; v < 8; ++v) {
@@ -734,7 +735,7 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
                 for (int r = 0; r < 16; ++r) {
                     const int m = mrow0 + 32 * i + 8 * (r >> 2) + (r & 3);
                     res[i][j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                        xrs, nok ? (unsigned)(m * a.x_sc + n) * 4u : kUSOOB, 0, 0));
+                        xrs, nok ? (unsigned)(m * a.x_sc + n + a.rsh) * 4u : kUSOOB, 0, 0));
                 }
         }
 #pragma unroll
@@ -950,8 +951,10 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
     k.b1 = a.bias1; k.b2 = a.bias2; k.a0 = a.alpha0; k.a2 = a.alpha2;
     k.x_sb = a.x_sb; k.x_sc = a.x_sc; k.y_sb = a.y_sb; k.y_sc = a.y_sc;
     k.T = a.t_len; k.d = a.dilation; k.pad_l = a.pad_left;
+    k.XL = a.x_len > 0 ? a.x_len : a.t_len;
+    k.rsh = a.res_shift;
     k.act = a.act; k.slope = a.leaky_slope;
-    const int64_t xb = ((int64_t)(C - 1) * a.x_sc + a.t_len) * 4;
+    const int64_t xb = ((int64_t)(C - 1) * a.x_sc + k.XL) * 4;
     const int64_t yb = ((int64_t)(C - 1) * a.y_sc + a.t_len) * 4;
     RAVE_CHECK_ARG(xb < (1ll << 31) && yb < (1ll << 31), "residual_unit: tensors beyond 2 GiB per item");
     k.x_bytes = (int)xb; k.y_bytes = (int)yb;
@@ -972,7 +975,7 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
         k.nb_magic = (unsigned)(((1u << 24) + nb - 1) / nb);
         return us_launch<CC, WGN, MI, KG, CB, RB>(k, a.batch, snake, a.precision == RAVE_PREC_F32_RING, st);
     };
-    k.xv = (a.t_len % 4 == 0 && a.x_sc % 4 == 0 && a.x_sb % 4 == 0 &&
+    k.xv = (k.XL % 4 == 0 && a.x_sc % 4 == 0 && a.x_sb % 4 == 0 &&
             reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && std::getenv("RAVE_UNIT_XV") == nullptr) ? 1 : 0;
     // cooperative form when the caller passed its workspace
     const CoopLayout L = coop_layout(a);

@@ -964,6 +964,74 @@ def test_residual_unit_cooperative(N, dev, case, precision):
     assert maxabs(got, ref) <= 2e-5 * max(1.0, float(np.abs(ref).max()))
 
 
+CACHED_UNIT_CASES = [
+    # C, d, act, causal, B, T, coop
+    (64, 1, "leaky", True, 1, 1, False),
+    (64, 9, "snake", False, 2, 16, False),
+    (128, 3, "leaky", True, 1, 128, False),
+    (128, 9, "leaky", False, 2, 37, False),
+    (128, 1, "snake", False, 2, 126, False),      # x_len % 4 == 0: 16-byte window loads
+    (256, 3, "snake", True, 1, 32, False),
+    (256, 9, "leaky", True, 2, 64, True),
+    (512, 1, "leaky", False, 1, 8, True),
+]
+
+
+@pytest.mark.parametrize("precision", ["f32", "split16", "f32_ring"])
+@pytest.mark.parametrize("case", CACHED_UNIT_CASES, ids=[str(c) for c in CACHED_UNIT_CASES])
+def test_residual_unit_cached_form(N, dev, case, precision):
+    """The cached (streaming) fused unit: x holds need = 2d history columns then
+    the block (x_len = 2d + T, pad_left 0, rows wider than x_len), the residual
+    is x shifted by res_shift = 2d - delay (AlignBranches: causal delay 0,
+    centred d; rave/blocks.py:32-46, cached_conv convs pad nothing), against
+    the oracle on the same window."""
+    from oracle.rave_oracle import conv1d, leaky_relu, snake
+    C, d, act, causal, B, T, coop = case
+    prec = N.PRECISION[precision]
+    if not N.unit_supported(C, prec):
+        pytest.skip(f"no fused {precision} unit for C={C}")
+    need = 2 * d
+    rs = need - (0 if causal else d)
+    XL = need + T
+    SC = (XL + 3) // 4 * 4 + 4                    # 16-byte rows, wider than x_len
+    rng = np.random.default_rng(C + d + T)
+    xw = np.zeros((B, C, SC), np.float32)
+    xw[:, :, :XL] = rng.standard_normal((B, C, XL))
+    xw[:, :, XL:] = np.nan                        # row padding past x_len is never read
+    w1 = (rng.standard_normal((C, C, 3)) / np.sqrt(3 * C)).astype(np.float32)
+    w2 = (rng.standard_normal((C, C, 1)) / np.sqrt(C)).astype(np.float32)
+    b1, b2 = (rng.standard_normal(C).astype(np.float32) * 0.1 for _ in range(2))
+    a0, a2 = ((1 + 0.3 * rng.standard_normal(C)).astype(np.float32) for _ in range(2))
+    f = (lambda v, al: snake(v, al.reshape(-1, 1))) if act == "snake" else (lambda v, al: leaky_relu(v, 0.2))
+    x = xw[:, :, :XL].astype(np.float64)
+    h = f(conv1d(f(x, a0), w1, b1, 1, d, (0, 0)), a2)
+    ref = x[:, :, rs:rs + T] + conv1d(h, w2, b2, 1, 1, (0, 0))
+    packed = torch.from_numpy(N.pack_unit_weight(w1, w2, C, precision=prec)).to(dev)
+    xd = torch.from_numpy(xw).to(dev)
+    dd = {k: torch.from_numpy(v).to(dev) for k, v in dict(b1=b1, b2=b2, a0=a0, a2=a2).items()}
+    y = torch.full((B, C, T), float("nan"), device=dev)
+
+    def args(ws):
+        return N.UnitArgs(channels=C, batch=B, t_len=T, dilation=d, pad_left=0, act=N.ACT[act],
+                          leaky_slope=0.2, precision=prec, x=xd.data_ptr(), x_sb=C * SC, x_sc=SC, y=y.data_ptr(),
+                          y_sb=C * T, y_sc=T, weight=packed.data_ptr(), bias1=dd["b1"].data_ptr(),
+                          bias2=dd["b2"].data_ptr(), alpha0=dd["a0"].data_ptr() if act == "snake" else None,
+                          alpha2=dd["a2"].data_ptr() if act == "snake" else None,
+                          workspace=ws.data_ptr() if ws is not None else None, x_len=XL, res_shift=rs)
+    ws = None
+    if coop:
+        nws = N.lib.rave_unit_workspace(C_.byref(args(None)))
+        if nws > 0:
+            ws = torch.zeros(nws, device=dev)
+    N.check(N.lib.rave_residual_unit(C_.byref(args(ws)), C_.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    got = y.cpu().numpy()
+    assert np.isfinite(got).all()
+    assert maxabs(got, ref) <= 2e-5 * max(1.0, float(np.abs(ref).max()))
+    if ws is not None:
+        assert int(torch.count_nonzero(ws[:N.SPLITK_TICKETS])) == 0
+
+
 @pytest.mark.parametrize("precision,n_fused", [("f32", 22), ("split16", 22), ("auto", 22)])
 def test_fused_units_match_unfused_model(N, dev, precision, n_fused):
     """The v2 plan with fused residual units equals the conv-by-conv plan."""
