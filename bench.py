@@ -53,7 +53,7 @@ FAMILIES = {
                  PEAK_FP32_TFLOPS),
     "conv_split16": ("conv1d_split_kernel + split_reduce_kernel, split-f16 MFMA 32x32x16 (3 per fp32 MAC)",
                      PEAK_SPLIT16_TFLOPS),
-    "unit_f32": ("residual_unit_kernel, fp32 MFMA 32x32x2", PEAK_FP32_TFLOPS),
+    "unit_f32": ("unit_ring_f32_kernel / residual_unit_kernel, exact fp32 MFMA 32x32x2", PEAK_FP32_TFLOPS),
     "unit_split16": ("unit_split_kernel, split-f16 MFMA 32x32x16 (3 per fp32 MAC)", PEAK_SPLIT16_TFLOPS),
     "stack_split16": ("stack_split_kernel (3 residual units per launch), split-f16 MFMA 32x32x16",
                       PEAK_SPLIT16_TFLOPS),
