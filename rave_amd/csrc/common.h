@@ -136,6 +136,11 @@ __device__ __forceinline__ void vote_cast(unsigned char* v, int wave, float m) {
     const bool over = __builtin_amdgcn_ballot_w64(m >= kSplitLimit) != 0;
     if ((threadIdx.x & 63) == 0) v[wave] = over ? 1 : 0;
 }
+// the same byte from a per-lane flag (the unguarded pass's non-finite check)
+__device__ __forceinline__ void vote_cast_any(unsigned char* v, int wave, bool bad) {
+    const bool any = __builtin_amdgcn_ballot_w64(bad) != 0;
+    if ((threadIdx.x & 63) == 0) v[wave] = any ? 1 : 0;
+}
 template <int NW>
 __device__ __forceinline__ bool vote_any(const unsigned char* v) {
     if (!RAVE_SPLIT_GUARD) return false;

@@ -82,9 +82,15 @@ template <int C, int NB, int CB> struct SSGeo {
     static_assert(NBX % CB == 0 && ST % R == 0 && NT <= 1024, "geometry");
 };
 
-template <int C, int NB, int CB, bool SNAKE>
-__global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_kernel(SSArgs a) {
+// Range guard in two passes, as unit_split.hip: GUARD = false runs no guard
+// code; a non-finite centre sum (an operand past the f16 range became inf in its
+// hi half) makes the workgroup run the stack again with GUARD = true, whose
+// window / seams / between-unit planes vote and re-stage scaled.  Returns false
+// when the unguarded pass found one (the guarded pass rewrites its stores).
+template <int C, int NB, int CB, bool SNAKE, bool GUARD>
+__device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
     using G = SSGeo<C, NB, CB>;
+    constexpr bool GV = GUARD && RAVE_SPLIT_GUARD != 0;
     constexpr int NT = G::NT, PH = G::PH, XR = G::XR, G8 = G::G8, XT = G::XT, R = G::R;
     constexpr int S1 = G::S1, ST = G::ST, CG = G::CG, OFF = G::OFF;
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -215,9 +221,9 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
     int sh0 = 0;                                       // range-guard shift of the current unit's act0(y) planes
     {
         const float cmax = stage_window(1.0f);
-        vote_cast(vote, wave, cmax);
+        if constexpr (GV) vote_cast(vote, wave, cmax);
         __syncthreads();
-        if (__builtin_expect(vote_any<G::NW>(vote), 0)) {      // rare: a rolled re-staging loop
+        if (GV && __builtin_expect(vote_any<G::NW>(vote), 0)) {      // rare: a rolled re-staging loop
             sh0 = __builtin_amdgcn_readfirstlane(split_shift(block_max<G::NW>(cmax, vred)));
             const float xs = ldexpf(1.0f, -sh0);
 #pragma nounroll
@@ -293,10 +299,10 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
     auto guarded_planes = [&](const float (*v)[16], const float* al_tab, bool mask)
         __attribute__((always_inline)) {
         const float cmax = write_planes(v, al_tab, mask, 1.0f);
-        vote_cast(vote, wave, cmax);
+        if constexpr (GV) vote_cast(vote, wave, cmax);
         __syncthreads();
         int sh = 0;
-        if (__builtin_expect(vote_any<G::NW>(vote), 0)) {
+        if (GV && __builtin_expect(vote_any<G::NW>(vote), 0)) {
             sh = __builtin_amdgcn_readfirstlane(split_shift(block_max<G::NW>(cmax, vred)));
             (void)write_planes(v, al_tab, mask, ldexpf(1.0f, -sh));
             __syncthreads();
@@ -385,6 +391,19 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
         }
     }
 
+    // unguarded pass: a non-finite centre sum -> run again guarded (flag here,
+    // workgroup vote after the stores, which the guarded pass rewrites)
+    constexpr bool CHECK = !GUARD && RAVE_SPLIT_GUARD != 0;
+    bool bad = false;
+    if constexpr (CHECK) {
+#pragma unroll
+        for (int j = 0; j < CB; ++j) {
+            const int blk = wn * CB + j;
+            const bool ok = blk >= 1 && blk <= NB && ext0 + col0 + 32 * j < a.T;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bad |= ok && !__builtin_isfinite(yv[j][r]);
+        }
+    }
     // ------------------------------------------------------------ centre blocks -> y
     const auto yrs = ss_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
 #pragma unroll
@@ -399,6 +418,20 @@ __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_k
                                                   ok ? (unsigned)(m * a.y_sc + t) * 4u : kSSOOB, 0, RAVE_YAUX);
         }
     }
+    if constexpr (CHECK) {
+        vote_cast_any(vote, wave, bad);
+        __syncthreads();
+        if (__builtin_expect(vote_any<G::NW>(vote), 0)) {
+            __syncthreads();                           // every wave read the vote
+            return false;
+        }
+    }
+    return true;
+}
+
+template <int C, int NB, int CB, bool SNAKE>
+__global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_kernel(SSArgs a) {
+    if (!stack_split_body<C, NB, CB, SNAKE, RAVE_SPLIT_GUARD == 0>(a)) (void)stack_split_body<C, NB, CB, SNAKE, true>(a);
 }
 
 template <int C, int NB, int CB>

@@ -158,9 +158,22 @@ template <int C, int WGN, int MI, int KG = 1, int CB = 2, int RB = 1> struct USG
 // floats per lane in the split image's slots (rave_unit_ring_pack_weight),
 // eight v_mfma_f32_32x32x2_f32 per 16-deep K-step (K-slot (s, half h) =
 // channel 8h + s), no range guard, row scales 1.
-template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, bool F32, int RB>
-__device__ __forceinline__ void unit_split_body(const USArgs& a) {
+//
+// Range guard, RB == 1 (GUARD = false first): the body runs with no guard code
+// at all; an operand past the f16 range became inf in its hi half, so it shows
+// as a non-finite output sum.  Only when some wave of the workgroup holds one
+// (one vote per workgroup, before any store) does the workgroup run the body
+// again with GUARD = true: the window and the seam vote, and a block past
+// kSplitLimit is re-staged as v * 2^-s (rare: values past 2^15, or a genuine
+// inf / NaN input, which then passes through as in fp32).  The cooperative form
+// (RB > 1) runs guarded only (its members cannot repeat a hand-off alone).
+// Returns false when the unguarded pass found a non-finite sum (its stores are
+// then rewritten by the guarded pass).
+template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, bool F32, int RB, bool GUARD>
+__device__ __forceinline__ bool unit_split_body(const USArgs& a) {
     using G = USGeo<C, WGN, MI, KG, CB, RB>;
+    constexpr bool GV = GUARD && !F32 && RAVE_SPLIT_GUARD != 0;   // votes inside the body
+    static_assert(RB == 1 || GUARD || F32, "the cooperative form runs guarded");
     constexpr int NT = G::NT, PH = G::PH, G8 = G::G8, XT = G::XT, R = G::R;
     constexpr int S1 = G::S1, ST = G::ST, CG = C / 16;
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -188,7 +201,7 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
         const int q = blockIdx.x >> 3;
         rb = q % RB;
         lg = (blockIdx.x & 7) * (int)(gridDim.x / (8 * RB)) + q / RB;
-        if (lg >= a.ngroups) return;             // padding group (all its members leave)
+        if (lg >= a.ngroups) return true;        // padding group (all its members leave)
     }
     const int b = lg / a.ntiles;
     const int n0 = (lg - b * a.ntiles) * G::BN;
@@ -365,9 +378,9 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
             store_tab();
             cmax = stage_window(1.0f);
         }
-        if constexpr (!F32) vote_cast(vote, wave, cmax);
+        if constexpr (GV) vote_cast(vote, wave, cmax);
         __syncthreads();
-        if (!F32 && __builtin_expect(vote_any<G::NW>(vote), 0)) {
+        if (GV && __builtin_expect(vote_any<G::NW>(vote), 0)) {
             sh0 = __builtin_amdgcn_readfirstlane(split_shift(block_max<G::NW>(cmax, vred)));
             const float xs = ldexpf(1.0f, -sh0);
 #pragma nounroll
@@ -588,9 +601,9 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
     bool gave_up = false;                        // cooperative seam: a member never arrived
     if constexpr (RB == 1) {                     // range guard of h (rare path: h * 2^-sh2)
         const float cmax = seam(1.0f, IC<0>{});
-        if constexpr (!F32) vote_cast(vote, wave, cmax);
+        if constexpr (GV) vote_cast(vote, wave, cmax);
         __syncthreads();
-        if (!F32 && __builtin_expect(vote_any<G::NW>(vote), 0)) {
+        if (GV && __builtin_expect(vote_any<G::NW>(vote), 0)) {
             sh2 = __builtin_amdgcn_readfirstlane(split_shift(block_max<G::NW>(cmax, vred)));
             (void)seam(ldexpf(1.0f, -sh2), IC<0>{});
             __syncthreads();
@@ -716,7 +729,37 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
     }
     fold_acc();
     combine();
-    if (KG == 2 && kg == 1) return;                  // (no barrier follows)
+    // unguarded pass: any non-finite output sum of a live column -> run again
+    // guarded.  The flag is taken here; the workgroup vote follows the epilogue's
+    // stores (KG == 1: the second pass rewrites them; a barrier there costs no
+    // wave anything), or comes here (KG == 2: the partner waves leave below)
+    constexpr bool CHECK = !GUARD && !F32 && RAVE_SPLIT_GUARD != 0;
+    bool bad = false;
+    if constexpr (CHECK) {
+        if (KG == 1 || kg == 0) {
+#pragma unroll
+            for (int j = 0; j < CB; ++j) {
+                const bool nok = n0 + col0 + 32 * j < a.T;
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) bad |= nok && !__builtin_isfinite(acc[i][j][r]);
+            }
+        }
+    }
+    auto vote_rerun = [&]() __attribute__((always_inline)) {
+        vote_cast_any(vote, wave, bad);
+        __syncthreads();
+        if (__builtin_expect(vote_any<G::NW>(vote), 0)) {
+            __syncthreads();                         // every wave read the vote
+            return true;
+        }
+        return false;
+    };
+    if constexpr (CHECK && KG == 2) {
+        if (vote_rerun()) return false;
+    }
+    if (KG == 2 && kg == 1) return true;             // (no barrier follows)
 
     US_STAMP(4);
     // ------------------------------------------------------------ epilogue: y*rs2 + b2 + x
@@ -759,15 +802,24 @@ __device__ __forceinline__ void unit_split_body(const USArgs& a) {
             }
     }
     US_STAMP(5);
+    if constexpr (CHECK && KG == 1) {
+        if (vote_rerun()) return false;
+    }
+    return true;
 }
 
 template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, int RB>
 __global__ __launch_bounds__(64 * (C / (32 * MI * RB)) * WGN * KG) void unit_split_kernel(USArgs a) {
-    unit_split_body<C, WGN, MI, KG, CB, SNAKE, false, RB>(a);
+    if constexpr (RB > 1 || RAVE_SPLIT_GUARD == 0) {
+        (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, false, RB, true>(a);
+    } else {
+        if (!unit_split_body<C, WGN, MI, KG, CB, SNAKE, false, RB, false>(a))
+            (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, false, RB, true>(a);
+    }
 }
 template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, int RB>
 __global__ __launch_bounds__(64 * (C / (32 * MI * RB)) * WGN * KG) void unit_ring_f32_kernel(USArgs a) {
-    unit_split_body<C, WGN, MI, KG, CB, SNAKE, true, RB>(a);
+    (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, true, RB, false>(a);
 }
 
 template <int C, int WGN, int MI, int KG, int CB, int RB = 1>
@@ -1007,6 +1059,37 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
 #ifndef RAVE_U128_WGN
 #define RAVE_U128_WGN 2
 #endif
+    // exact fp32 (RAVE_PREC_F32_RING): its own geometry knobs (A/B builds; the
+    // defaults are the split form's)
+#ifndef RAVE_F64_WGN
+#define RAVE_F64_WGN RAVE_U64_WGN
+#endif
+#ifndef RAVE_F64_CB
+#define RAVE_F64_CB RAVE_U64_CB
+#endif
+#ifndef RAVE_F64_MI
+#define RAVE_F64_MI 1
+#endif
+#ifndef RAVE_F128_WGN
+#define RAVE_F128_WGN RAVE_U128_WGN
+#endif
+#ifndef RAVE_F128_CB
+#define RAVE_F128_CB 1
+#endif
+#ifndef RAVE_F128_MI
+#define RAVE_F128_MI 1
+#endif
+#ifndef RAVE_F256_WGN
+#define RAVE_F256_WGN 1
+#endif
+#ifndef RAVE_F256_CB
+#define RAVE_F256_CB 1
+#endif
+    if (a.precision == RAVE_PREC_F32_RING) {
+        if (C == 64) return go(IC<64>{}, IC<RAVE_F64_WGN>{}, IC<RAVE_F64_MI>{}, IC<1>{}, IC<RAVE_F64_CB>{}, IC<1>{});
+        if (C == 128) return go(IC<128>{}, IC<RAVE_F128_WGN>{}, IC<RAVE_F128_MI>{}, IC<1>{}, IC<RAVE_F128_CB>{}, IC<1>{});
+        if (C == 256) return go(IC<256>{}, IC<RAVE_F256_WGN>{}, IC<1>{}, IC<1>{}, IC<RAVE_F256_CB>{}, IC<1>{});
+    }
     if (C == 64) return go(IC<64>{}, IC<RAVE_U64_WGN>{}, IC<1>{}, IC<1>{}, IC<RAVE_U64_CB>{}, IC<1>{});
 #ifndef RAVE_U128_KG
 #define RAVE_U128_KG 1
