@@ -43,7 +43,8 @@ def main(path, bench=None):
     if bench:
         d = json.load(open(bench))
         fams = dict(d["roofline"]["families"])
-        fams.update(d.get("f32_exact", {}).get("roofline", {}).get("families", {}) or {})
+        for side in ("f32_exact", "split16_auto"):
+            fams.update(((d.get(side) or {}).get("roofline") or {}).get("families") or {})
         for f, v in fams.items():
             flop[f] = v.get("flop_per_launch_avg")
     out = {}
