@@ -19,13 +19,15 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from rocprof_summary import FAMILIES, classify  # noqa: E402
+from rocprof_summary import FAMILIES, classify, set_precision  # noqa: E402
 
 SIMDS = 1024          # 256 CUs x 4 SIMDs
 FLOP_PER_SIMD_CYCLE = 1024.0   # dense f16 MFMA: 2516.6 TFLOP/s / (1024 SIMDs x 2.4 GHz)
 
 
 def main(path, bench=None):
+    if bench:      # exact-fp32 runs: the edges and the split-K reduce belong to fp32 families
+        set_precision(json.load(open(bench)).get("precision", "auto"))
     busy, active, launches = defaultdict(float), defaultdict(float), defaultdict(set)
     with open(path, newline="") as fh:
         for r in csv.DictReader(fh):
