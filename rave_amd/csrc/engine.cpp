@@ -395,7 +395,8 @@ struct Model {
     float* scratch_buf(int64_t n);
 
     // planning
-    std::pair<int, int> conv_launch(const Node& n, const rave_conv1d_args& scalars, bool stream_form, bool timed);
+    std::pair<int, int> conv_launch(const Node& n, const rave_conv1d_args& scalars, bool stream_form, bool timed,
+                                    bool allow_ring = true);
     rave_conv1d_args conv_desc(const Node& n, int B, int t_in, const View& src, const View& dst, const View* res,
                                int& t_out) const;
     void conv_op(Plan& p, const Node& n, int B, int t_in, const View& src, const View& dst, const View* res);
@@ -527,7 +528,10 @@ static std::string key_of(std::initializer_list<std::string> parts) {
 // (precision, launch config) of one conv op; with autotune every arithmetic and
 // every configuration rave_conv1d_configs lists is timed on scratch tensors of
 // the op's shape and the fastest kept (its time is recorded for fusion choices).
-std::pair<int, int> Model::conv_launch(const Node& n, const rave_conv1d_args& s, bool stream_form, bool timed) {
+// allow_ring = false: the op's input rows are not 16-byte pieces (a stream
+// plan's history buffers), which the fp32 ring kernels need
+std::pair<int, int> Model::conv_launch(const Node& n, const rave_conv1d_args& s, bool stream_form, bool timed,
+                                       bool allow_ring) {
     auto& pack = stream_form ? w_pack_stream : w_pack;
     const std::string key = key_of({"conv", n.name, std::to_string(stream_form), std::to_string(s.batch),
                                     std::to_string(s.t_in)});
@@ -549,6 +553,7 @@ std::pair<int, int> Model::conv_launch(const Node& n, const rave_conv1d_args& s,
         base.partial = nullptr;
         std::vector<std::pair<int, int>> cands;
         for (int pr : precs) {
+            if (!allow_ring && pr == RAVE_PREC_F32_RING) continue;
             base.precision = pr;
             base.weight = aptr(pack.at({n.name, pr}));
             cands.push_back({pr, 0});
@@ -573,7 +578,10 @@ std::pair<int, int> Model::conv_launch(const Node& n, const rave_conv1d_args& s,
         }
         double best_ms = 1e30;
         std::pair<int, int> best{-1, -1};
+        std::set<int> bad;                           // arithmetics whose default launch failed
+        std::string why;
         for (auto& c : cands) {
+            if (bad.count(c.first)) continue;
             rave_conv1d_args a = base;
             a.precision = c.first;
             a.config = c.second;
@@ -581,9 +589,11 @@ std::pair<int, int> Model::conv_launch(const Node& n, const rave_conv1d_args& s,
             a.partial = ws;
             const double ms = time_native([&](hipStream_t st) { return rave_conv1d(&a, st); });
             if (ms < 0) {
+                // a failing default launch rules its arithmetic out for this shape
+                // (e.g. the fp32 ring kernels on rows that are not 16-byte pieces)
                 if (c.second == 0) {
-                    if (ws) (void)hipFree(ws);
-                    fail(RAVE_ERR_STATE, "conv " + n.name + ": default configuration failed: " + rave_last_error());
+                    bad.insert(c.first);
+                    why = rave_last_error();
                 }
                 continue;
             }
@@ -593,6 +603,7 @@ std::pair<int, int> Model::conv_launch(const Node& n, const rave_conv1d_args& s,
             }
         }
         if (ws) RAVE_HIP_OR_THROW(hipFree(ws));
+        if (best.first < 0) fail(RAVE_ERR_STATE, "conv " + n.name + ": default configuration failed: " + why);
         tuned[key] = {(int64_t)best.first * 65536 + best.second, best_ms};
     }
     auto it = tuned.find(key);
@@ -2242,7 +2253,11 @@ static void conv_stream(Model* m, Plan& p, const Node& n, int B, std::map<std::s
     a.y_sc = y.sc;
     a.r_sb = has_res ? res.sb : 0;
     a.r_sc = has_res ? res.sc : 0;
-    const auto pc = m->conv_launch(n, a, n.transposed, false);
+    // the fp32 ring kernels read 16-byte row pieces: workspace rows whose stride
+    // and start (the history offset) are multiples of 4 floats, t_in % 4 == 0
+    const bool vec_rows = x.p.kind == PRef::WS && x.sc % 4 == 0 && x.sb % 4 == 0 && x.p.off % 16 == 0 &&
+                          a.t_in % 4 == 0;
+    const auto pc = m->conv_launch(n, a, n.transposed, false, vec_rows);
     a.precision = pc.first;
     a.config = pc.second;
     auto& pack = n.transposed ? m->w_pack_stream : m->w_pack;   // ConvTranspose: the cached (out_shift 0) form

@@ -538,7 +538,7 @@ def test_batch_independence_and_determinism(dev, precision):
 
 
 # ------------------------------------------------------------------ streaming (BASELINE config 3)
-@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("precision", MODEL_PRECISIONS)
 def test_causal_streaming_golden(dev, golden, precision):
     """Block streaming (2048-sample blocks, persistent caches) reproduces the
     reference's cached_conv streaming outputs block for block."""
