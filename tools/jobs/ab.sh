@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of kernel variants on the GPU box (run through gpurun):
-#   bash tools/ab.sh <tag> <variant>...   ("" = the product librave_amd.so)
+#   bash tools/jobs/ab.sh <tag> <variant>...   ("" = the product librave_amd.so)
 # Per variant: the fixed-cost probe and a short bench (no CPU baseline, no
 # exact-fp32 pass); each GPU step has its own time limit, stop at the first failure.
 set -e -o pipefail

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of an environment switch on the whole bench step (alternating runs):
-#   tools/ab_env.sh TAG VAR   (VAR=0 vs VAR=1, e.g. RAVE_UNIT_COOP, RAVE_EDGES)
+#   tools/jobs/ab_env.sh TAG VAR   (VAR=0 vs VAR=1, e.g. RAVE_UNIT_COOP, RAVE_EDGES)
 set -e -o pipefail
 T=${1:-abenv}; V=${2:-RAVE_UNIT_COOP}; O=gpurun_out/$T; mkdir -p $O
 for i in 1 2 3; do

@@ -5,4 +5,4 @@ set -e -o pipefail
 O=gpurun_out/wt; mkdir -p $O
 RAVE_AMD_LIB_VARIANT=wt timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -k "conv or unit or stack or model_golden" --timeout 120 --timeout-method thread > $O/pytest_wt.log 2>&1
 echo "wt: $(tail -1 $O/pytest_wt.log)"
-TAG=wt bash tools/ab_xcd.sh "" wt
+TAG=wt bash tools/jobs/ab_xcd.sh "" wt

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Two SQ counter passes (each within one gfx950 pass budget) over single-layer
 # runs of tools/layer_bench.py; CSVs under gpurun_out/pmc_<tag>/.
-#   bash tools/pmc_layer.sh <tag> <layer_bench args...>
+#   bash tools/jobs/pmc_layer.sh <tag> <layer_bench args...>
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift

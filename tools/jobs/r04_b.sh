@@ -12,7 +12,7 @@ timeout -k 10 300 python -u -m pytest -q --timeout 120 --timeout-method thread -
 rc=$?; tail -2 "$OUT/pytest_gemv.log"; step_ok $rc || exit $rc
 timeout -k 10 900 python -u -m pytest -q --timeout 120 --timeout-method thread -m gpu tests > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; tail -2 "$OUT/pytest_gpu.log"; step_ok $rc || exit $rc
-bash tools/tuning_ab.sh ${1:-r04_b}/tuning_ab 2 || exit $?
+bash tools/jobs/tuning_ab.sh ${1:-r04_b}/tuning_ab 2 || exit $?
 R=$(pwd)
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$OUT/c3kt" -o run -- \

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-kernel mean of each SQ counter over the dispatches in rocprofv3
-counter_collection CSVs (tools/pmc_layer.sh)."""
+counter_collection CSVs (tools/jobs/pmc_layer.sh)."""
 import csv
 import sys
 from collections import defaultdict
