@@ -378,7 +378,7 @@ def _model(cfg, g, dev, golden, precision="f32"):
 
 
 PRECISIONS = ["f32", "split16", "auto"]
-# model-level modes: + exact fp32 with autotuned launch choices (bench.py's f32_exact pass)
+# model-level modes: + exact fp32 with autotuned launch choices (bench.py's headline mode)
 MODEL_PRECISIONS = PRECISIONS + ["f32_tuned"]
 
 
