@@ -141,7 +141,8 @@ constexpr int kHBP = 24;                            // halves per band-plane row
 constexpr int kHXS = 512 * (kHAB - 1) + 32 * 15 + kEdgeKW;   // window samples (5120 + 32)
 __host__ __device__ constexpr int e_xi(int i) { return i + 8 * (i >> 7); }   // 8 halves of pad per 128
 constexpr int kHXP = e_xi(kHXS) + 8;                // halves per window plane
-constexpr int kHeadLds = (2 * 16 * kEdgeFP + 2 * kHXP + 2 * kHBR * kHBP) * 2 + 4 * kEdgeWaves * 4 + 16;
+constexpr int kHeadLds = (2 * 16 * kEdgeFP + 2 * kHXP + 2 * kHBR * kHBP) * 2 + 4 * kEdgeWaves * 4 + 16 +
+                         kEdgeWaves * 64 * 4 * 4;        // + the split analysis block's partial sums
 
 template <bool F32>
 __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a, EdgeGeo geo) {
@@ -154,6 +155,7 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     _Float16* bh = xl + kHXP;                                      // [kHBR][kHBP]
     _Float16* bl = bh + kHBR * kHBP;
     float* red = reinterpret_cast<float*>(bl + kHBR * kHBP);
+    float* part = red + 4 * kEdgeWaves + 4;                        // [waves][64 lanes][4] (after the votes)
     // F32: one fp32 plane in the bytes of each (hi, lo) pair
     float* ff = reinterpret_cast<float*>(fh);                     // [16][kEdgeFP]
     float* xf = reinterpret_cast<float*>(xh);                     // [kHXP] flat, padded
@@ -268,6 +270,36 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
         }
         acc = (c0 + c1) + c2;
     };
+    // K-steps s0, s0 + waves, s0 + 2 waves of block blk (the block the waves share)
+    auto analysis_steps = [&](int blk, e_f32x4& acc, int s0) __attribute__((always_inline)) {
+        e_f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0;
+#pragma unroll
+        for (int j = 0; j < (kEdgeKW / 32 + kEdgeWaves - 1) / kEdgeWaves; ++j) {
+            const int s = s0 + kEdgeWaves * j;
+            if (s >= kEdgeKW / 32) break;               // (wave-uniform)
+            if constexpr (F32) {
+                const e_f32x8 af = e_ld8(ff + col * kEdgeFP + 32 * s + 8 * g);
+                const e_f32x8 xf8 = e_ld8(xf + e_xi(512 * blk + 32 * col + 32 * s + 8 * g));
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[e], xf8[e], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[e + 1], xf8[e + 1], c1, 0, 0, 0);
+                }
+            } else {
+                const int ka = col * kEdgeFP + 32 * s + 8 * g;
+                const e_h8 ah = *reinterpret_cast<const e_h8*>(fh + ka);
+                const e_h8 al = *reinterpret_cast<const e_h8*>(fl + ka);
+                const e_h8 a2 = ah * (_Float16)2048.0f;
+                const int xi = e_xi(512 * blk + 32 * col + 32 * s + 8 * g);
+                const e_h8 xh8 = *reinterpret_cast<const e_h8*>(xh + xi);
+                const e_h8 xl8 = *reinterpret_cast<const e_h8*>(xl + xi);
+                c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, xh8, c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, xl8, c1, 0, 0, 0);
+                c2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, xh8, c2, 0, 0, 0);
+            }
+        }
+        acc = (c0 + c1) + c2;
+    };
     // acc rows 4g + r = (p = g >> 1, k = 4 (g & 1) + r); value = band k of frame
     // g0 + 32 blk + 2 col + p (reverse_half, zero outside [0, F))
     const float unscale = f_unscale / xs;
@@ -288,10 +320,22 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     float bmax = 0.f;
     analysis_block(wave, acc0);
     band_values(wave, acc0, v0, bmax);
-    const bool extra = wave + kEdgeWaves < kHAB;
+    // the ninth block (kHAB = waves + 1): its K-steps split over every wave, the
+    // partial sums added in wave order (fixed: reproducible) by wave 0, so that
+    // no wave computes two whole blocks
+    static_assert(kHAB == kEdgeWaves + 1, "one shared analysis block");
+    {
+        e_f32x4 pacc;
+        analysis_steps(kEdgeWaves, pacc, wave);
+        *reinterpret_cast<e_f32x4*>(part + (wave * 64 + lane) * 4) = pacc;
+    }
+    __syncthreads();
+    const bool extra = wave == 0;
     if (extra) {
-        analysis_block(wave + kEdgeWaves, acc1);
-        band_values(wave + kEdgeWaves, acc1, v1, bmax);
+        acc1 = *reinterpret_cast<const e_f32x4*>(part + lane * 4);
+#pragma unroll
+        for (int w2 = 1; w2 < kEdgeWaves; ++w2) acc1 += *reinterpret_cast<const e_f32x4*>(part + (w2 * 64 + lane) * 4);
+        band_values(kEdgeWaves, acc1, v1, bmax);
     }
     auto put_bands = [&](int blk, const e_f32x4& v, float bs) __attribute__((always_inline)) {
         const int row = 32 * blk + 2 * col + (g >> 1);
@@ -345,13 +389,22 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     for (int q = 0; q < kEdgeK7; ++q) {
         const int row = 32 * wave + l32 + q;
         if constexpr (F32) {
-            const e_f32x8 x8 = e_ld8(bf + row * kHBP + 8 * h);
+            // K pairs of input channels (2e, 2e + 1) on the two lane halves: ceil(c_in / 2)
+            // MFMAs per tap instead of 8 (the image's lane half 1 holds channels 8-15, all
+            // zero for the <= 8 bands here; lane half 0 holds channels 0-7)
+            const e_f32x8 x8 = e_ld8(bf + row * kHBP);
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 if (j >= MB) break;
                 const e_f32x8 w8 = EdgeW::f32(wr[q][j][0], wr[q][j][1]);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(x8[e], w8[e], acc[j], 0, 0, 0);
+                for (int e = 0; e < 4; ++e) {
+                    if (2 * e >= a.conv_c_in) break;                    // (wave-uniform)
+                    const float w_odd = __shfl(w8[2 * e + 1], l32);    // lane half 0's channel 2e + 1
+                    const float wv = h ? w_odd : w8[2 * e];
+                    const float xv = h ? x8[2 * e + 1] : x8[2 * e];
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(xv, wv, acc[j], 0, 0, 0);
+                }
             }
             continue;
         }
