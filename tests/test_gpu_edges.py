@@ -49,16 +49,20 @@ def _filters(golden):
     return pqmf_filters(hk)
 
 
+HEAD_CASES = [(600, 2, 1.0, 6), (4096, 3, 1.0, 6), (257, 1, 3e6, 6),
+              (600, 2, 1.0, 5), (600, 1, 1.0, 8)]     # odd / full band counts: the fp32 conv's channel pairs
+
+
 @pytest.mark.parametrize("prec", ["split16", "f32_ring"])
 @pytest.mark.parametrize("causal", [False, True])
-@pytest.mark.parametrize("F,B,scale", [(600, 2, 1.0), (4096, 3, 1.0), (257, 1, 3e6)])
-def test_encoder_head(N, dev, golden, causal, F, B, scale, prec):
+@pytest.mark.parametrize("F,B,scale,nb", HEAD_CASES)
+def test_encoder_head(N, dev, golden, causal, F, B, scale, nb, prec):
     from oracle.rave_oracle import conv1d, get_padding, reverse_half
     hkf, _ = _filters(golden)
-    rng = np.random.default_rng(F + 7 * causal)
+    rng = np.random.default_rng(F + 7 * causal + nb)
     T = 16 * F
     x = (scale * (0.3 * np.sin(np.arange(T) * 0.05)[None, None] + 0.1 * rng.standard_normal((B, 1, T)))).astype(np.float32)
-    nb, co, k = 6, 64, 7
+    co, k = 64, 7
     w = (rng.uniform(-1, 1, (co, nb, k)) / np.sqrt(nb * k)).astype(np.float32)
     b = (0.1 * rng.standard_normal(co)).astype(np.float32)
     bands = reverse_half(conv1d(x.astype(np.float64), hkf.astype(np.float64), None, stride=16,
