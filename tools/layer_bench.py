@@ -29,6 +29,7 @@ LAYERS = {
     "down4_64": (64, 128, 8, 4, 1, 0, "leaky", False, 4096),
     "down2_256": (256, 512, 4, 2, 1, 0, "leaky", False, 256),
     "convT2_1024": (1024, 512, 4, 2, 1, 1, "leaky", False, 64),
+    "down2_512": (512, 1024, 4, 2, 1, 0, "leaky", False, 128),
     "convT4_128": (128, 64, 8, 4, 1, 1, "leaky", False, 1024),
     "enc_out": (1024, 64, 3, 1, 1, 0, "leaky", False, 64),
     "dec_in": (320, 1024, 3, 1, 1, 0, "none", False, 64),
