@@ -48,6 +48,8 @@ PEAK_F16_TFLOPS = 2516.6      # MI355X dense F16 MFMA (256 CU x 4 SIMD x 1024 FL
 # split16 issues three f16 MFMAs (hi*hi, hi*lo, lo*hi) per fp32 multiply-accumulate,
 # so its ceiling in fp32-op FLOP is a third of the f16 peak
 PEAK_SPLIT16_TFLOPS = round(PEAK_F16_TFLOPS / 3, 1)
+# bf16x3 issues six bf16 MFMAs per fp32 multiply-accumulate (bf16 peak = f16 peak)
+PEAK_BF3_TFLOPS = round(PEAK_F16_TFLOPS / 6, 1)
 SR = 48000
 
 # GEMM-shaped kernel families of a step: name -> (kernels, peak in fp32-op TFLOP/s).
@@ -59,6 +61,8 @@ FAMILIES = {
                      PEAK_SPLIT16_TFLOPS),
     "unit_f32": ("unit_ring_f32_kernel / residual_unit_kernel, exact fp32 MFMA 32x32x2", PEAK_FP32_TFLOPS),
     "unit_split16": ("unit_split_kernel, split-f16 MFMA 32x32x16 (3 per fp32 MAC)", PEAK_SPLIT16_TFLOPS),
+    "unit_bf16x3": ("unit_bf3_kernel, fp32 as exact bf16x3 operands, bf16 MFMA 32x32x16 (6 per fp32 MAC)",
+                    PEAK_BF3_TFLOPS),
     "stack_split16": ("stack_split_kernel (3 residual units per launch), split-f16 MFMA 32x32x16",
                       PEAK_SPLIT16_TFLOPS),
     "pqmf_analysis_f32": ("pqmf_analysis_kernel, fp32 MFMA 16x16x4", PEAK_FP32_TFLOPS),
@@ -81,6 +85,8 @@ FAMILIES = {
 def op_family(kind: int, precision: int) -> str:
     from rave_amd import _native as N
     prec = "split16" if precision == N.PREC_SPLIT16 else "f32"
+    if kind == N.OP_UNIT and precision == N.PREC_BF16X3:
+        return "unit_bf16x3"
     if kind == N.OP_CONV:
         return "conv_" + prec
     if kind == N.OP_UNIT:
@@ -174,6 +180,9 @@ DTYPE = {"f32": "fp32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32)",
          "f32_tuned": "fp32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32 on every op; per conv the faster of the "
                       "register-staged kernel and the LDS-DMA ring kernel, launch configurations and "
                       "fused/unfused units autotuned)",
+         "f32_bf3": "fp32 (every op exact-fp32 MFMA or, per fused unit where faster, fp32 on the bf16 matrix "
+                    "cores: operands split exactly into 3 bf16 parts (24 significand bits), 6 of the 9 cross "
+                    "products (the 3 dropped are each < 2^-25 |a b|), fp32 accumulate)",
          "split16": "fp32 I/O, split-f16 GEMMs (3 f16 MFMA passes hi*hi+hi*lo+lo*hi on ~22-bit operands, "
                     "fp32 accumulate)",
          "auto": "fp32 I/O; per op the faster of exact-fp32 MFMA and split-f16 GEMMs (3 f16 MFMA passes on "
@@ -447,7 +456,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
     ap.add_argument("--samples", type=int, default=65536, help="samples per clip")
     ap.add_argument("--config", default="v2")
-    ap.add_argument("--precision", default="f32_tuned", choices=["f32", "f32_tuned", "split16", "auto"],
+    ap.add_argument("--precision", default="f32_tuned", choices=["f32", "f32_tuned", "f32_bf3", "split16", "auto"],
                     help="conv/unit GEMM arithmetic of the headline (include/rave_amd.h RAVE_PREC_*). "
                          "Default f32_tuned: exact fp32 MFMA on every op (the reference's arithmetic), "
                          "launch choices pinned; auto = per op the faster of exact fp32 and split-f16")

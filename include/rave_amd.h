@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 15
+#define RAVE_ABI_VERSION 16
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 /* The last of those words is reserved: no conv ticket uses it.  A cooperative
@@ -86,6 +86,14 @@ enum { RAVE_PREC_F32 = 0, RAVE_PREC_SPLIT16 = 1 };
  *                      packed with rave_conv1d_ring_pack_weight (sizes as the split
  *                      image).  Value 4: 2 and 3 are model-level modes below. */
 #define RAVE_PREC_F32_RING 4
+/*   RAVE_PREC_BF16X3   fp32 on the bf16 matrix cores (fused units, C in {64, 128, 256}):
+ *                      every operand split exactly into three bf16 parts
+ *                      (v = hi + mid + lo, 24 significand bits, the fp32 exponent
+ *                      range: no row scales, no range guard); six
+ *                      v_mfma_f32_32x32x16_bf16 products per K-step (all cross
+ *                      products but mid*lo, lo*mid, lo*lo: each < 2^-25 |a b|) into one
+ *                      fp32 accumulator.  Weights packed with rave_unit_bf3_pack_weight. */
+#define RAVE_PREC_BF16X3 5
 
 const char* rave_last_error(void);
 int rave_abi_version(void);
@@ -347,6 +355,11 @@ int rave_unit_split_pack_weight(const float* w1, const float* w2, int channels, 
  * the split image's layout with 8 fp32 values per lane and K-step, row scales 1
  * (sizes as rave_unit_split_packed_size). */
 int rave_unit_ring_pack_weight(const float* w1, const float* w2, int channels, float* packed);
+/* RAVE_PREC_BF16X3 unit weights (C in {64, 128, 256}; else -1 / RAVE_ERR_UNSUPPORTED):
+ * (hi, lo, mid) bf16 A-fragments per 32-row block and K-step, then the two
+ * row-scale vectors (all 1). */
+int64_t rave_unit_bf3_packed_size(int channels);
+int rave_unit_bf3_pack_weight(const float* w1, const float* w2, int channels, float* packed);
 /* Workspace (floats) of the cooperative fused unit (C in {256, 512}, RAVE_PREC_SPLIT16 /
  * RAVE_PREC_F32_RING): groups of C/128 workgroups share a 32-column slab, each owning
  * C/(C/128) output rows of both GEMMs, and hand the intermediate act2(h) rows to each
@@ -609,6 +622,9 @@ int rave_maxpool(const rave_maxpool_args* a, void* stream);
 enum { RAVE_PREC_AUTO = 2,     /* per op the faster of F32 / SPLIT16, timed at plan build */
        RAVE_PREC_F32_TUNED = 3 /* exact fp32 on every op; launch configurations and fused /
                                   unfused unit choices timed at plan build as in AUTO */ };
+/* fp32 on every op with the fused units also timed in RAVE_PREC_BF16X3 (exact
+ * operand split, fp32 accumulation): per op the fastest of F32 / F32_RING / BF16X3 */
+#define RAVE_PREC_F32_BF3 6
 
 typedef struct rave_model_config {
     int32_t n_band;               /* PQMF bands (v1.gin: 16)                                */

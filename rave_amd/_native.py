@@ -42,7 +42,7 @@ OP_UNIT = 11
 OP_STACK = 12
 OP_HEAD = 13
 OP_TAIL = 14
-ABI_VERSION = 15
+ABI_VERSION = 16
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 SPLITK_STATUS_WORD = SPLITK_TICKETS - 1   # RAVE_SPLITK_STATUS_WORD: the cooperative unit's give-up word
 
@@ -52,7 +52,9 @@ PREC_SPLIT16 = 1
 PREC_AUTO = 2
 PREC_F32_TUNED = 3      # exact fp32, launch choices autotuned (RAVE_PREC_F32_TUNED)
 PREC_F32_RING = 4       # exact fp32 on the split16 kernels' staging machinery (RAVE_PREC_F32_RING)
-PRECISION = {"f32": PREC_F32, "split16": PREC_SPLIT16, "f32_ring": PREC_F32_RING}
+PREC_BF16X3 = 5         # fp32 on the bf16 matrix cores, exact 3-way operand split (RAVE_PREC_BF16X3)
+PREC_F32_BF3 = 6        # model mode: per op the fastest of F32 / F32_RING / BF16X3 (RAVE_PREC_F32_BF3)
+PRECISION = {"f32": PREC_F32, "split16": PREC_SPLIT16, "f32_ring": PREC_F32_RING, "bf16x3": PREC_BF16X3}
 STREAM_GRAPH = 1
 STREAM_ENCODE_ONLY = 2
 STREAM_DECODE_ONLY = 4
@@ -243,6 +245,7 @@ EXPORTS = [
     "rave_rvq_workspace", "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
     "rave_unit_packed_size", "rave_unit_pack_weight", "rave_residual_unit",
     "rave_unit_split_packed_size", "rave_unit_split_pack_weight", "rave_unit_ring_pack_weight",
+    "rave_unit_bf3_packed_size", "rave_unit_bf3_pack_weight",
     "rave_unit_workspace", "rave_debug_coop", "rave_model_check",
     "rave_stack_supported", "rave_residual_stack",
     "rave_plan_create", "rave_plan_run", "rave_plan_destroy", "rave_plan_size",
@@ -301,6 +304,9 @@ def _load():
     lib.rave_unit_split_packed_size.restype = i64
     lib.rave_unit_split_pack_weight.argtypes = [vp, vp, C.c_int, vp]
     lib.rave_unit_ring_pack_weight.argtypes = [vp, vp, C.c_int, vp]
+    lib.rave_unit_bf3_packed_size.argtypes = [C.c_int]
+    lib.rave_unit_bf3_packed_size.restype = i64
+    lib.rave_unit_bf3_pack_weight.argtypes = [vp, vp, C.c_int, vp]
     lib.rave_conv1d_workspace.restype = i64
     lib.rave_rvq_workspace.argtypes = [C.POINTER(RvqArgs)]
     lib.rave_rvq_workspace.restype = i64
@@ -476,17 +482,21 @@ def stack_supported(channels: int) -> bool:
 
 
 def unit_supported(channels: int, precision: int = PREC_F32) -> bool:
-    size_fn = lib.rave_unit_packed_size if precision == PREC_F32 else lib.rave_unit_split_packed_size
+    size_fn = (lib.rave_unit_packed_size if precision == PREC_F32 else lib.rave_unit_bf3_packed_size
+               if precision == PREC_BF16X3 else lib.rave_unit_split_packed_size)
     return int(size_fn(int(channels))) > 0
 
 
 def pack_unit_weight(w1, w2, channels, precision=PREC_F32):
     """Fused residual unit weights: W1 (C, C, 3) and W2 (C, C, 1) -> packed float32
-    (PREC_SPLIT16: f16 fragment image + row scales, in 4-byte units)."""
+    (PREC_SPLIT16: f16 fragment image + row scales, in 4-byte units; PREC_BF16X3:
+    bf16 (hi, lo, mid) fragment image)."""
     import numpy as np
     size_fn, pack_fn = ((lib.rave_unit_packed_size, lib.rave_unit_pack_weight) if precision == PREC_F32
                         else (lib.rave_unit_split_packed_size, lib.rave_unit_ring_pack_weight)
                         if precision == PREC_F32_RING
+                        else (lib.rave_unit_bf3_packed_size, lib.rave_unit_bf3_pack_weight)
+                        if precision == PREC_BF16X3
                         else (lib.rave_unit_split_packed_size, lib.rave_unit_split_pack_weight))
     n = int(size_fn(int(channels)))
     if n <= 0:

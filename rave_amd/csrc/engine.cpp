@@ -554,6 +554,7 @@ std::pair<int, int> Model::conv_launch(const Node& n, const rave_conv1d_args& s,
         std::vector<std::pair<int, int>> cands;
         for (int pr : precs) {
             if (!allow_ring && pr == RAVE_PREC_F32_RING) continue;
+            if (!pack.count({n.name, pr})) continue;     // (an arithmetic of the fused units only)
             base.precision = pr;
             base.weight = aptr(pack.at({n.name, pr}));
             cands.push_back({pr, 0});
@@ -1638,8 +1639,10 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
     if (precision == RAVE_PREC_AUTO) m->precs = {RAVE_PREC_F32, RAVE_PREC_SPLIT16};
     else if (precision == RAVE_PREC_F32 || precision == RAVE_PREC_SPLIT16) m->precs = {precision};
     else if (precision == RAVE_PREC_F32_TUNED) m->precs = {RAVE_PREC_F32, RAVE_PREC_F32_RING};
-    else fail(RAVE_ERR_ARG, "precision must be RAVE_PREC_F32, RAVE_PREC_SPLIT16, RAVE_PREC_AUTO or RAVE_PREC_F32_TUNED");
-    m->autotune = precision == RAVE_PREC_AUTO || precision == RAVE_PREC_F32_TUNED;
+    else if (precision == RAVE_PREC_F32_BF3) m->precs = {RAVE_PREC_F32, RAVE_PREC_F32_RING, RAVE_PREC_BF16X3};
+    else fail(RAVE_ERR_ARG, "precision must be RAVE_PREC_F32, RAVE_PREC_SPLIT16, RAVE_PREC_AUTO, RAVE_PREC_F32_TUNED "
+                            "or RAVE_PREC_F32_BF3");
+    m->autotune = precision == RAVE_PREC_AUTO || precision == RAVE_PREC_F32_TUNED || precision == RAVE_PREC_F32_BF3;
     m->hop = cfg.n_band;
     for (int i = 0; i < cfg.n_ratios; ++i) m->hop *= cfg.ratios[i];
     m->dec_in = cfg.latent_size + cfg.speaker_size;
@@ -1675,6 +1678,7 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
                                               : std::vector<float>(get(n->name + ".weight"),
                                                                    get(n->name + ".weight") + rows * per_row);
         for (int pr : m->precs) {
+            if (pr == RAVE_PREC_BF16X3) continue;    // (fused units only)
             for (int form = 0; form < (n->transposed ? 2 : 1); ++form) {
                 const int os = n->transposed ? (form == 0 ? n->stride / 2 : 0) : 0;
                 // split16 and the fp32 ring path share the fragment image layout
@@ -1714,11 +1718,14 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
             for (int p : m->precs) {
                 // split16 and the fp32 ring kernel share the fragment image layout
                 const bool sp = p == RAVE_PREC_SPLIT16 || p == RAVE_PREC_F32_RING;
-                const int64_t sz = sp ? rave_unit_split_packed_size(C_) : rave_unit_packed_size(C_);
+                const int64_t sz = p == RAVE_PREC_BF16X3 ? rave_unit_bf3_packed_size(C_)
+                                   : sp                  ? rave_unit_split_packed_size(C_)
+                                                         : rave_unit_packed_size(C_);
                 if (sz <= 0) continue;
                 std::vector<float> packed((size_t)sz, 0.f);
-                check_rc(p == RAVE_PREC_SPLIT16 ? rave_unit_split_pack_weight(w1.data(), w2.data(), C_, packed.data())
+                check_rc(p == RAVE_PREC_SPLIT16    ? rave_unit_split_pack_weight(w1.data(), w2.data(), C_, packed.data())
                          : p == RAVE_PREC_F32_RING ? rave_unit_ring_pack_weight(w1.data(), w2.data(), C_, packed.data())
+                         : p == RAVE_PREC_BF16X3   ? rave_unit_bf3_pack_weight(w1.data(), w2.data(), C_, packed.data())
                                                    : rave_unit_pack_weight(w1.data(), w2.data(), C_, packed.data()),
                          "unit pack " + k3.name);
                 m->unit_pack[{k3.name, p}] = m->add(packed);

@@ -357,7 +357,8 @@ int residual_unit_split(const rave_unit_args& a, void* stream);   // unit_split.
 extern "C" int rave_residual_unit(const rave_unit_args* p, void* stream) {
     RAVE_CHECK_ARG(p && p->x && p->y && p->weight, "residual_unit: null pointer");
     const rave_unit_args& a = *p;
-    RAVE_CHECK_ARG(a.precision == RAVE_PREC_F32 || a.precision == RAVE_PREC_SPLIT16 || a.precision == RAVE_PREC_F32_RING,
+    RAVE_CHECK_ARG(a.precision == RAVE_PREC_F32 || a.precision == RAVE_PREC_SPLIT16 || a.precision == RAVE_PREC_F32_RING ||
+                       a.precision == RAVE_PREC_BF16X3,
                    "residual_unit: unknown precision");
     if (!unit_supported(a.channels)) {
         set_error("residual_unit: fused residual unit supports C in {64, 128, 256, 512}");
@@ -378,7 +379,8 @@ extern "C" int rave_residual_unit(const rave_unit_args* p, void* stream) {
                        "residual_unit: x_len / res_shift leave the residual outside x");
         RAVE_CHECK_ARG(a.x_len <= 0 || a.x_sc >= xl, "residual_unit: x_len exceeds the row stride");
     }
-    if (a.precision == RAVE_PREC_SPLIT16 || a.precision == RAVE_PREC_F32_RING) return residual_unit_split(a, stream);
+    if (a.precision == RAVE_PREC_SPLIT16 || a.precision == RAVE_PREC_F32_RING || a.precision == RAVE_PREC_BF16X3)
+        return residual_unit_split(a, stream);
     const int C = a.channels;
     UnitKArgs k{};
     k.x = a.x; k.y = a.y; k.w = a.weight;

@@ -55,6 +55,18 @@ typedef float us_f32x8 __attribute__((ext_vector_type(8)));
 typedef float us_f32x4 __attribute__((ext_vector_type(4)));
 typedef float us_f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned us_u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 us_b8 __attribute__((ext_vector_type(8)));
+typedef __bf16 us_b4 __attribute__((ext_vector_type(4)));
+
+// fp32 -> three bf16 parts with v == hi + mid + lo exactly (8 + 8 + 8 bits of
+// the 24-bit significand; each remainder is exact in fp32)
+template <typename FV, typename BV>
+__device__ __forceinline__ void bf3_split(const FV& v, BV& hi, BV& mid, BV& lo) {
+    hi = __builtin_convertvector(v, BV);
+    const FV r = v - __builtin_convertvector(hi, FV);
+    mid = __builtin_convertvector(r, BV);
+    lo = __builtin_convertvector(r - __builtin_convertvector(mid, FV), BV);
+}
 
 constexpr int kUSMaxDil = 16;
 #ifndef RAVE_US_R
@@ -130,7 +142,7 @@ __device__ __forceinline__ float us_act(float v, float slope, float alpha) {
 
 // C channels; WGN waves along time (each 64 columns); C/(32 MI) waves along
 // rows (each MI 32-row blocks).
-template <int C, int WGN, int MI, int KG = 1, int CB = 2, int RB = 1> struct USGeo {
+template <int C, int WGN, int MI, int KG = 1, int CB = 2, int RB = 1, int NP = 2> struct USGeo {
     static constexpr int WGM = C / (32 * MI * RB), NWT = WGM * WGN, NW = NWT * KG, NT = 64 * NW;
     static constexpr int BN = 32 * CB * WGN;           // CB 32-column blocks per wave
     static constexpr int S1 = 3 * C / 16, S2 = C / 16, ST = S1 + S2;   // K-steps
@@ -138,7 +150,8 @@ template <int C, int WGN, int MI, int KG = 1, int CB = 2, int RB = 1> struct USG
     static constexpr int XW_MAX = BN + 2 * kUSMaxDil;
     static constexpr int XPLANE = XW_MAX * PH * 2;    // bytes per f16 plane
     static constexpr int HPLANE = BN * PH * 2;
-    static constexpr int PLANES = 2 * (XPLANE > HPLANE ? XPLANE : HPLANE);
+    static constexpr int PL1 = XPLANE > HPLANE ? XPLANE : HPLANE;   // bytes per plane
+    static constexpr int PLANES = NP * PL1;           // NP = 2 (hi, lo) or 3 (bf16x3: hi, lo, mid)
     // + per-row table: rs1 b1 a2 | rs2 b2 a0, + range-guard votes (16 B) and wave maxima (16 floats)
     static constexpr int TAB = PLANES, VOTE = PLANES + 6 * C * 4, VRED = VOTE + 16;
     static constexpr int LDS = VRED + 64;
@@ -159,6 +172,14 @@ template <int C, int WGN, int MI, int KG = 1, int CB = 2, int RB = 1> struct USG
 // eight v_mfma_f32_32x32x2_f32 per 16-deep K-step (K-slot (s, half h) =
 // channel 8h + s), no range guard, row scales 1.
 //
+// BF (RAVE_PREC_BF16X3, RB == 1 only): fp32 on the bf16 matrix cores.  Every
+// operand v is split exactly as hi + mid + lo (bf16 each: 24 significand bits,
+// the fp32 exponent range, so no row scales and no range guard); three planes
+// (hi, lo, mid) in LDS and three weight fragments per K-step; six
+// v_mfma_f32_32x32x16_bf16 per K-step take every cross product but mid*lo,
+// lo*mid and lo*lo (each below 2^-25 of |a b|, under fp32's own rounding of a
+// product), smallest first, into one fp32 accumulator.
+//
 // Range guard, RB == 1 (GUARD = false first): the body runs with no guard code
 // at all; an operand past the f16 range became inf in its hi half, so it shows
 // as a non-finite output sum.  Only when some wave of the workgroup holds one
@@ -169,16 +190,19 @@ template <int C, int WGN, int MI, int KG = 1, int CB = 2, int RB = 1> struct USG
 // (RB > 1) runs guarded only (its members cannot repeat a hand-off alone).
 // Returns false when the unguarded pass found a non-finite sum (its stores are
 // then rewritten by the guarded pass).
-template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, bool F32, int RB, bool GUARD>
+template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, int AR, int RB, bool GUARD>
 __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
-    using G = USGeo<C, WGN, MI, KG, CB, RB>;
-    constexpr bool GV = GUARD && !F32 && RAVE_SPLIT_GUARD != 0;   // votes inside the body
+    constexpr bool F32 = AR == 1, BF = AR == 2;      // arithmetic: 0 split16, 1 fp32, 2 bf16x3
+    constexpr int NPW = BF ? 3 : 2;                  // operand planes / weight fragments per K-step
+    using G = USGeo<C, WGN, MI, KG, CB, RB, NPW>;
+    constexpr bool GV = GUARD && AR == 0 && RAVE_SPLIT_GUARD != 0;   // votes inside the body
     static_assert(RB == 1 || GUARD || F32, "the cooperative form runs guarded");
     constexpr int NT = G::NT, PH = G::PH, G8 = G::G8, XT = G::XT, R = G::R;
     constexpr int S1 = G::S1, ST = G::ST, CG = C / 16;
     extern __shared__ __attribute__((aligned(16))) char lds[];
     _Float16* ph = reinterpret_cast<_Float16*>(lds);
-    _Float16* pl = reinterpret_cast<_Float16*>(lds + G::PLANES / 2);
+    _Float16* pl = reinterpret_cast<_Float16*>(lds + G::PL1);
+    _Float16* pm = reinterpret_cast<_Float16*>(lds + 2 * G::PL1);   // BF: the mid plane
     float* pf = reinterpret_cast<float*>(lds);                 // F32: the fp32 plane
     float* tab = reinterpret_cast<float*>(lds + G::TAB);      // [6][C]
     unsigned char* vote = reinterpret_cast<unsigned char*>(lds + G::VOTE);
@@ -217,16 +241,16 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
     // ------------------------------------------------------------ weight ring
     // this wave's m-blocks MI*wm .. MI*wm+MI-1; fragment (mb, s, plane) at ((mb*ST + s)*2 + plane) KB
     // (ring slot = this wave's local step t % R; s = the global K-step, t*KG + kg)
-    us_h8 ring[R][MI][2];
+    us_h8 ring[R][MI][NPW];
     const int wmg = wm + rb * G::WGM;                // this wave's row-block index in the unit
-    const unsigned abase = (unsigned)((MI * wmg) * ST * 2) * 1024u + (unsigned)lane * 16u;
+    const unsigned abase = (unsigned)((MI * wmg) * ST * NPW) * 1024u + (unsigned)lane * 16u;
     auto load_a = [&](int slot, int s) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int p = 0; p < 2; ++p)
+            for (int p = 0; p < NPW; ++p)
                 ring[slot][i][p] = __builtin_bit_cast(us_h8, __builtin_amdgcn_raw_buffer_load_b128(
-                    wrs, s < ST ? abase + (unsigned)(((i * ST + s) * 2 + p) * 1024) : kUSOOB, 0, 0));
+                    wrs, s < ST ? abase + (unsigned)(((i * ST + s) * NPW + p) * 1024) : kUSOOB, 0, 0));
     };
     // (the 16-byte window path issues the ring's first fill after its window
     // loads, so the window's wait does not include the weights)
@@ -294,6 +318,14 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
                     *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8) = us_f32x4{v8[0], v8[1], v8[2], v8[3]};
                     *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8 + 4) = us_f32x4{v8[4], v8[5], v8[6], v8[7]};
                 }
+            } else if constexpr (BF) {
+                us_b8 hi, mid, lo;
+                bf3_split(v8, hi, mid, lo);
+                if (e < ntask) {
+                    *reinterpret_cast<us_b8*>(ph + w * PH + g * 8) = hi;
+                    *reinterpret_cast<us_b8*>(pl + w * PH + g * 8) = lo;
+                    *reinterpret_cast<us_b8*>(pm + w * PH + g * 8) = mid;
+                }
             } else {
                 cmax = fmaxf(cmax, absmax8(v8));
                 const us_h8 hi = __builtin_convertvector(v8, us_h8);
@@ -355,6 +387,12 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
                     if constexpr (F32) {
                         *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8) = us_f32x4{v8[0], v8[1], v8[2], v8[3]};
                         *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8 + 4) = us_f32x4{v8[4], v8[5], v8[6], v8[7]};
+                    } else if constexpr (BF) {
+                        us_b8 hi, mid, lo;
+                        bf3_split(v8, hi, mid, lo);
+                        *reinterpret_cast<us_b8*>(ph + w * PH + g * 8) = hi;
+                        *reinterpret_cast<us_b8*>(pl + w * PH + g * 8) = lo;
+                        *reinterpret_cast<us_b8*>(pm + w * PH + g * 8) = mid;
                     } else {
                         cmax = fmaxf(cmax, absmax8(v8));
                         const us_h8 hi = __builtin_convertvector(v8, us_h8);
@@ -432,10 +470,10 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
 
     // B fragments: column wn*64 + j*32 + l32, 8 channels at 8*hh
     const int col0 = wn * 32 * CB + l32;
-    struct BF {
-        us_h8 h[CB], l[CB];
+    struct BFr {
+        us_h8 h[CB], l[CB], m[CB];
     };
-    auto read_b = [&](int s, BF& f) __attribute__((always_inline)) {
+    auto read_b = [&](int s, BFr& f) __attribute__((always_inline)) {
         int row, ch;
         if (s < S1) {
             const int tap = s / CG;
@@ -454,6 +492,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
             } else {
                 f.h[j] = *reinterpret_cast<const us_h8*>(ph + off);
                 f.l[j] = *reinterpret_cast<const us_h8*>(pl + off);
+                if constexpr (BF) f.m[j] = *reinterpret_cast<const us_h8*>(pm + off);
             }
         }
     };
@@ -466,13 +505,38 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
         if (u >= CG) u -= CG;
         return S1 + u;
     };
-    auto step = [&](int t, int s, const BF& f, us_f32x16 (&acc)[MI][CB]) __attribute__((always_inline)) {
+    auto step = [&](int t, int s, const BFr& f, us_f32x16 (&acc)[MI][CB]) __attribute__((always_inline)) {
         us_h8 ah[MI], al[MI], a2[MI];
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
             ah[i] = ring[t % R][i][0];
             al[i] = ring[t % R][i][1];
             a2[i] = ah[i] * (_Float16)2048.0f;
+        }
+        if constexpr (BF) {
+            us_b8 wh[MI], wl[MI], wmd[MI];
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                wh[i] = __builtin_bit_cast(us_b8, ring[t % R][i][0]);
+                wl[i] = __builtin_bit_cast(us_b8, ring[t % R][i][1]);
+                wmd[i] = __builtin_bit_cast(us_b8, ring[t % R][i][2]);
+            }
+            load_a(t % R, s + R * KG);               // refill the slot (runs on into W2)
+            // smallest products first: lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < CB; ++j) {
+                    const us_b8 xh = __builtin_bit_cast(us_b8, f.h[j]), xl = __builtin_bit_cast(us_b8, f.l[j]),
+                                xm = __builtin_bit_cast(us_b8, f.m[j]);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[i], xh, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[i], xl, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wmd[i], xm, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wmd[i], xh, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[i], xm, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[i], xh, acc[i][j], 0, 0, 0);
+                }
+            return;
         }
         load_a(t % R, RB > 1 ? smap(t + R) : s + R * KG);   // refill the slot (runs on into W2)
         if constexpr (F32) {
@@ -510,7 +574,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
     auto kloop = [&](auto gtag, auto t0tag, auto t1tag) __attribute__((always_inline)) {
         constexpr int GG = decltype(gtag)::value;
         constexpr int T0 = decltype(t0tag)::value, T1 = decltype(t1tag)::value;
-        BF f[2];
+        BFr f[2];
         auto sidx = [&](int t) __attribute__((always_inline)) { return RB > 1 ? smap(t) : t * KG + GG; };
         read_b(sidx(T0), f[0]);
 #pragma unroll
@@ -585,6 +649,14 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
                                 (xslot + (unsigned)((col0 + 32 * j) * C + m)) * 4u, 0, 16);
                         if constexpr (F32) {
                             *reinterpret_cast<us_f32x4*>(pf + (col0 + 32 * j) * PH + m) = v;
+                            continue;
+                        }
+                        if constexpr (BF) {
+                            us_b4 hi, mid, lo;
+                            bf3_split(v, hi, mid, lo);
+                            *reinterpret_cast<us_b4*>(ph + (col0 + 32 * j) * PH + m) = hi;
+                            *reinterpret_cast<us_b4*>(pl + (col0 + 32 * j) * PH + m) = lo;
+                            *reinterpret_cast<us_b4*>(pm + (col0 + 32 * j) * PH + m) = mid;
                             continue;
                         }
 #pragma unroll
@@ -733,7 +805,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
     // guarded.  The flag is taken here; the workgroup vote follows the epilogue's
     // stores (KG == 1: the second pass rewrites them; a barrier there costs no
     // wave anything), or comes here (KG == 2: the partner waves leave below)
-    constexpr bool CHECK = !GUARD && !F32 && RAVE_SPLIT_GUARD != 0;
+    constexpr bool CHECK = !GUARD && AR == 0 && RAVE_SPLIT_GUARD != 0;
     bool bad = false;
     if constexpr (CHECK) {
         if (KG == 1 || kg == 0) {
@@ -811,32 +883,52 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
 template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, int RB>
 __global__ __launch_bounds__(64 * (C / (32 * MI * RB)) * WGN * KG) void unit_split_kernel(USArgs a) {
     if constexpr (RB > 1 || RAVE_SPLIT_GUARD == 0) {
-        (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, false, RB, true>(a);
+        (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, 0, RB, true>(a);
     } else {
-        if (!unit_split_body<C, WGN, MI, KG, CB, SNAKE, false, RB, false>(a))
-            (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, false, RB, true>(a);
+        if (!unit_split_body<C, WGN, MI, KG, CB, SNAKE, 0, RB, false>(a))
+            (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, 0, RB, true>(a);
     }
 }
 template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, int RB>
 __global__ __launch_bounds__(64 * (C / (32 * MI * RB)) * WGN * KG) void unit_ring_f32_kernel(USArgs a) {
-    (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, true, RB, false>(a);
+    (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, 1, RB, false>(a);
+}
+template <int C, int WGN, int MI, int KG, int CB, bool SNAKE>
+__global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_bf3_kernel(USArgs a) {
+    (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, 2, 1, false>(a);
 }
 
+// ar: 0 split16, 1 exact fp32 (ring), 2 bf16x3
 template <int C, int WGN, int MI, int KG, int CB, int RB = 1>
-static int us_launch(USArgs k, int B, bool snake, bool f32, hipStream_t st) {
+static int us_launch(USArgs k, int B, bool snake, int ar, hipStream_t st) {
     using G = USGeo<C, WGN, MI, KG, CB, RB>;
+    using G3 = USGeo<C, WGN, MI, KG, CB, RB, 3>;
+    const bool f32 = ar == 1;
     if (k.XW > G::XW_MAX) {
         set_error("residual_unit(split16): dilation too large");
         return RAVE_ERR_UNSUPPORTED;
     }
     k.ntiles = ceil_div(k.T, G::BN);
-    auto kern = f32 ? (snake ? unit_ring_f32_kernel<C, WGN, MI, KG, CB, true, RB> : unit_ring_f32_kernel<C, WGN, MI, KG, CB, false, RB>)
-                    : (snake ? unit_split_kernel<C, WGN, MI, KG, CB, true, RB> : unit_split_kernel<C, WGN, MI, KG, CB, false, RB>);
-    static bool attr[4] = {false, false, false, false};
-    if (G::LDS > 65536 && !attr[2 * f32 + snake]) {
+    void (*kern)(USArgs) = nullptr;
+    int lds = G::LDS;
+    if (ar == 2) {
+        // three operand planes: built where they fit the CU's LDS (one workgroup per slab)
+        if constexpr (RB == 1 && G3::LDS <= 160 * 1024) {
+            kern = snake ? unit_bf3_kernel<C, WGN, MI, KG, CB, true> : unit_bf3_kernel<C, WGN, MI, KG, CB, false>;
+            lds = G3::LDS;
+        } else {
+            set_error("residual_unit(bf16x3): this width does not fit the CU's LDS as three planes");
+            return RAVE_ERR_UNSUPPORTED;
+        }
+    } else {
+        kern = f32 ? (snake ? unit_ring_f32_kernel<C, WGN, MI, KG, CB, true, RB> : unit_ring_f32_kernel<C, WGN, MI, KG, CB, false, RB>)
+                   : (snake ? unit_split_kernel<C, WGN, MI, KG, CB, true, RB> : unit_split_kernel<C, WGN, MI, KG, CB, false, RB>);
+    }
+    static bool attr[6] = {false, false, false, false, false, false};
+    if (lds > 65536 && !attr[2 * ar + snake]) {
         RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr[2 * f32 + snake] = true;
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        attr[2 * ar + snake] = true;
     }
     int grid = k.ntiles * B;
     if constexpr (RB > 1) {
@@ -857,8 +949,8 @@ static int us_launch(USArgs k, int B, bool snake, bool f32, hipStream_t st) {
         k.ngroups = grid;
         grid = ceil_div(grid, 8) * 8 * RB;          // whole groups per XCD slot
     }
-    launch(kern, dim3(grid), dim3(G::NT), (uint32_t)G::LDS, st, k);
-    return launch_status(f32 ? "unit_ring_f32_kernel" : "unit_split_kernel");
+    launch(kern, dim3(grid), dim3(G::NT), (uint32_t)lds, st, k);
+    return launch_status(ar == 2 ? "unit_bf3_kernel" : f32 ? "unit_ring_f32_kernel" : "unit_split_kernel");
 }
 
 static bool us_supported(int C) { return C == 64 || C == 128 || C == 256 || C == 512; }
@@ -885,7 +977,24 @@ extern "C" int64_t rave_unit_split_packed_size(int C) {
     return (int64_t)(C / 32) * ST * 2 * 256 + 2 * C;
 }
 
-static int unit_pack(const float* w1, const float* w2, int C, float* packed, bool f32) {
+// host fp32 -> bf16, round to nearest even (finite weights)
+static uint16_t bf16_bits(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+static float bf16_value(uint16_t h) {
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+// mode: 0 split16 (hi, lo f16, row scales), 1 exact fp32, 2 bf16x3 (hi, lo, mid)
+static int unit_pack(const float* w1, const float* w2, int C, float* packed, int mode) {
+    const bool f32 = mode != 0;                      // (no row scales)
+    const int NPW = mode == 2 ? 3 : 2;
     RAVE_CHECK_ARG(w1 && w2 && packed, "unit_split_pack_weight: null pointer");
     if (!us_supported(C)) {
         set_error("unit_split_pack_weight: split16 fused residual unit supports C in {64, 128, 256, 512}");
@@ -901,8 +1010,10 @@ static int unit_pack(const float* w1, const float* w2, int C, float* packed, boo
         e2[m] = f32 ? 0 : us_row_exponent(a2);
     }
     _Float16* out = reinterpret_cast<_Float16*>(packed);
+    uint16_t* bout = reinterpret_cast<uint16_t*>(packed);
     for (int mb = 0; mb < C / 32; ++mb)
         for (int s = 0; s < ST; ++s) {
+            uint16_t* bp = bout + ((int64_t)(mb * ST + s) * 3) * 512;   // bf16x3: hi, lo, mid
             _Float16* hi = out + ((int64_t)(mb * ST + s) * 2) * 512;
             _Float16* lo = hi + 512;
             float* f32s = packed + ((int64_t)(mb * ST + s) * 2) * 256;   // fp32: floats 0-3 slot 0, 4-7 slot 1
@@ -918,6 +1029,15 @@ static int unit_pack(const float* w1, const float* w2, int C, float* packed, boo
                         const int ci = (s - S1) * 16 + kk;
                         v = std::ldexp(w2[(int64_t)m * C + ci], e2[m]);
                     }
+                    if (mode == 2) {
+                        const uint16_t h = bf16_bits(v);
+                        const float r = v - bf16_value(h);
+                        const uint16_t md = bf16_bits(r);
+                        bp[l * 8 + e] = h;
+                        bp[1024 + l * 8 + e] = md;
+                        bp[512 + l * 8 + e] = bf16_bits(r - bf16_value(md));
+                        continue;
+                    }
                     if (f32) {
                         f32s[(e >> 2) * 256 + l * 4 + (e & 3)] = v;
                         continue;
@@ -927,7 +1047,7 @@ static int unit_pack(const float* w1, const float* w2, int C, float* packed, boo
                     lo[l * 8 + e] = (_Float16)((v - (float)vh) * 2048.0f);
                 }
         }
-    float* rs = packed + (int64_t)(C / 32) * ST * 2 * 256;
+    float* rs = packed + (int64_t)(C / 32) * ST * NPW * 256;
     for (int m = 0; m < C; ++m) {
         rs[m] = f32 ? 1.0f : (float)std::ldexp(1.0, -(e1[m] + 11));
         rs[C + m] = f32 ? 1.0f : (float)std::ldexp(1.0, -(e2[m] + 11));
@@ -936,11 +1056,26 @@ static int unit_pack(const float* w1, const float* w2, int C, float* packed, boo
 }
 
 extern "C" int rave_unit_split_pack_weight(const float* w1, const float* w2, int C, float* packed) {
-    return unit_pack(w1, w2, C, packed, false);
+    return unit_pack(w1, w2, C, packed, 0);
 }
 
 extern "C" int rave_unit_ring_pack_weight(const float* w1, const float* w2, int C, float* packed) {
-    return unit_pack(w1, w2, C, packed, true);
+    return unit_pack(w1, w2, C, packed, 1);
+}
+
+// bf16x3: fragments [C/32][S1+S2][hi, lo, mid][64 lanes][8 bf16], then rs1, rs2 (= 1)
+extern "C" int64_t rave_unit_bf3_packed_size(int C) {
+    if (C != 64 && C != 128 && C != 256) return -1;
+    const int ST = 4 * C / 16;
+    return (int64_t)(C / 32) * ST * 3 * 256 + 2 * C;
+}
+
+extern "C" int rave_unit_bf3_pack_weight(const float* w1, const float* w2, int C, float* packed) {
+    if (C != 64 && C != 128 && C != 256) {
+        set_error("unit_bf3_pack_weight: the bf16x3 fused unit supports C in {64, 128, 256}");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    return unit_pack(w1, w2, C, packed, 2);
 }
 
 #ifdef RAVE_STAMPS
@@ -998,7 +1133,12 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
     }
     USArgs k{};
     k.x = a.x; k.y = a.y; k.w = a.weight;
-    const int64_t frag = (int64_t)(C / 32) * (4 * C / 16) * 2 * 256;
+    const int ar = a.precision == RAVE_PREC_BF16X3 ? 2 : a.precision == RAVE_PREC_F32_RING ? 1 : 0;
+    if (ar == 2 && C == 512) {
+        set_error("residual_unit(bf16x3): C = 512 does not fit the CU's LDS as three planes");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    const int64_t frag = (int64_t)(C / 32) * (4 * C / 16) * (ar == 2 ? 3 : 2) * 256;
     k.rs1 = a.weight + frag; k.rs2 = a.weight + frag + C;
     k.b1 = a.bias1; k.b2 = a.bias2; k.a0 = a.alpha0; k.a2 = a.alpha2;
     k.x_sb = a.x_sb; k.x_sc = a.x_sc; k.y_sb = a.y_sb; k.y_sc = a.y_sc;
@@ -1025,13 +1165,13 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
         const int off = (4 - a.pad_left % 4) % 4;      // window start past its 4-aligned block start
         const int nb = (off + k.XW + 3) / 4;
         k.nb_magic = (unsigned)(((1u << 24) + nb - 1) / nb);
-        return us_launch<CC, WGN, MI, KG, CB, RB>(k, a.batch, snake, a.precision == RAVE_PREC_F32_RING, st);
+        return us_launch<CC, WGN, MI, KG, CB, RB>(k, a.batch, snake, ar, st);
     };
     k.xv = (k.XL % 4 == 0 && a.x_sc % 4 == 0 && a.x_sb % 4 == 0 &&
             reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && std::getenv("RAVE_UNIT_XV") == nullptr) ? 1 : 0;
     // cooperative form when the caller passed its workspace
     const CoopLayout L = coop_layout(a);
-    if (L.rb > 1 && a.workspace) {
+    if (L.rb > 1 && a.workspace && ar != 2) {
         k.flag_stride = L.stride;
         k.flags = reinterpret_cast<unsigned*>(a.workspace);
         k.tmo = k.flags + RAVE_SPLITK_STATUS_WORD;

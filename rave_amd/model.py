@@ -46,7 +46,9 @@ class RAVE:
     ``precision``: "f32" (exact fp32 MFMA), "split16" (split-f16 GEMMs), or
     "auto" (per op the faster of the two, with every launch configuration,
     fused unit and residual stack timed at plan build), or "f32_tuned" (exact
-    fp32 on every op, launch configurations and fused units timed as in auto).  ``tuning`` replays the
+    fp32 on every op, launch configurations and fused units timed as in auto), or
+    "f32_bf3" (as f32_tuned, with the fused units also timed in bf16x3: fp32 on
+    the bf16 matrix cores with an exact three-way operand split).  ``tuning`` replays the
     choices of an earlier model's ``tuning()`` without timing runs."""
 
     def __init__(self, cfg: RaveConfig, params: Mapping[str, np.ndarray], speaker: np.ndarray,
@@ -54,8 +56,10 @@ class RAVE:
                  adain_stats: Optional[Mapping] = None, fuse_units: bool = True,
                  precision: str = "f32", tuning: Optional[list] = None):
         check_params(cfg, params)
-        if precision not in list(N.PRECISION) + ["auto", "f32_tuned"]:
-            raise ValueError(f"precision must be one of {sorted(N.PRECISION) + ['auto', 'f32_tuned']}")
+        modes = {"auto": N.PREC_AUTO, "f32_tuned": N.PREC_F32_TUNED, "f32_bf3": N.PREC_F32_BF3,
+                 "f32": N.PREC_F32, "split16": N.PREC_SPLIT16}
+        if precision not in modes:
+            raise ValueError(f"precision must be one of {sorted(modes)}")
         self.precision = precision
         self.cfg = cfg
         self.graph = build_graph(cfg)          # reference names (AdaIN modules, tests)
@@ -78,8 +82,7 @@ class RAVE:
             keep.append(a)
             plist.append(N.Param(name.encode(), a.ctypes.data, a.size))
         parr = (N.Param * len(plist))(*plist)
-        prec = {"auto": N.PREC_AUTO, "f32_tuned": N.PREC_F32_TUNED}.get(precision) \
-            if precision in ("auto", "f32_tuned") else N.PRECISION[precision]
+        prec = modes[precision]
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             N.check(N.lib.rave_model_create(C.byref(ccfg), parr, len(plist), spk.ctypes.data, prec, C.byref(h)),

@@ -379,7 +379,7 @@ def _model(cfg, g, dev, golden, precision="f32"):
 
 PRECISIONS = ["f32", "split16", "auto"]
 # model-level modes: + exact fp32 with autotuned launch choices (bench.py's headline mode)
-MODEL_PRECISIONS = PRECISIONS + ["f32_tuned"]
+MODEL_PRECISIONS = PRECISIONS + ["f32_tuned", "f32_bf3"]
 
 
 @pytest.mark.parametrize("precision", MODEL_PRECISIONS)
@@ -863,7 +863,7 @@ UNIT_CASES = [
 ]
 
 
-@pytest.mark.parametrize("precision", PRECISIONS + ["f32_ring"])
+@pytest.mark.parametrize("precision", PRECISIONS + ["f32_ring", "bf16x3"])
 @pytest.mark.parametrize("case", UNIT_CASES, ids=[str(c) for c in UNIT_CASES])
 def test_residual_unit_kernel(N, dev, case, precision):
     """rave_residual_unit == x + conv1x1(act(conv3_d(act(x)) + b1)) + b2 (oracle, float64)."""
@@ -900,6 +900,55 @@ def test_residual_unit_kernel(N, dev, case, precision):
     got = y.cpu().numpy()
     assert np.isfinite(got).all()
     assert maxabs(got, ref) <= 2e-5 * max(1.0, float(np.abs(ref).max()))
+
+
+BF3_CASES = [(64, 9, "snake", False, 4, 1000), (128, 3, "leaky", True, 3, 517), (256, 1, "leaky", False, 16, 256)]
+
+
+@pytest.mark.parametrize("case", BF3_CASES, ids=[str(c) for c in BF3_CASES])
+def test_residual_unit_bf16x3_is_fp32_class(N, dev, case):
+    """bf16x3 (exact 3-way bf16 operand split, six products, fp32 accumulation)
+    against the exact-fp32 ring kernel on the same inputs: its error against the
+    float64 oracle is that of fp32 (within 1.5x + 1e-7 of the ring kernel's) and
+    the two differ by a few fp32 ulps of the output scale, not by f16/bf16
+    rounding (~1e-3)."""
+    from oracle.rave_oracle import conv1d, leaky_relu, snake
+    C, d, act, causal, B, T = case
+    rng = np.random.default_rng(7 * C + d)
+    x = (4.0 * rng.standard_normal((B, C, T))).astype(np.float32)   # operands well past 1
+    w1 = (rng.standard_normal((C, C, 3)) / np.sqrt(3 * C)).astype(np.float32)
+    w2 = (rng.standard_normal((C, C, 1)) / np.sqrt(C)).astype(np.float32)
+    b1 = rng.standard_normal(C).astype(np.float32) * 0.1
+    b2 = rng.standard_normal(C).astype(np.float32) * 0.1
+    a0 = (1 + 0.3 * rng.standard_normal(C)).astype(np.float32)
+    a2 = (1 + 0.3 * rng.standard_normal(C)).astype(np.float32)
+    pad = (2 * d, 0) if causal else (d, d)
+    f = (lambda v, al: snake(v, al.reshape(-1, 1))) if act == "snake" else (lambda v, al: leaky_relu(v, 0.2))
+    h = f(conv1d(f(x.astype(np.float64), a0), w1, b1, 1, d, pad), a2)
+    ref = x + conv1d(h, w2, b2, 1, 1, (0, 0))
+    xd = torch.from_numpy(x).to(dev)
+    dd = {k: torch.from_numpy(v).to(dev) for k, v in dict(b1=b1, b2=b2, a0=a0, a2=a2).items()}
+    outs = {}
+    for name in ("f32_ring", "bf16x3"):
+        prec = N.PRECISION[name]
+        packed = torch.from_numpy(N.pack_unit_weight(w1, w2, C, precision=prec)).to(dev)
+        y = torch.full_like(xd, float("nan"))
+        a = N.UnitArgs(channels=C, batch=B, t_len=T, dilation=d, pad_left=pad[0], act=N.ACT[act],
+                       leaky_slope=0.2, precision=prec, x=xd.data_ptr(), x_sb=C * T, x_sc=T, y=y.data_ptr(),
+                       y_sb=C * T, y_sc=T, weight=packed.data_ptr(), bias1=dd["b1"].data_ptr(),
+                       bias2=dd["b2"].data_ptr(), alpha0=dd["a0"].data_ptr() if act == "snake" else None,
+                       alpha2=dd["a2"].data_ptr() if act == "snake" else None)
+        N.check(N.lib.rave_residual_unit(C_.byref(a), C_.c_void_p(torch.cuda.current_stream().cuda_stream)))
+        torch.cuda.synchronize()
+        outs[name] = y.cpu().numpy()
+    scale = float(np.abs(ref).max())
+    e_ring = maxabs(outs["f32_ring"], ref) / scale
+    e_bf3 = maxabs(outs["bf16x3"], ref) / scale
+    d_rb = maxabs(outs["bf16x3"], outs["f32_ring"]) / scale
+    print(f"\n[bf16x3] C={C}: rel err vs float64 ring {e_ring:.2e} bf16x3 {e_bf3:.2e}; bf16x3 vs ring {d_rb:.2e}")
+    assert np.isfinite(outs["bf16x3"]).all()
+    assert e_bf3 <= 1.5 * e_ring + 1e-7
+    assert d_rb <= 1e-6
 
 
 COOP_CASES = [
@@ -977,7 +1026,7 @@ CACHED_UNIT_CASES = [
 ]
 
 
-@pytest.mark.parametrize("precision", ["f32", "split16", "f32_ring"])
+@pytest.mark.parametrize("precision", ["f32", "split16", "f32_ring", "bf16x3"])
 @pytest.mark.parametrize("case", CACHED_UNIT_CASES, ids=[str(c) for c in CACHED_UNIT_CASES])
 def test_residual_unit_cached_form(N, dev, case, precision):
     """The cached (streaming) fused unit: x holds need = 2d history columns then

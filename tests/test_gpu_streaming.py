@@ -14,7 +14,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-4
-PRECISIONS = ["f32", "split16", "auto", "f32_tuned"]   # f32_tuned: exact fp32 incl. the ring kernels
+PRECISIONS = ["f32", "split16", "auto", "f32_tuned", "f32_bf3"]   # f32_tuned: exact fp32 incl. the ring kernels
 
 
 def maxabs(a, b):

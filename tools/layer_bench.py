@@ -176,7 +176,7 @@ def main():
     ap.add_argument("--layers", default=",".join(list(LAYERS) + list(UNITS)))
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--batch", type=int, default=16)
-    ap.add_argument("--precision", default="split16", choices=["f32", "split16", "f32_ring"])
+    ap.add_argument("--precision", default="split16", choices=["f32", "split16", "f32_ring", "bf16x3"])
     ap.add_argument("--config", default="0", help="launch config value, or 'all' (every listed one)")
     a = ap.parse_args()
     global PREC

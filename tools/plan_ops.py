@@ -3,6 +3,8 @@
 sorted by time: where a config's step goes.
 
     python tools/plan_ops.py --config discrete --plan encode_codes --batch 8 --samples 65536
+    python tools/plan_ops.py --config v2 --plan decode --batch 16 --precision f32_tuned \
+        --tuning-in profiles/tuning/v2_16x65536_f32_tuned.json
 """
 import argparse
 import json
@@ -27,10 +29,15 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--samples", type=int, default=65536)
     ap.add_argument("--runs", type=int, default=20)
+    ap.add_argument("--tuning-in", help="JSON of RAVE.tuning() (e.g. profiles/tuning/*.json): the pinned launch choices")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     cfg = rcfg.get_config(a.config)
-    m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=a.precision)
+    tuning = None
+    if a.tuning_in:
+        with open(a.tuning_in) as fh:
+            tuning = json.load(fh)
+    m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=a.precision, tuning=tuning)
     B, T = a.batch, a.samples
     x = (0.2 * torch.randn(B, 1, T, generator=torch.Generator().manual_seed(0))).to(dev)
     which = PLANS[a.plan]
