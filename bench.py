@@ -9,15 +9,20 @@ rank's 16 clips -> RCCL all-gather of the latents over all ranks -> RAVE.decode
 of the rank's own latent shard.  Per-GPU work is fixed
 as N grows ("scaling": "weak").
 
-The headline ``value`` runs ``--precision f32_tuned`` (since round 4): exact
-fp32 MFMA (v_mfma_f32_32x32x2_f32) on every conv / unit GEMM, the reference's
-arithmetic, with the committed launch choices (profiles/tuning/).  The same
-invocation then times ``--precision auto`` on the same input
-(``split16_auto``): per op the faster of exact fp32 and split-f16 GEMMs (fp32
-operands carried as f16 hi/lo pairs, ~22-bit, three f16 MFMA passes, fp32
-accumulation), with the max-abs difference of the two outputs.  (Before round
-4 the line's ``value`` was the auto mode and ``f32_exact`` rode beside it;
-``--precision auto`` still gives that layout.)  ``cpu_baseline`` is the
+The headline ``value`` runs ``--precision f32_bf3`` (since round 4, late): fp32
+arithmetic on every conv / unit GEMM with the committed launch choices
+(profiles/tuning/) -- per op the faster of exact fp32 MFMA
+(v_mfma_f32_32x32x2_f32) and, for the fused residual units, fp32 on the bf16
+matrix cores with every operand split exactly into three bf16 parts (24
+significand bits, the fp32 exponent range) and six of the nine cross products
+(the three dropped are each below 2^-25 of the product), fp32 accumulation.
+Its error against a float64 reference is at or below the exact-fp32 kernels'
+(tests/test_gpu_parity.py::test_residual_unit_bf16x3_is_fp32_class).  The
+same invocation then times, on the same input, ``f32_exact`` (``--precision
+f32_tuned``: exact fp32 MFMA on every op) and ``split16_auto`` (per op the
+faster of exact fp32 and split-f16 GEMMs on ~22-bit f16 hi/lo operands), each
+with the max-abs difference of its output from the headline's.
+``--precision f32_tuned`` / ``auto`` give the earlier layouts.  ``cpu_baseline`` is the
 reference's module graph on torch fp32 CPU (oracle/torch_cpu.py) over the same
 step.
 
@@ -61,6 +66,8 @@ FAMILIES = {
                      PEAK_SPLIT16_TFLOPS),
     "unit_f32": ("unit_ring_f32_kernel / residual_unit_kernel, exact fp32 MFMA 32x32x2", PEAK_FP32_TFLOPS),
     "unit_split16": ("unit_split_kernel, split-f16 MFMA 32x32x16 (3 per fp32 MAC)", PEAK_SPLIT16_TFLOPS),
+    "conv_bf16x3": ("conv1d_bf3_kernel (+ split-K reduce), fp32 as exact bf16x3 operands, bf16 MFMA 32x32x16 "
+                    "(6 per fp32 MAC)", PEAK_BF3_TFLOPS),
     "unit_bf16x3": ("unit_bf3_kernel, fp32 as exact bf16x3 operands, bf16 MFMA 32x32x16 (6 per fp32 MAC)",
                     PEAK_BF3_TFLOPS),
     "stack_split16": ("stack_split_kernel (3 residual units per launch), split-f16 MFMA 32x32x16",
@@ -85,8 +92,8 @@ FAMILIES = {
 def op_family(kind: int, precision: int) -> str:
     from rave_amd import _native as N
     prec = "split16" if precision == N.PREC_SPLIT16 else "f32"
-    if kind == N.OP_UNIT and precision == N.PREC_BF16X3:
-        return "unit_bf16x3"
+    if kind in (N.OP_UNIT, N.OP_CONV) and precision == N.PREC_BF16X3:
+        return ("unit_" if kind == N.OP_UNIT else "conv_") + "bf16x3"
     if kind == N.OP_CONV:
         return "conv_" + prec
     if kind == N.OP_UNIT:
@@ -106,7 +113,8 @@ def op_family(kind: int, precision: int) -> str:
 
 # committed PMC traffic per arithmetic mode (tools/profile_round.sh -> tools/rocprof_summary.py)
 TRAFFIC_FILES = {"auto": os.path.join(REPO, "profiles", "traffic.json"),
-                 "f32_tuned": os.path.join(REPO, "profiles", "traffic_f32_tuned.json")}
+                 "f32_tuned": os.path.join(REPO, "profiles", "traffic_f32_tuned.json"),
+                 "f32_bf3": os.path.join(REPO, "profiles", "traffic_f32_bf3.json")}
 
 
 def traffic_per_launch(config: str, B: int, T: int, precision: str):
@@ -456,13 +464,14 @@ def main():
     ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
     ap.add_argument("--samples", type=int, default=65536, help="samples per clip")
     ap.add_argument("--config", default="v2")
-    ap.add_argument("--precision", default="f32_tuned", choices=["f32", "f32_tuned", "f32_bf3", "split16", "auto"],
+    ap.add_argument("--precision", default="f32_bf3", choices=["f32", "f32_tuned", "f32_bf3", "split16", "auto"],
                     help="conv/unit GEMM arithmetic of the headline (include/rave_amd.h RAVE_PREC_*). "
-                         "Default f32_tuned: exact fp32 MFMA on every op (the reference's arithmetic), "
-                         "launch choices pinned; auto = per op the faster of exact fp32 and split-f16")
+                         "Default f32_bf3: fp32 on every op (exact fp32 MFMA, or for fused units bf16x3 with "
+                         "an exact operand split), launch choices pinned; f32_tuned = exact fp32 MFMA on "
+                         "every op; auto = per op the faster of exact fp32 and split-f16")
     ap.add_argument("--no-f32", "--no-secondary", dest="no_f32", action="store_true",
-                    help="skip the second arithmetic mode that rides along the headline (auto beside an "
-                         "fp32 headline, exact fp32 beside any other)")
+                    help="skip the arithmetic modes that ride along the headline (exact fp32 and auto "
+                         "beside f32_bf3; auto beside f32_tuned; exact fp32 beside auto)")
     ap.add_argument("--tuning-in", help="JSON of RAVE.tuning() to reuse (no timing runs at plan build)")
     ap.add_argument("--tuning-out", help="write RAVE.tuning() here after the plans are built")
     ap.add_argument("--retune", action="store_true",
@@ -520,19 +529,19 @@ def main():
     head, y_head = run_mode(a, cfg, params, spk, a.precision, x, dev, world, rank, rank == 0)
     exact = None
     fast = None
-    if a.precision in ("f32", "f32_tuned") and not a.no_f32:
-        # beside the exact-fp32 headline: the fastest mixed mode (per op exact fp32 or
-        # split-f16, ~22-bit operands), its error against the headline on the same input
-        fast, y_fast = run_mode(a, cfg, params, spk, "auto", x, dev, world, rank, rank == 0)
-        fast["vs_headline_max_abs"] = float((y_head - y_fast).abs().max())
-        fast["precision"] = "auto"
-        del y_fast
-    elif a.precision not in ("f32", "f32_tuned") and not a.no_f32:
-        # exact fp32 on every op, with the same launch-configuration autotuning as the headline
+    if a.precision not in ("f32", "f32_tuned") and not a.no_f32:
+        # exact fp32 MFMA on every op, with the same launch-configuration autotuning as the headline
         exact, y_f32 = run_mode(a, cfg, params, spk, "f32_tuned", x, dev, world, rank, rank == 0)
         # the same input through both arithmetic modes (north star: <= 1e-4 max-abs)
         exact["headline_vs_f32_max_abs"] = float((y_head - y_f32).abs().max())
         del y_f32
+    if a.precision not in ("auto", "split16") and not a.no_f32:
+        # the fastest mixed mode (per op exact fp32 or split-f16, ~22-bit operands),
+        # its error against the headline on the same input
+        fast, y_fast = run_mode(a, cfg, params, spk, "auto", x, dev, world, rank, rank == 0)
+        fast["vs_headline_max_abs"] = float((y_head - y_fast).abs().max())
+        fast["precision"] = "auto"
+        del y_fast
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

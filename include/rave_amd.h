@@ -86,13 +86,16 @@ enum { RAVE_PREC_F32 = 0, RAVE_PREC_SPLIT16 = 1 };
  *                      packed with rave_conv1d_ring_pack_weight (sizes as the split
  *                      image).  Value 4: 2 and 3 are model-level modes below. */
 #define RAVE_PREC_F32_RING 4
-/*   RAVE_PREC_BF16X3   fp32 on the bf16 matrix cores (fused units, C in {64, 128, 256}):
+/*   RAVE_PREC_BF16X3   fp32 on the bf16 matrix cores (fused units, C in {64, 128, 256}, and
+ *                      512 at dilations <= 4; rave_conv1d on the split kernels' machinery,
+ *                      16-byte aligned input rows):
  *                      every operand split exactly into three bf16 parts
  *                      (v = hi + mid + lo, 24 significand bits, the fp32 exponent
  *                      range: no row scales, no range guard); six
  *                      v_mfma_f32_32x32x16_bf16 products per K-step (all cross
  *                      products but mid*lo, lo*mid, lo*lo: each < 2^-25 |a b|) into one
- *                      fp32 accumulator.  Weights packed with rave_unit_bf3_pack_weight. */
+ *                      fp32 accumulator.  Weights packed with rave_unit_bf3_pack_weight /
+ *                      rave_conv1d_bf3_pack_weight. */
 #define RAVE_PREC_BF16X3 5
 
 const char* rave_last_error(void);
@@ -178,6 +181,11 @@ int rave_conv1d_split_pack_weight(const float* w, int c_in, int c_out, int kerne
  * per lane and K-step (4 in each 1 KB slot) and row scales 1 */
 int rave_conv1d_ring_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
                                  int dilation, int transposed, int out_shift, float* packed);
+/* RAVE_PREC_BF16X3 weight image: the split image's layout with three bf16 fragments
+ * (hi, lo, mid) per 32-row block and K-step, row scales 1. */
+int64_t rave_conv1d_bf3_packed_size(int c_in, int c_out, int kernel, int stride, int dilation, int transposed);
+int rave_conv1d_bf3_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride, int dilation,
+                                int transposed, int out_shift, float* packed);
 int rave_conv1d(const rave_conv1d_args* a, void* stream);
 
 /* ---------------------------------------------------------------- PQMF
@@ -355,7 +363,7 @@ int rave_unit_split_pack_weight(const float* w1, const float* w2, int channels, 
  * the split image's layout with 8 fp32 values per lane and K-step, row scales 1
  * (sizes as rave_unit_split_packed_size). */
 int rave_unit_ring_pack_weight(const float* w1, const float* w2, int channels, float* packed);
-/* RAVE_PREC_BF16X3 unit weights (C in {64, 128, 256}; else -1 / RAVE_ERR_UNSUPPORTED):
+/* RAVE_PREC_BF16X3 unit weights (C in {64, 128, 256, 512}; else -1 / RAVE_ERR_UNSUPPORTED):
  * (hi, lo, mid) bf16 A-fragments per 32-row block and K-step, then the two
  * row-scale vectors (all 1). */
 int64_t rave_unit_bf3_packed_size(int channels);

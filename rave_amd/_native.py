@@ -240,7 +240,7 @@ EXPORTS = [
     "rave_last_error", "rave_abi_version", "rave_struct_sizes",
     "rave_conv1d_chunk", "rave_conv1d_packed_size", "rave_conv1d_pack_weight", "rave_conv1d",
     "rave_conv1d_workspace", "rave_conv1d_configs", "rave_conv1d_split_packed_size", "rave_conv1d_split_pack_weight",
-    "rave_conv1d_ring_pack_weight",
+    "rave_conv1d_ring_pack_weight", "rave_conv1d_bf3_packed_size", "rave_conv1d_bf3_pack_weight",
     "rave_pqmf_analysis", "rave_pqmf_synthesis", "rave_fill_channels", "rave_copy",
     "rave_rvq_workspace", "rave_rvq_encode", "rave_rvq_decode", "rave_shift_history", "rave_noise_synth", "rave_adain",
     "rave_unit_packed_size", "rave_unit_pack_weight", "rave_residual_unit",
@@ -289,6 +289,9 @@ def _load():
     lib.rave_conv1d_split_packed_size.restype = i64
     lib.rave_conv1d_split_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
     lib.rave_conv1d_ring_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
+    lib.rave_conv1d_bf3_packed_size.argtypes = [C.c_int] * 6
+    lib.rave_conv1d_bf3_packed_size.restype = i64
+    lib.rave_conv1d_bf3_pack_weight.argtypes = [vp] + [C.c_int] * 7 + [vp]
     lib.rave_encoder_head_pack_filter.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp]
     lib.rave_encoder_head_pack_filter_f32.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp]
     lib.rave_decoder_tail_pack_filter_f32.argtypes = [vp, C.c_int, C.c_int, vp]
@@ -450,6 +453,8 @@ def pack_conv_weight(w, c_in, c_out, kernel, stride, dilation, transposed, out_s
                         if precision == PREC_F32 else
                         (lib.rave_conv1d_split_packed_size, lib.rave_conv1d_ring_pack_weight)
                         if precision == PREC_F32_RING else
+                        (lib.rave_conv1d_bf3_packed_size, lib.rave_conv1d_bf3_pack_weight)
+                        if precision == PREC_BF16X3 else
                         (lib.rave_conv1d_split_packed_size, lib.rave_conv1d_split_pack_weight))
     n = int(size_fn(c_in, c_out, kernel, stride, dilation, int(transposed)))
     if n <= 0:

@@ -552,7 +552,7 @@ constexpr int kGemvSplits[] = {1, 2, 4, 8, 16, 32};
 
 extern "C" int rave_conv1d_configs(const rave_conv1d_args* p, int32_t* cfgs, int max_cfgs) {
     RAVE_CHECK_ARG(p && max_cfgs >= 0, "conv1d_configs: null args");
-    if (p->precision == RAVE_PREC_SPLIT16 || p->precision == RAVE_PREC_F32_RING)
+    if (p->precision == RAVE_PREC_SPLIT16 || p->precision == RAVE_PREC_F32_RING || p->precision == RAVE_PREC_BF16X3)
         return conv1d_split_configs(*p, cfgs, max_cfgs);
     RAVE_CHECK_ARG(p->precision == RAVE_PREC_F32, "conv1d_configs: unknown precision");
     ConvKArgs k;
@@ -594,7 +594,7 @@ extern "C" int rave_conv1d_configs(const rave_conv1d_args* p, int32_t* cfgs, int
 
 extern "C" int64_t rave_conv1d_workspace(const rave_conv1d_args* p) {
     if (!p) return -1;
-    if (p->precision == RAVE_PREC_SPLIT16 || p->precision == RAVE_PREC_F32_RING) return conv1d_split_workspace(*p);
+    if (p->precision == RAVE_PREC_SPLIT16 || p->precision == RAVE_PREC_F32_RING || p->precision == RAVE_PREC_BF16X3) return conv1d_split_workspace(*p);
     if (p->precision != RAVE_PREC_F32) return -1;
     ConvKArgs k;
     int taps;
@@ -607,7 +607,7 @@ extern "C" int64_t rave_conv1d_workspace(const rave_conv1d_args* p) {
 
 extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
     RAVE_CHECK_ARG(p, "conv1d: null args");
-    if (p->precision == RAVE_PREC_SPLIT16 || p->precision == RAVE_PREC_F32_RING) return conv1d_split(*p, stream);
+    if (p->precision == RAVE_PREC_SPLIT16 || p->precision == RAVE_PREC_F32_RING || p->precision == RAVE_PREC_BF16X3) return conv1d_split(*p, stream);
     RAVE_CHECK_ARG(p->precision == RAVE_PREC_F32, "conv1d: unknown precision");
     ConvKArgs k;
     int taps;

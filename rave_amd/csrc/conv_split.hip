@@ -43,6 +43,14 @@ namespace rave {
 typedef _Float16 s_h8 __attribute__((ext_vector_type(8)));
 typedef float s_f32x8 __attribute__((ext_vector_type(8)));
 typedef float s_f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 s_b8 __attribute__((ext_vector_type(8)));
+// fp32 x 8 -> three bf16 parts with v == hi + mid + lo exactly (each remainder exact in fp32)
+__device__ __forceinline__ void s_bf3_split(const s_f32x8& v, s_b8& hi, s_b8& mid, s_b8& lo) {
+    hi = __builtin_convertvector(v, s_b8);
+    const s_f32x8 r = v - __builtin_convertvector(hi, s_f32x8);
+    mid = __builtin_convertvector(r, s_b8);
+    lo = __builtin_convertvector(r - __builtin_convertvector(mid, s_f32x8), s_b8);
+}
 
 // (taps after polyphase Q, phases S, virtual channels per chunk VC, max row shift)
 template <int KT> struct SFam;
@@ -115,6 +123,10 @@ __device__ __forceinline__ void wait_vm_regs(u32x4_t& a0, u32x4_t& a1) {
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a0), "+v"(a1) : "n"(N) : "memory");
 }
 template <int N>
+__device__ __forceinline__ void wait_vm_regs3(u32x4_t& a0, u32x4_t& a1, u32x4_t& a2) {
+    asm volatile("s_waitcnt vmcnt(%3)" : "+v"(a0), "+v"(a1), "+v"(a2) : "n"(N) : "memory");
+}
+template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
@@ -140,7 +152,10 @@ __device__ __forceinline__ u32x4_t raw_rsrc(const void* p, int bytes) {
 // family's VC virtual channels -- more K-steps per barrier and per window DMA
 // round, and enough of them for four K-groups on the short-N layers (C >= 512
 // at 64-128 frames), which would otherwise need split-K slabs in HBM.
-template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 4096 / WM, int VCX = 1, int NS_ = 3>
+// NP: operand planes per staged buffer and weight fragments per K-step (2: the
+// split16 (hi, lo) pair or one fp32 plane in its bytes; 3: bf16x3 hi, lo, mid)
+template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 4096 / WM, int VCX = 1, int NS_ = 3,
+          int NP = 2>
 struct SGeo {
     using F = SFam<KT>;
     static constexpr int Q = F::Q, S = F::S, VC0 = F::VC, VC = VC0 * VCX;
@@ -156,7 +171,7 @@ struct SGeo {
     static constexpr int XW_MAX = BN + (Q - 1) * F::DMAX + (KT == 2 ? 1 : 0);
     static constexpr int PH = VC + 8;                        // halves per plane row (conflict-free b128)
     static constexpr int XPLANE = XW_MAX * PH * 2;           // bytes per f16 plane
-    static constexpr int WR = KS0 * NJ * 2;                  // weight fragment loads per wave per chunk (max)
+    static constexpr int WR = KS0 * NJ * NP;                 // weight fragment loads per wave per chunk (max)
     // raw window rows: XV = 16-byte pieces from a 4-sample-aligned start (row
     // stride rounded up to 4 samples), else 4-byte pieces
     static constexpr int RS_MAX = XV ? ((XW_MAX * S + 3 + 3) / 4) * 4 : XW_MAX * S;
@@ -174,14 +189,14 @@ struct SGeo {
     // of K-steps to land (NS = 2 trades that for room for wider chunks)
     static constexpr int NS = NS_;
     // hand-counted vmcnt waits (kernel body): prologue, end of chunk, weights
-    static constexpr int WAIT_PRO = (NS - 1) * XI + 2 * KS0 * NJ;
-    static constexpr int WAIT_END = (NS - 1) * 2 * KS0 * NJ + (NS - 2) * XI;
+    static constexpr int WAIT_PRO = (NS - 1) * XI + NP * KS0 * NJ;
+    static constexpr int WAIT_END = (NS - 1) * NP * KS0 * NJ + (NS - 2) * XI;
     static constexpr int WAIT_MAX = WAIT_PRO > WAIT_END ? WAIT_PRO : WAIT_END;
     static constexpr int ALPHA = 4096;                       // Snake alphas (<= 1024 channels)
     static constexpr int EROW = WN + 4;                      // epilogue transpose row stride (floats)
     static constexpr int EPI = NW * WM * EROW * 4;           // epilogue transpose area (reuses the ring)
-    // ring + two (hi, lo) plane pairs + Snake alphas + the surplus DMAs' dump piece
-    static constexpr int MAIN = NS * STAGE + 2 * 2 * XPLANE + ALPHA + PB;
+    // ring + two plane buffers (NP planes each) + Snake alphas + the surplus DMAs' dump piece
+    static constexpr int MAIN = NS * STAGE + 2 * NP * XPLANE + ALPHA + PB;
     static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
     // + the split-K "last arriver" word, the range guard's per-wave overflow votes
     // (two plane buffers + the tile vote, x 16 waves, bytes) and wave maxima (16 floats)
@@ -202,14 +217,20 @@ template <int V> struct IC {
     static constexpr int value = V;
 };
 
-// F32: the same machinery with exact fp32 operands (RAVE_PREC_F32_RING): one
-// fp32 plane per staged buffer (row pitch PH floats, the bytes of the hi / lo
-// pair), weight fragments of 8 floats per lane in the split image's slots, and
-// eight v_mfma_f32_32x32x2_f32 per 16-deep K-step (K-slot (s, half h) =
-// channel 8h + s of the step's 16); no range guard, row scales 1.
-template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX, int NS, bool F32>
+// AR: 0 split16; 1 F32: the same machinery with exact fp32 operands
+// (RAVE_PREC_F32_RING): one fp32 plane per staged buffer (row pitch PH floats,
+// the bytes of the hi / lo pair), weight fragments of 8 floats per lane in the
+// split image's slots, and eight v_mfma_f32_32x32x2_f32 per 16-deep K-step
+// (K-slot (s, half h) = channel 8h + s of the step's 16); no range guard, row
+// scales 1.  2 BF (RAVE_PREC_BF16X3): every operand split exactly into bf16
+// (hi, lo, mid) -- three planes per staged buffer, three weight fragments per
+// K-step, six v_mfma_f32_32x32x16_bf16 (every cross product but mid*lo, lo*mid,
+// lo*lo: each < 2^-25 |a b|), smallest first; no range guard, row scales 1.
+template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX, int NS, int AR>
 __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
-    using G = SGeo<KT, BM, BN, WM, XV, KG, WN_, VCX, NS>;
+    constexpr bool F32 = AR == 1, BF = AR == 2;
+    constexpr int NP = BF ? 3 : 2;
+    using G = SGeo<KT, BM, BN, WM, XV, KG, WN_, VCX, NS, NP>;
     constexpr int S = G::S, CPC = G::CPC, PH = G::PH;
     constexpr int NT = G::NT, NW = G::NW, NWT = G::NWT, WGM = G::WGM, G8 = G::G8, XT = G::XT;
     constexpr int NI = G::NI, NJ = G::NJ, WN = G::WN;
@@ -270,11 +291,11 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
     const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
     const u32x4_t wrs = raw_rsrc(a.w, a.w_bytes);
     // packed weights: [packed chunk][32-row block][KSC0 K-steps][hi|lo][64 lanes][8 halves]
-    const unsigned wcstride = (unsigned)(a.MB * KSC0 * 2) * 1024u;
-    const unsigned wbase = (unsigned)((mw / 32) * KSC0 * 2) * 1024u + (unsigned)lane * 16u;
+    const unsigned wcstride = (unsigned)(a.MB * KSC0 * NP) * 1024u;
+    const unsigned wbase = (unsigned)((mw / 32) * KSC0 * NP) * 1024u + (unsigned)lane * 16u;
     const uint32_t lds0 = lds_addr(smem);
     char* planes = smem + G::NS * G::STAGE;
-    float* alpha_s = reinterpret_cast<float*>(smem + G::NS * G::STAGE + 4 * G::XPLANE);
+    float* alpha_s = reinterpret_cast<float*>(smem + G::NS * G::STAGE + 2 * NP * G::XPLANE);
     if constexpr (SNAKE) {
         for (int i = tid; i < a.c_in; i += NT) alpha_s[i] = a.alpha[i];
     }
@@ -308,7 +329,7 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
     }
 
     // window of chunk c -> ring slot (per-lane offsets, out-of-range -> zeros)
-    const uint32_t dump = lds0 + G::NS * G::STAGE + 4 * G::XPLANE + G::ALPHA;
+    const uint32_t dump = lds0 + G::NS * G::STAGE + 2 * NP * G::XPLANE + G::ALPHA;
     auto issue = [&](int c, int stage) __attribute__((always_inline)) {
         const uint32_t sbase = lds0 + stage * G::STAGE;
         const int ci0 = c * CPC;
@@ -330,23 +351,24 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
     // this wave's weight fragments: register ring, one chunk ahead (chunks past
     // the packed image read zeros)
     // (slot = this group's local K-step; st = the chunk's K-step)
-    u32x4_t wr[G::KS0][NJ][2];
+    u32x4_t wr[G::KS0][NJ][NP];
     // (staged chunk c, K-step st = sub-chunk u, packed K-step s0)
     auto load_w = [&](int c, int slot, int st) __attribute__((always_inline)) {
         const int u = st / KSC0, s0 = st - u * KSC0;
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
-            for (int pl = 0; pl < 2; ++pl)
+            for (int pl = 0; pl < NP; ++pl)
                 wr[slot][j][pl] = bload16(wrs, wbase + (unsigned)(c * VCX + u) * wcstride +
-                                                   (unsigned)(((j * KSC0 + s0) * 2 + pl) * 1024));
+                                                   (unsigned)(((j * KSC0 + s0) * NP + pl) * 1024));
     };
     // raw window of a stage -> activation (* xs) -> (hi, lo) f16 planes; returns
     // max |act| of the task's values (the range guard's vote input)
     auto convert_task = [&](int c, int stage, int pb, int i, float xs) __attribute__((always_inline)) {
         const float* raw = reinterpret_cast<const float*>(smem + stage * G::STAGE);
-        _Float16* xh = reinterpret_cast<_Float16*>(planes + pb * 2 * G::XPLANE);
-        _Float16* xl = reinterpret_cast<_Float16*>(planes + pb * 2 * G::XPLANE + G::XPLANE);
+        _Float16* xh = reinterpret_cast<_Float16*>(planes + pb * NP * G::XPLANE);
+        _Float16* xl = reinterpret_cast<_Float16*>(planes + pb * NP * G::XPLANE + G::XPLANE);
+        _Float16* xm = reinterpret_cast<_Float16*>(planes + pb * NP * G::XPLANE + 2 * G::XPLANE);   // BF
         const int ci0 = c * CPC;
         float m = 0.f;
         {
@@ -358,7 +380,7 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
                 // timing-only A/B variant (wrong results, never shipped): the planes
                 // arrive ready-made, as a producer-side split would deliver them --
                 // one 16-byte copy per plane row piece instead of act + split
-                if constexpr (!F32) {
+                if constexpr (AR == 0) {
                     const s_h8 r8 = *reinterpret_cast<const s_h8*>(raw + (g * 8 / S) * RS + off0 + w * S);
                     *reinterpret_cast<s_h8*>(xh + w * PH + g * 8) = r8;
                     *reinterpret_cast<s_h8*>(xl + w * PH + g * 8) = r8;
@@ -379,9 +401,15 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
                     v8[v] = val * xs;
                 }
                 if constexpr (F32) {
-                    float* xf = reinterpret_cast<float*>(planes + pb * 2 * G::XPLANE);
+                    float* xf = reinterpret_cast<float*>(planes + pb * NP * G::XPLANE);
                     *reinterpret_cast<s_f32x4*>(xf + w * PH + g * 8) = s_f32x4{v8[0], v8[1], v8[2], v8[3]};
                     *reinterpret_cast<s_f32x4*>(xf + w * PH + g * 8 + 4) = s_f32x4{v8[4], v8[5], v8[6], v8[7]};
+                } else if constexpr (BF) {
+                    s_b8 hi, mid, lo;
+                    s_bf3_split(v8, hi, mid, lo);
+                    *reinterpret_cast<s_b8*>(xh + w * PH + g * 8) = hi;
+                    *reinterpret_cast<s_b8*>(xl + w * PH + g * 8) = lo;
+                    *reinterpret_cast<s_b8*>(xm + w * PH + g * 8) = mid;
                 } else {
                     m = absmax8(v8);
                     const s_h8 hi = __builtin_convertvector(v8, s_h8);
@@ -444,23 +472,25 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
     for (int q = 0; q < G::Q; ++q) xoff[q] = (wn * WN + l32 + q * a.d + gshift) * PH + 8 * h;
 
     struct AFrag {
-        s_h8 h[NI], l[NI];
+        s_h8 h[NI], l[NI], m[NI];
     };
     auto read_a = [&](int pb, int st, AFrag& f) __attribute__((always_inline)) {
         const int u = st / KSC0, s0 = st - u * KSC0;
         const int q = s0 / HPS0, hv = u * (VC0 / 16) + (s0 - q * HPS0);   // 16-channel column group
-        const _Float16* xh = reinterpret_cast<const _Float16*>(planes + pb * 2 * G::XPLANE);
-        const _Float16* xl = reinterpret_cast<const _Float16*>(planes + pb * 2 * G::XPLANE + G::XPLANE);
+        const _Float16* xh = reinterpret_cast<const _Float16*>(planes + pb * NP * G::XPLANE);
+        const _Float16* xl = reinterpret_cast<const _Float16*>(planes + pb * NP * G::XPLANE + G::XPLANE);
+        const _Float16* xm = reinterpret_cast<const _Float16*>(planes + pb * NP * G::XPLANE + 2 * G::XPLANE);
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             if constexpr (F32) {   // 8 floats: channels 8h..8h+7 of the step's 16 (xoff counts floats)
-                const float* xf = reinterpret_cast<const float*>(planes + pb * 2 * G::XPLANE) + xoff[q] + i * 32 * PH +
+                const float* xf = reinterpret_cast<const float*>(planes + pb * NP * G::XPLANE) + xoff[q] + i * 32 * PH +
                                   hv * 16;
                 f.h[i] = *reinterpret_cast<const s_h8*>(xf);
                 f.l[i] = *reinterpret_cast<const s_h8*>(xf + 4);
             } else {
                 f.h[i] = *reinterpret_cast<const s_h8*>(xh + xoff[q] + i * 32 * PH + hv * 16);
                 f.l[i] = *reinterpret_cast<const s_h8*>(xl + xoff[q] + i * 32 * PH + hv * 16);
+                if constexpr (BF) f.m[i] = *reinterpret_cast<const s_h8*>(xm + xoff[q] + i * 32 * PH + hv * 16);
             }
         }
     };
@@ -477,7 +507,7 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
         constexpr bool guarded = decltype(guardtag)::value != 0;
         constexpr int KS = G::ks_of(GG);                // own K-steps per chunk
         constexpr int ST0 = G::st_of(GG);               // first own K-step
-        constexpr int WR = KS * NJ * 2, XI = G::XI;
+        constexpr int WR = KS * NJ * NP, XI = G::XI;
 #pragma unroll
         for (int i = 0; i < NS; ++i) issue(c_begin + i, i);
 #pragma unroll
@@ -516,10 +546,30 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
                 // weights of (c, k): issued one chunk ago; younger: the rest of that
                 // chunk's weights, this chunk's window DMA and this chunk's earlier refills
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) wait_vm_regs<2 * (WR / 2 - NJ) + XI>(wr[k][j][0], wr[k][j][1]);
+                for (int j = 0; j < NJ; ++j) {
+                    if constexpr (BF) wait_vm_regs3<WR - NP * NJ + XI>(wr[k][j][0], wr[k][j][1], wr[k][j][2]);
+                    else wait_vm_regs<WR - NP * NJ + XI>(wr[k][j][0], wr[k][j][1]);
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 const AFrag& g = f[k & 1];
-                if constexpr (F32) {
+                if constexpr (BF) {
+                    // smallest products first: (x, w) = hi*lo, lo*hi, mid*mid, hi*mid, mid*hi, hi*hi
+#pragma unroll
+                    for (int i = 0; i < NI; ++i)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) {
+                            const s_b8 xh8 = __builtin_bit_cast(s_b8, g.h[i]), xl8 = __builtin_bit_cast(s_b8, g.l[i]),
+                                       xm8 = __builtin_bit_cast(s_b8, g.m[i]);
+                            const s_b8 wh8 = __builtin_bit_cast(s_b8, wr[k][j][0]), wl8 = __builtin_bit_cast(s_b8, wr[k][j][1]),
+                                       wm8 = __builtin_bit_cast(s_b8, wr[k][j][2]);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh8, wl8, acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl8, wh8, acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xm8, wm8, acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh8, wm8, acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xm8, wh8, acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh8, wh8, acc[i][j], 0, 0, 0);
+                        }
+                } else if constexpr (F32) {
 #pragma unroll
                     for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
@@ -594,7 +644,7 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
         wait_vm<0>();                       // drain the ring (epilogue loads / a second attempt)
     };
     run_k(IC<0>{});
-    if (RAVE_SPLIT_GUARD && !F32) {
+    if (RAVE_SPLIT_GUARD && AR == 0) {
         bool bad = false;
 #pragma unroll
         for (int i = 0; i < NI; ++i)
@@ -866,11 +916,15 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
 
 template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX, int NS>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_split_kernel(ConvKArgs a) {
-    conv1d_split_body<KT, BM, BN, WM, SNAKE, XV, KG, WN_, VCX, NS, false>(a);
+    conv1d_split_body<KT, BM, BN, WM, SNAKE, XV, KG, WN_, VCX, NS, 0>(a);
 }
 template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX, int NS>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_ring_f32_kernel(ConvKArgs a) {
-    conv1d_split_body<KT, BM, BN, WM, SNAKE, XV, KG, WN_, VCX, NS, true>(a);
+    conv1d_split_body<KT, BM, BN, WM, SNAKE, XV, KG, WN_, VCX, NS, 1>(a);
+}
+template <int KT, int BM, int BN, int WM, bool SNAKE, bool XV, int KG, int WN_, int VCX, int NS>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN_) * KG) void conv1d_bf3_kernel(ConvKArgs a) {
+    conv1d_split_body<KT, BM, BN, WM, SNAKE, XV, KG, WN_, VCX, NS, 2>(a);
 }
 
 // --------------------------------------------------------------------- tiles
@@ -932,13 +986,13 @@ static inline auto with_tile(int ti, Fn&& f) {
 // instantiations are spread over separate translation units (the Makefile
 // compiles this file once per (KT, SNAKE, XV) with -DRAVE_SPLIT_KT / _SNAKE / _XV,
 // and once without them for the host side) so the build runs in parallel.
-template <int KT, bool SNAKE, bool XV, bool F32>
+template <int KT, bool SNAKE, bool XV, int AR>
 int split_launch_inst(ConvKArgs k, int tile, hipStream_t st);
 
 #ifdef RAVE_SPLIT_KT
-template <int KT, int BM, int BN, int WM, int KG, int WN, int VCX, int NS, bool SNAKE, bool XV, bool F32>
+template <int KT, int BM, int BN, int WM, int KG, int WN, int VCX, int NS, bool SNAKE, bool XV, int AR>
 static int split_launch_xv(ConvKArgs k, hipStream_t st) {
-    using G = SGeo<KT, BM, BN, WM, XV, KG, WN, VCX, NS>;
+    using G = SGeo<KT, BM, BN, WM, XV, KG, WN, VCX, NS, AR == 2 ? 3 : 2>;
     if constexpr (!G::VALID) {
         set_error("conv1d(split16): tile exceeds LDS or the vmcnt range");
         return RAVE_ERR_UNSUPPORTED;
@@ -951,7 +1005,8 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
         static_assert(lds <= 160 * 1024, "LDS budget");
         dim3 grid(k.gx * k.gy * k.B * k.S);
         auto kern = [] {
-            if constexpr (F32) return conv1d_ring_f32_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN, VCX, NS>;
+            if constexpr (AR == 2) return conv1d_bf3_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN, VCX, NS>;
+            else if constexpr (AR == 1) return conv1d_ring_f32_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN, VCX, NS>;
             else return conv1d_split_kernel<KT, BM, BN, WM, SNAKE, XV, KG, WN, VCX, NS>;
         }();
         if (lds > 64 * 1024) {
@@ -963,23 +1018,23 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
             }
         }
         launch(kern, grid, dim3(G::NT), (uint32_t)lds, st, k);
-        return launch_status(F32 ? "conv1d_ring_f32_kernel" : "conv1d_split_kernel");
+        return launch_status(AR == 2 ? "conv1d_bf3_kernel" : AR == 1 ? "conv1d_ring_f32_kernel" : "conv1d_split_kernel");
     }
 }
 
-template <int KT, bool SNAKE, bool XV, bool F32>
+template <int KT, bool SNAKE, bool XV, int AR>
 int split_launch_inst(ConvKArgs k, int tile, hipStream_t st) {
     return with_tile(tile, [&](auto bm, auto bn, auto wm, auto kg, auto wn, auto vcx, auto ns) {
         constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
                       KG = decltype(kg)::value, WN = decltype(wn)::value, VCX = decltype(vcx)::value,
                       NS = decltype(ns)::value;
-        return split_launch_xv<KT, BM, BN, WM, KG, WN, VCX, NS, SNAKE, XV, F32>(k, st);
+        return split_launch_xv<KT, BM, BN, WM, KG, WN, VCX, NS, SNAKE, XV, AR>(k, st);
     });
 }
 #ifndef RAVE_SPLIT_F32
 #define RAVE_SPLIT_F32 0
 #endif
-template int split_launch_inst<RAVE_SPLIT_KT, (RAVE_SPLIT_SNAKE != 0), (RAVE_SPLIT_XV != 0), (RAVE_SPLIT_F32 != 0)>(
+template int split_launch_inst<RAVE_SPLIT_KT, (RAVE_SPLIT_SNAKE != 0), (RAVE_SPLIT_XV != 0), RAVE_SPLIT_F32>(
     ConvKArgs, int, hipStream_t);
 
 }  // namespace rave
@@ -1027,34 +1082,39 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(ConvKArgs a) {
 // Tile + split-K choice: least padding with the most waves per workgroup
 // that still fills the chip; K split over workgroups (fp32 slabs, fixed-order
 // combine) when the output alone cannot give every SIMD a wave.
+// operand planes / weight fragments per K-step of an arithmetic (bf16x3: three)
+static int split_planes(int precision) { return precision == RAVE_PREC_BF16X3 ? 3 : 2; }
 static inline int tile_waves(int ti) {   // waves per workgroup
     const int* t = kSplitTiles[ti];
     return (t[0] / t[2]) * (t[1] / t[4]) * t[3];
 }
 
 template <int KT>
-static bool split_tile_fits(int idx) {   // both DMA variants must fit
-    return with_tile(idx, [](auto bm, auto bn, auto wm, auto kg, auto wn, auto vcx, auto ns) {
+static bool split_tile_fits(int idx, int np) {   // both DMA variants must fit (np: operand planes)
+    return with_tile(idx, [np](auto bm, auto bn, auto wm, auto kg, auto wn, auto vcx, auto ns) {
         constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, WM = decltype(wm)::value,
                       KG = decltype(kg)::value, WN = decltype(wn)::value, VCX = decltype(vcx)::value,
                       NS = decltype(ns)::value;
+        if (np == 3)
+            return SGeo<KT, BM, BN, WM, true, KG, WN, VCX, NS, 3>::VALID &&
+                   SGeo<KT, BM, BN, WM, false, KG, WN, VCX, NS, 3>::VALID;
         return SGeo<KT, BM, BN, WM, true, KG, WN, VCX, NS>::VALID &&
                SGeo<KT, BM, BN, WM, false, KG, WN, VCX, NS>::VALID;
     });
 }
-static bool split_fits(int taps, int idx) {
+static bool split_fits(int taps, int idx, int np) {
     if (idx < 0 || idx >= kNumSplitTiles || !kSplitTileBuilt[idx]) return false;
     switch (taps) {
-        case 1: return split_tile_fits<1>(idx);
-        case 2: return split_tile_fits<2>(idx);
-        case 3: return split_tile_fits<3>(idx);
-        case 4: return split_tile_fits<4>(idx);
-        case 7: return split_tile_fits<7>(idx);
-        default: return split_tile_fits<8>(idx);
+        case 1: return split_tile_fits<1>(idx, np);
+        case 2: return split_tile_fits<2>(idx, np);
+        case 3: return split_tile_fits<3>(idx, np);
+        case 4: return split_tile_fits<4>(idx, np);
+        case 7: return split_tile_fits<7>(idx, np);
+        default: return split_tile_fits<8>(idx, np);
     }
 }
 
-static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int split_row) {
+static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int split_row, int np) {
     const auto& all = kSplitTiles;
     auto waste = [&](int bm, int bn) {
         return double(ceil_div(M, bm) * bm) * double(ceil_div(U, bn) * bn) / (double(M) * double(U));
@@ -1064,7 +1124,7 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
     for (int ti = 0; ti < kNumSplitTiles; ++ti) {   // the heuristic keeps to the KG = 1 tiles
         const int* c = all[ti];
         if (c[3] != 1) continue;
-        if (!split_fits(taps, ti)) continue;
+        if (!split_fits(taps, ti, np)) continue;
         if (split_row < M && split_row % c[2] != 0) continue;      // a wave never straddles ConvT groups
         const int nw = tile_waves(ti);
         const int64_t wgs = (int64_t)ceil_div(M, c[0]) * ceil_div(U, c[1]) * B;
@@ -1085,22 +1145,24 @@ static SplitCfg split_choose(int taps, int M, int U, int B, int nchunks, int spl
 }
 
 template <int KT>
-static int split_launch_family(ConvKArgs k, const SplitCfg& c, bool f32, hipStream_t st) {
+static int split_launch_family(ConvKArgs k, const SplitCfg& c, int ar, hipStream_t st) {
     const int* t = kSplitTiles[c.tile];
     k.XW = t[1] + (SFam<KT>::Q - 1) * k.d + (k.transposed ? 1 : 0);
     k.xw_magic = (unsigned)(((1u << 24) + k.XW - 1) / k.XW);
     const unsigned rl = (unsigned)(k.XW * SFam<KT>::S);
     k.rl_magic = (unsigned)((0x100000000ull + rl - 1) / rl);
     const bool snake = k.act == RAVE_ACT_SNAKE;
-    if (f32 && !k.x_vec) {
-        // the fp32 ring kernels are built for 16-byte window DMA only (the
-        // register-staged RAVE_PREC_F32 kernel covers unaligned inputs)
-        set_error("conv1d(f32_ring): needs 16-byte aligned input rows and t_in % 4 == 0");
+    if (ar != 0 && !k.x_vec) {
+        // the fp32 ring and bf16x3 kernels are built for 16-byte window DMA only
+        // (the register-staged RAVE_PREC_F32 kernel covers unaligned inputs)
+        set_error(ar == 2 ? "conv1d(bf16x3): needs 16-byte aligned input rows and t_in % 4 == 0"
+                          : "conv1d(f32_ring): needs 16-byte aligned input rows and t_in % 4 == 0");
         return RAVE_ERR_UNSUPPORTED;
     }
-    auto fn = f32 ? (snake ? split_launch_inst<KT, true, true, true> : split_launch_inst<KT, false, true, true>)
-                  : (snake ? (k.x_vec ? split_launch_inst<KT, true, true, false> : split_launch_inst<KT, true, false, false>)
-                           : (k.x_vec ? split_launch_inst<KT, false, true, false> : split_launch_inst<KT, false, false, false>));
+    auto fn = ar == 2 ? (snake ? split_launch_inst<KT, true, true, 2> : split_launch_inst<KT, false, true, 2>)
+              : ar == 1 ? (snake ? split_launch_inst<KT, true, true, 1> : split_launch_inst<KT, false, true, 1>)
+              : (snake ? (k.x_vec ? split_launch_inst<KT, true, true, 0> : split_launch_inst<KT, true, false, 0>)
+                       : (k.x_vec ? split_launch_inst<KT, false, true, 0> : split_launch_inst<KT, false, false, 0>));
     return fn(k, c.tile, st);
 }
 
@@ -1110,7 +1172,7 @@ static int split_prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
     k.nchunks = ceil_div(a.c_in, split_cpc(taps));
     k.Mpad = ceil_div(k.M, 128) * 128;
     k.MB = k.Mpad / 32;
-    const int64_t frag_floats = (int64_t)k.nchunks * k.MB * split_ksc(taps) * 2 * 256;
+    const int64_t frag_floats = (int64_t)k.nchunks * k.MB * split_ksc(taps) * split_planes(a.precision) * 256;
     RAVE_CHECK_ARG(frag_floats * 4 < (1ll << 31), "conv1d(split16): packed weight beyond 2 GiB");
     k.w_bytes = (int)(frag_floats * 4);
     k.rscale = a.weight + frag_floats;                 // after the fragments
@@ -1124,19 +1186,19 @@ static int split_prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
     return RAVE_OK;
 }
 
-static bool split_tile_ok(int taps, int ti, int M, int split_row) {
-    return ti >= 0 && ti < kNumSplitTiles && split_fits(taps, ti) &&
+static bool split_tile_ok(int taps, int ti, int M, int split_row, int np) {
+    return ti >= 0 && ti < kNumSplitTiles && split_fits(taps, ti, np) &&
            (split_row >= M || split_row % kSplitTiles[ti][2] == 0);   // a wave never straddles ConvT groups
 }
 
 // The launch configuration: args.config when set (validated), else the heuristic.
 static int split_resolve(const rave_conv1d_args& a, const ConvKArgs& k, int taps, SplitCfg& c) {
     if (a.config == 0) {
-        c = split_choose(taps, k.M, k.U, k.B, k.nchunks, k.split_row);
+        c = split_choose(taps, k.M, k.U, k.B, k.nchunks, k.split_row, split_planes(a.precision));
         return RAVE_OK;
     }
     ConfigCode cc;
-    RAVE_CHECK_ARG(decode_config(a.config, cc) && split_tile_ok(taps, cc.tile, k.M, k.split_row) &&
+    RAVE_CHECK_ARG(decode_config(a.config, cc) && split_tile_ok(taps, cc.tile, k.M, k.split_row, split_planes(a.precision)) &&
                        split_count_distinct(cc.S, ceil_div(k.nchunks, kSplitTiles[cc.tile][5])),
                    "conv1d(split16): config not valid for these args (see rave_conv1d_configs)");
     c = {cc.tile, cc.S, cc.sep};
@@ -1154,7 +1216,7 @@ int conv1d_split_configs(const rave_conv1d_args& a, int32_t* cfgs, int max_cfgs)
         ++n;
     };
     for (int ti = 0; ti < kNumSplitTiles; ++ti) {
-        if (!split_tile_ok(taps, ti, k.M, k.split_row)) continue;
+        if (!split_tile_ok(taps, ti, k.M, k.split_row, split_planes(a.precision))) continue;
         const int* t = kSplitTiles[ti];
         const int nw = tile_waves(ti);
         const int64_t ntiles = (int64_t)ceil_div(k.M, t[0]) * ceil_div(k.U, t[1]) * k.B;
@@ -1207,14 +1269,14 @@ int conv1d_split(const rave_conv1d_args& a, void* stream) {
     k.stamps = a.stamps;
 #endif
     hipStream_t st = as_stream(stream);
-    const bool f32 = a.precision == RAVE_PREC_F32_RING;
+    const int ar = a.precision == RAVE_PREC_BF16X3 ? 2 : a.precision == RAVE_PREC_F32_RING ? 1 : 0;
     switch (taps) {
-        case 1: rc = split_launch_family<1>(k, c, f32, st); break;
-        case 2: rc = split_launch_family<2>(k, c, f32, st); break;
-        case 3: rc = split_launch_family<3>(k, c, f32, st); break;
-        case 4: rc = split_launch_family<4>(k, c, f32, st); break;
-        case 7: rc = split_launch_family<7>(k, c, f32, st); break;
-        case 8: rc = split_launch_family<8>(k, c, f32, st); break;
+        case 1: rc = split_launch_family<1>(k, c, ar, st); break;
+        case 2: rc = split_launch_family<2>(k, c, ar, st); break;
+        case 3: rc = split_launch_family<3>(k, c, ar, st); break;
+        case 4: rc = split_launch_family<4>(k, c, ar, st); break;
+        case 7: rc = split_launch_family<7>(k, c, ar, st); break;
+        case 8: rc = split_launch_family<8>(k, c, ar, st); break;
         default: set_error("conv1d: unsupported kernel size"); return RAVE_ERR_UNSUPPORTED;
     }
     if (rc != RAVE_OK || k.S <= 1 || k.inlaunch) return rc;
@@ -1260,8 +1322,8 @@ static int split_geometry(int c_in, int c_out, int kernel, int stride, int dilat
     return 0;
 }
 
-extern "C" int64_t rave_conv1d_split_packed_size(int c_in, int c_out, int kernel, int stride, int dilation,
-                                                 int transposed) {
+static int64_t split_packed_floats(int c_in, int c_out, int kernel, int stride, int dilation, int transposed,
+                                   int np) {
     if (c_in <= 0 || c_out <= 0) return -1;
     int taps, M, Mpad, nchunks, split_row, q0;
     // transposed: the larger of the two row layouts (out_shift 0 / stride/2)
@@ -1270,15 +1332,41 @@ extern "C" int64_t rave_conv1d_split_packed_size(int c_in, int c_out, int kernel
         if (split_geometry(c_in, c_out, kernel, stride, dilation, transposed, os ? stride / 2 : 0, taps, M,
                            Mpad, nchunks, split_row, q0) != 0)
             return -1;
-        const int64_t n = (int64_t)nchunks * (Mpad / 32) * split_ksc(taps) * 2 * 256 + Mpad;
+        const int64_t n = (int64_t)nchunks * (Mpad / 32) * split_ksc(taps) * np * 256 + Mpad;
         best = std::max(best, n);
     }
     return best;
 }
 
+extern "C" int64_t rave_conv1d_split_packed_size(int c_in, int c_out, int kernel, int stride, int dilation,
+                                                 int transposed) {
+    return split_packed_floats(c_in, c_out, kernel, stride, dilation, transposed, 2);
+}
+
+extern "C" int64_t rave_conv1d_bf3_packed_size(int c_in, int c_out, int kernel, int stride, int dilation,
+                                               int transposed) {
+    return split_packed_floats(c_in, c_out, kernel, stride, dilation, transposed, 3);
+}
+
+// host fp32 -> bf16, round to nearest even (finite weights)
+static uint16_t bf16_bits(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+static float bf16_value(uint16_t h) {
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
 static int split_pack(const float* w, int c_in, int c_out, int kernel, int stride, int dilation, int transposed,
-                      int out_shift, float* packed, bool f32) {
+                      int out_shift, float* packed, int mode) {   // 0 split16, 1 fp32, 2 bf16x3
     RAVE_CHECK_ARG(w && packed, "split_pack_weight: null pointer");
+    const bool f32 = mode != 0;                        // (row scales 1)
+    const int NPW = mode == 2 ? 3 : 2;
     RAVE_CHECK_ARG(c_in > 0 && c_out > 0 && kernel > 0 && stride > 0 && dilation > 0,
                    "split_pack_weight: bad shape");
     RAVE_CHECK_ARG(!transposed || out_shift == 0 || out_shift == stride / 2,
@@ -1321,11 +1409,13 @@ static int split_pack(const float* w, int c_in, int c_out, int kernel, int strid
         ex[m] = row_exponent(amax);
     }
     _Float16* out = reinterpret_cast<_Float16*>(packed);
+    uint16_t* bout = reinterpret_cast<uint16_t*>(packed);
     for (int c = 0; c < nchunks; ++c)
         for (int mb = 0; mb < MB; ++mb)
             for (int st = 0; st < KSC; ++st) {
                 const int q = st / HPS, hv = st % HPS;
-                const int64_t blk = ((int64_t)(c * MB + mb) * KSC + st) * 2;   // 1 KB slots
+                const int64_t blk = ((int64_t)(c * MB + mb) * KSC + st) * NPW;   // 1 KB slots
+                uint16_t* bp = bout + blk * 512;       // bf16x3: hi, lo, mid
                 _Float16* hi = out + blk * 512;
                 _Float16* lo = hi + 512;
                 float* f32s = packed + blk * 256;      // fp32: floats 0-3 of a lane in slot 0, 4-7 in slot 1
@@ -1335,6 +1425,16 @@ static int split_pack(const float* w, int c_in, int c_out, int kernel, int strid
                         const int vc = hv * 16 + 8 * (l >> 5) + e;
                         int ci, j;
                         kmap(c, q, vc, ci, j);
+                        if (mode == 2) {
+                            const float v = wval(m, ci, j);
+                            const uint16_t h = bf16_bits(v);
+                            const float r = v - bf16_value(h);
+                            const uint16_t md = bf16_bits(r);
+                            bp[l * 8 + e] = h;
+                            bp[1024 + l * 8 + e] = md;
+                            bp[512 + l * 8 + e] = bf16_bits(r - bf16_value(md));
+                            continue;
+                        }
                         if (f32) {
                             f32s[(e >> 2) * 256 + l * 4 + (e & 3)] = wval(m, ci, j);
                             continue;
@@ -1346,18 +1446,23 @@ static int split_pack(const float* w, int c_in, int c_out, int kernel, int strid
                         lo[l * 8 + e] = vl;
                     }
             }
-    float* rs = packed + (int64_t)nchunks * MB * KSC * 2 * 256;
+    float* rs = packed + (int64_t)nchunks * MB * KSC * NPW * 256;
     for (int m = 0; m < Mpad; ++m) rs[m] = f32 ? 1.0f : (float)std::ldexp(1.0, -(ex[m] + 11));
     return RAVE_OK;
 }
 
 extern "C" int rave_conv1d_split_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
                                              int dilation, int transposed, int out_shift, float* packed) {
-    return split_pack(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift, packed, false);
+    return split_pack(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift, packed, 0);
 }
 
 extern "C" int rave_conv1d_ring_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
                                             int dilation, int transposed, int out_shift, float* packed) {
-    return split_pack(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift, packed, true);
+    return split_pack(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift, packed, 1);
+}
+
+extern "C" int rave_conv1d_bf3_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
+                                           int dilation, int transposed, int out_shift, float* packed) {
+    return split_pack(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift, packed, 2);
 }
 #endif  // RAVE_SPLIT_KT

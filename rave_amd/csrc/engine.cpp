@@ -553,7 +553,7 @@ std::pair<int, int> Model::conv_launch(const Node& n, const rave_conv1d_args& s,
         base.partial = nullptr;
         std::vector<std::pair<int, int>> cands;
         for (int pr : precs) {
-            if (!allow_ring && pr == RAVE_PREC_F32_RING) continue;
+            if (!allow_ring && (pr == RAVE_PREC_F32_RING || pr == RAVE_PREC_BF16X3)) continue;
             if (!pack.count({n.name, pr})) continue;     // (an arithmetic of the fused units only)
             base.precision = pr;
             base.weight = aptr(pack.at({n.name, pr}));
@@ -1678,15 +1678,17 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
                                               : std::vector<float>(get(n->name + ".weight"),
                                                                    get(n->name + ".weight") + rows * per_row);
         for (int pr : m->precs) {
-            if (pr == RAVE_PREC_BF16X3) continue;    // (fused units only)
             for (int form = 0; form < (n->transposed ? 2 : 1); ++form) {
                 const int os = n->transposed ? (form == 0 ? n->stride / 2 : 0) : 0;
                 // split16 and the fp32 ring path share the fragment image layout
                 const bool sp = pr == RAVE_PREC_SPLIT16 || pr == RAVE_PREC_F32_RING;
-                const int64_t sz = sp ? rave_conv1d_split_packed_size(n->c_in, n->c_out, n->kernel, n->stride,
-                                                                      n->dilation, n->transposed)
-                                      : rave_conv1d_packed_size(n->c_in, n->c_out, n->kernel, n->stride, n->dilation,
-                                                                n->transposed);
+                const int64_t sz = pr == RAVE_PREC_BF16X3
+                                       ? rave_conv1d_bf3_packed_size(n->c_in, n->c_out, n->kernel, n->stride,
+                                                                     n->dilation, n->transposed)
+                                   : sp ? rave_conv1d_split_packed_size(n->c_in, n->c_out, n->kernel, n->stride,
+                                                                        n->dilation, n->transposed)
+                                        : rave_conv1d_packed_size(n->c_in, n->c_out, n->kernel, n->stride, n->dilation,
+                                                                  n->transposed);
                 if (sz <= 0) fail(RAVE_ERR_UNSUPPORTED, "conv " + n->name + ": unsupported layer shape");
                 std::vector<float> packed((size_t)sz, 0.f);
                 const int rc =
@@ -1696,6 +1698,9 @@ static Model* create_model(const rave_model_config& cfg, const rave_param* param
                     : pr == RAVE_PREC_F32_RING
                         ? rave_conv1d_ring_pack_weight(w.data(), n->c_in, n->c_out, n->kernel, n->stride, n->dilation,
                                                        n->transposed, os, packed.data())
+                    : pr == RAVE_PREC_BF16X3
+                        ? rave_conv1d_bf3_pack_weight(w.data(), n->c_in, n->c_out, n->kernel, n->stride, n->dilation,
+                                                      n->transposed, os, packed.data())
                         : rave_conv1d_pack_weight(w.data(), n->c_in, n->c_out, n->kernel, n->stride, n->dilation,
                                                   n->transposed, os, packed.data());
                 check_rc(rc, "pack " + n->name);

@@ -142,12 +142,15 @@ __device__ __forceinline__ float us_act(float v, float slope, float alpha) {
 
 // C channels; WGN waves along time (each 64 columns); C/(32 MI) waves along
 // rows (each MI 32-row blocks).
+// NP = 3 (bf16x3) at C = 512: the window is sized for dilations <= kUSBf512Dil so
+// that three planes fit the CU's LDS (RAVE's C = 512 stages use dilations 1 and 3)
+constexpr int kUSBf512Dil = 4;
 template <int C, int WGN, int MI, int KG = 1, int CB = 2, int RB = 1, int NP = 2> struct USGeo {
     static constexpr int WGM = C / (32 * MI * RB), NWT = WGM * WGN, NW = NWT * KG, NT = 64 * NW;
     static constexpr int BN = 32 * CB * WGN;           // CB 32-column blocks per wave
     static constexpr int S1 = 3 * C / 16, S2 = C / 16, ST = S1 + S2;   // K-steps
     static constexpr int PH = C + 8;                  // halves per LDS row (conflict-free b128)
-    static constexpr int XW_MAX = BN + 2 * kUSMaxDil;
+    static constexpr int XW_MAX = BN + 2 * ((NP == 3 && C == 512) ? kUSBf512Dil : kUSMaxDil);
     static constexpr int XPLANE = XW_MAX * PH * 2;    // bytes per f16 plane
     static constexpr int HPLANE = BN * PH * 2;
     static constexpr int PL1 = XPLANE > HPLANE ? XPLANE : HPLANE;   // bytes per plane
@@ -904,8 +907,9 @@ static int us_launch(USArgs k, int B, bool snake, int ar, hipStream_t st) {
     using G = USGeo<C, WGN, MI, KG, CB, RB>;
     using G3 = USGeo<C, WGN, MI, KG, CB, RB, 3>;
     const bool f32 = ar == 1;
-    if (k.XW > G::XW_MAX) {
-        set_error("residual_unit(split16): dilation too large");
+    if (k.XW > (ar == 2 ? G3::XW_MAX : G::XW_MAX)) {
+        set_error(ar == 2 && C == 512 ? "residual_unit(bf16x3): C = 512 supports dilations <= 4"
+                                      : "residual_unit(split16): dilation too large");
         return RAVE_ERR_UNSUPPORTED;
     }
     k.ntiles = ceil_div(k.T, G::BN);
@@ -1065,16 +1069,12 @@ extern "C" int rave_unit_ring_pack_weight(const float* w1, const float* w2, int 
 
 // bf16x3: fragments [C/32][S1+S2][hi, lo, mid][64 lanes][8 bf16], then rs1, rs2 (= 1)
 extern "C" int64_t rave_unit_bf3_packed_size(int C) {
-    if (C != 64 && C != 128 && C != 256) return -1;
+    if (!us_supported(C)) return -1;
     const int ST = 4 * C / 16;
     return (int64_t)(C / 32) * ST * 3 * 256 + 2 * C;
 }
 
 extern "C" int rave_unit_bf3_pack_weight(const float* w1, const float* w2, int C, float* packed) {
-    if (C != 64 && C != 128 && C != 256) {
-        set_error("unit_bf3_pack_weight: the bf16x3 fused unit supports C in {64, 128, 256}");
-        return RAVE_ERR_UNSUPPORTED;
-    }
     return unit_pack(w1, w2, C, packed, 2);
 }
 
@@ -1134,10 +1134,6 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
     USArgs k{};
     k.x = a.x; k.y = a.y; k.w = a.weight;
     const int ar = a.precision == RAVE_PREC_BF16X3 ? 2 : a.precision == RAVE_PREC_F32_RING ? 1 : 0;
-    if (ar == 2 && C == 512) {
-        set_error("residual_unit(bf16x3): C = 512 does not fit the CU's LDS as three planes");
-        return RAVE_ERR_UNSUPPORTED;
-    }
     const int64_t frag = (int64_t)(C / 32) * (4 * C / 16) * (ar == 2 ? 3 : 2) * 256;
     k.rs1 = a.weight + frag; k.rs2 = a.weight + frag + C;
     k.b1 = a.bias1; k.b2 = a.bias2; k.a0 = a.alpha0; k.a2 = a.alpha2;

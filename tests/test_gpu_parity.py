@@ -150,11 +150,11 @@ def conv_case(case):
 
 
 def _ring_skip(precision, T):
-    if precision == "f32_ring" and T % 4:
+    if precision in ("f32_ring", "bf16x3") and T % 4:
         pytest.skip("the fp32 ring kernels need 16-byte aligned rows (refusal: test_conv_ring_refuses_unaligned)")
 
 
-@pytest.mark.parametrize("precision", ["f32", "split16", "f32_ring"])
+@pytest.mark.parametrize("precision", ["f32", "split16", "f32_ring", "bf16x3"])
 @pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("case", CONV_CASES, ids=[str(c[:8]) for c in CONV_CASES])
 def test_conv_layer(N, dev, case, split, precision):
@@ -170,7 +170,7 @@ def test_conv_layer(N, dev, case, split, precision):
 CONFIG_CASES = [CONV_CASES[i] for i in (1, 2, 4, 5, 8, 9, 11, 12, 14)] + CONV_CASES[-2:]
 
 
-@pytest.mark.parametrize("precision", ["f32", "split16", "f32_ring"])
+@pytest.mark.parametrize("precision", ["f32", "split16", "f32_ring", "bf16x3"])
 @pytest.mark.parametrize("case", CONFIG_CASES, ids=[str(c[:8]) for c in CONFIG_CASES])
 def test_conv_every_config(N, dev, case, precision):
     """Every launch configuration rave_conv1d_configs() offers the autotuner

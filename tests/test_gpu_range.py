@@ -290,3 +290,49 @@ def test_model_range_guard_vs_oracle(dev, precision):
     print(f"\n[range] v2 {precision}: |z| max {np.abs(zr).max():.2f}, z err {ez:.3e} (f32 {maxabs(zf, zr):.3e}); "
           f"y err {ey:.3e} (f32 {maxabs(yf, yr):.3e})")
     assert ez < 1e-4 and ey < 1e-4
+
+
+# ------------------------------------------------------------------ bf16x3: no guard needed
+@pytest.mark.parametrize("scale", [3e6, 1e-20])
+@pytest.mark.parametrize("C_", [64, 256, 512])
+def test_unit_bf16x3_wide_range(N, dev, C_, scale):
+    """rave_residual_unit in bf16x3: the three bf16 parts keep fp32's exponent
+    range, so operands far past f16's (3e6) or far below it (1e-20) need no
+    range guard and stay fp32-exact relative to the output scale."""
+    d, B, T = 3, 2, 200
+    rng = np.random.default_rng(C_ + 11)
+    x = (scale * rng.standard_normal((B, C_, T))).astype(np.float32)
+    w1 = (rng.standard_normal((C_, C_, 3)) / np.sqrt(3 * C_)).astype(np.float32)
+    w2 = (rng.standard_normal((C_, C_, 1)) / np.sqrt(C_)).astype(np.float32)
+    b1 = (0.1 * scale * rng.standard_normal(C_)).astype(np.float32)
+    b2 = (0.1 * scale * rng.standard_normal(C_)).astype(np.float32)
+    ref = _unit_ref(x, w1, w2, b1, b2, d, (d, d))
+    packed = torch.from_numpy(N.pack_unit_weight(w1, w2, C_, precision=N.PREC_BF16X3)).to(dev)
+    xd = torch.from_numpy(x).to(dev)
+    y = torch.full_like(xd, float("nan"))
+    bd1, bd2 = torch.from_numpy(b1).to(dev), torch.from_numpy(b2).to(dev)
+    a = N.UnitArgs(channels=C_, batch=B, t_len=T, dilation=d, pad_left=d, act=N.ACT["leaky"], leaky_slope=0.2,
+                   precision=N.PREC_BF16X3, x=xd.data_ptr(), x_sb=C_ * T, x_sc=T, y=y.data_ptr(), y_sb=C_ * T,
+                   y_sc=T, weight=packed.data_ptr(), bias1=bd1.data_ptr(), bias2=bd2.data_ptr())
+    N.check(N.lib.rave_residual_unit(C.byref(a), _stream()))
+    torch.cuda.synchronize()
+    got = y.cpu().numpy()
+    assert np.isfinite(got).all()
+    assert maxabs(got, ref) <= 2e-6 * float(np.abs(ref).max())
+
+
+@pytest.mark.parametrize("scale", [3e6, 1e-20])
+def test_conv_bf16x3_wide_range(N, dev, scale):
+    """rave_conv1d in bf16x3 far outside f16's range (no guard pass exists)."""
+    from oracle.rave_oracle import conv1d, leaky_relu
+    from tests.test_gpu_parity import run_conv
+    c_in, c_out, k, d, B, T = 256, 512, 4, 1, 4, 64
+    rng = np.random.default_rng(3)
+    x = (scale * rng.standard_normal((B, c_in, T))).astype(np.float32)
+    bound = 1 / np.sqrt(c_in * k)
+    w = rng.uniform(-bound, bound, (c_out, c_in, k)).astype(np.float32)
+    b = (scale * rng.uniform(-bound, bound, c_out)).astype(np.float32)
+    ref = conv1d(leaky_relu(x.astype(np.float64)), w, b, 2, d, (1, 1))
+    got = run_conv(N, dev, x, w, b, None, None, c_in, c_out, k, 2, d, (1, 1), 0, "leaky", precision=N.PREC_BF16X3)
+    assert np.isfinite(got).all()
+    assert maxabs(got, ref) <= 2e-6 * float(np.abs(ref).max())

@@ -1,13 +1,15 @@
 #!/bin/bash
-# One profiling pass of bench.py on the GPU box (run through gpurun), for both
-# arithmetic modes the bench line reports -- the headline (f32_tuned: exact fp32
-# on every op) and the mixed line beside it (auto: split-f16 / fp32 per op):
+# One profiling pass of bench.py on the GPU box (run through gpurun), for the
+# arithmetic modes the bench line reports -- the headline (f32_bf3: fp32 on every
+# op, exact-fp32 MFMA or bf16x3), f32_tuned (exact fp32 MFMA on every op) and the
+# mixed line (auto: split-f16 / fp32 per op):
 #   1. the plain bench line (with the CPU baseline), then each mode alone,
 #   2. rocprofv3 --kernel-trace --stats of the same command (per-kernel times),
 #   3./4. separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes (HBM traffic; the two
 #      counters do not fit one gfx950 pass),
 #   5. a --pmc SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE pass (MFMA utilisation per family),
-# then tools/rocprof_summary.py and tools/mfma_util.py; steps 2-5 again for f32_tuned.
+# then tools/rocprof_summary.py and tools/mfma_util.py; steps 2-5 again for f32_tuned
+# and for f32_bf3.
 # Every run uses the committed launch choices (profiles/tuning/, bench.py's
 # default), so no autotune launches enter the traces and every pass runs the
 # same plan.  Every GPU step has its own time limit; the script stops at the
@@ -25,7 +27,7 @@ timeout -k 10 300 python3 $R/bench.py --steps 10 --warmup 3 --precision auto --n
     > "$OUT/bench_auto.json" 2> "$OUT/bench_auto.err"
 gemm_rows() {   # counter CSVs are large; keep the GEMM-family rows only
     head -n 1 "$1" > "$1.gemm"
-    grep -E 'conv1d|split_reduce|unit_kernel|unit_split|unit_ring|stack_split|pqmf|encoder_head|decoder_tail' "$1" >> "$1.gemm" || true
+    grep -E 'conv1d|split_reduce|unit_kernel|unit_split|unit_ring|unit_bf3|stack_split|pqmf|encoder_head|decoder_tail' "$1" >> "$1.gemm" || true
     rm -f "$1"
 }
 # ---------------------------------------------------------------- mixed mode (auto)
@@ -79,4 +81,30 @@ python3 "$R/tools/rocprof_summary.py" --trace "$KT32" --fetch "$FE32" --write "$
 find "$OUT/kt_f32" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats_f32.csv" \;
 gemm_rows "$FE32"
 gemm_rows "$WR32"
+# ---------------------------------------------------------------- headline: f32_bf3
+timeout -k 10 300 python3 $R/bench.py --steps 10 --warmup 3 --precision f32_bf3 --no-f32 $QUIET \
+    > "$OUT/bench_bf3.json" 2> "$OUT/bench_bf3.err"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_bf3" -o run -- \
+    python3 $R/bench.py --steps 10 --warmup 3 --precision f32_bf3 --no-f32 $QUIET > "$OUT/bench_bf3_kt.json" 2> "$OUT/bench_bf3_kt.err"
+echo "bf3 kernel-trace pass done"
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch_bf3" -o run -- \
+    python3 $R/bench.py --steps 2 --warmup 1 --no-profile --precision f32_bf3 --no-f32 $QUIET > "$OUT/bench_bf3_fetch.json" 2> "$OUT/bench_bf3_fetch.err"
+echo "bf3 fetch pass done"
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write_bf3" -o run -- \
+    python3 $R/bench.py --steps 2 --warmup 1 --no-profile --precision f32_bf3 --no-f32 $QUIET > "$OUT/bench_bf3_write.json" 2> "$OUT/bench_bf3_write.err"
+echo "bf3 write pass done"
+timeout -k 10 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/mfma_bf3" -o run -- \
+    python3 $R/bench.py --steps 2 --warmup 1 --no-profile --precision f32_bf3 --no-f32 $QUIET > "$OUT/bench_bf3_mfma.json" 2> "$OUT/bench_bf3_mfma.err"
+echo "bf3 mfma pass done"
+MFB=$(find "$OUT/mfma_bf3" -name '*counter_collection.csv' | head -n 1)
+python3 "$R/tools/mfma_util.py" "$MFB" "$OUT/bench_bf3.json" > "$OUT/mfma_util_bf3.json"
+gemm_rows "$MFB"
+KTB=$(find "$OUT/kt_bf3" -name '*kernel_trace.csv' | head -n 1)
+FEB=$(find "$OUT/fetch_bf3" -name '*counter_collection.csv' | head -n 1)
+WRB=$(find "$OUT/write_bf3" -name '*counter_collection.csv' | head -n 1)
+python3 "$R/tools/rocprof_summary.py" --trace "$KTB" --fetch "$FEB" --write "$WRB" --bench "$OUT/bench_bf3.json" \
+    --out "$OUT/summary_bf3.json" --traffic-out "$OUT/traffic_f32_bf3.json" --precision f32_bf3 > /dev/null
+find "$OUT/kt_bf3" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats_bf3.csv" \;
+gemm_rows "$FEB"
+gemm_rows "$WRB"
 ls -la "$OUT"

@@ -30,6 +30,8 @@ FAMILIES = {
     "conv_split16": (("conv1d_split_kernel",), ("split_reduce_kernel",)),
     "unit_f32": (("residual_unit_kernel", "unit_ring_f32_kernel"), ()),
     "unit_split16": (("unit_split_kernel",), ()),
+    "conv_bf16x3": (("conv1d_bf3_kernel",), ()),
+    "unit_bf16x3": (("unit_bf3_kernel",), ()),
     "stack_split16": (("stack_split_kernel",), ()),
     "pqmf_analysis_f32": (("pqmf_analysis_kernel",), ()),
     "pqmf_synthesis_f32": (("pqmf_synthesis_kernel",), ()),
@@ -51,6 +53,11 @@ for _fam, (_mains, _helpers) in FAMILIES.items():
 def set_precision(precision: str) -> None:
     """Exact-fp32 runs: the split kernels' separate K-split reduce belongs to
     the fp32 ring convs (conv1d_ring_f32_kernel), not to a split16 family."""
+    if precision == "f32_bf3":
+        # (the split kernels' reduce: counted with the bf16x3 convs, which take most split-K launches)
+        _KERNEL_FAMILY["split_reduce_kernel"] = ("conv_bf16x3", False)
+        _KERNEL_FAMILY["encoder_head_kernel"] = ("head_f32", True)
+        _KERNEL_FAMILY["decoder_tail_kernel"] = ("tail_f32", True)
     if precision in ("f32", "f32_tuned"):
         _KERNEL_FAMILY["split_reduce_kernel"] = ("conv_f32", False)
         _KERNEL_FAMILY["encoder_head_kernel"] = ("head_f32", True)     # the edges' exact-fp32 form
