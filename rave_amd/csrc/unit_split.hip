@@ -199,7 +199,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
     constexpr int NPW = BF ? 3 : 2;                  // operand planes / weight fragments per K-step
     using G = USGeo<C, WGN, MI, KG, CB, RB, NPW>;
     constexpr bool GV = GUARD && AR == 0 && RAVE_SPLIT_GUARD != 0;   // votes inside the body
-    static_assert(RB == 1 || GUARD || F32, "the cooperative form runs guarded");
+    static_assert(RB == 1 || GUARD || AR != 0, "the cooperative split16 form runs guarded");
     constexpr int NT = G::NT, PH = G::PH, G8 = G::G8, XT = G::XT, R = G::R;
     constexpr int S1 = G::S1, ST = G::ST, CG = C / 16;
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -524,7 +524,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
                 wl[i] = __builtin_bit_cast(us_b8, ring[t % R][i][1]);
                 wmd[i] = __builtin_bit_cast(us_b8, ring[t % R][i][2]);
             }
-            load_a(t % R, s + R * KG);               // refill the slot (runs on into W2)
+            load_a(t % R, RB > 1 ? smap(t + R) : s + R * KG);   // refill the slot (runs on into W2)
             // smallest products first: lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi
 #pragma unroll
             for (int i = 0; i < MI; ++i)
@@ -733,7 +733,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
         for (int r = 0; r < RB; ++r)
             gmax = fmaxf(gmax, __builtin_bit_cast(float, __hip_atomic_load(reinterpret_cast<unsigned*>(a.xmax) + lg * RB + r,
                                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-        if constexpr (!F32) sh2 = __builtin_amdgcn_readfirstlane((RAVE_SPLIT_GUARD && gmax >= kSplitLimit) ? split_shift(gmax) : 0);
+        if constexpr (AR == 0) sh2 = __builtin_amdgcn_readfirstlane((RAVE_SPLIT_GUARD && gmax >= kSplitLimit) ? split_shift(gmax) : 0);
         // stage the other members' rows (all rows, scaled, on the rare guarded path)
         auto stage_rows = [&](auto alltag, float xs) __attribute__((always_inline)) {
             constexpr bool all = decltype(alltag)::value != 0;
@@ -760,6 +760,14 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
                 if constexpr (F32) {
                     *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8) = v0[i];
                     *reinterpret_cast<us_f32x4*>(pf + w * PH + g * 8 + 4) = v1[i];
+                } else if constexpr (BF) {
+                    const us_f32x8 v8 = us_f32x8{v0[i][0], v0[i][1], v0[i][2], v0[i][3],
+                                                 v1[i][0], v1[i][1], v1[i][2], v1[i][3]};
+                    us_b8 hi, mid, lo;
+                    bf3_split(v8, hi, mid, lo);
+                    *reinterpret_cast<us_b8*>(ph + w * PH + g * 8) = hi;
+                    *reinterpret_cast<us_b8*>(pl + w * PH + g * 8) = lo;
+                    *reinterpret_cast<us_b8*>(pm + w * PH + g * 8) = mid;
                 } else {
                     const us_f32x8 v8 = us_f32x8{v0[i][0], v0[i][1], v0[i][2], v0[i][3],
                                                  v1[i][0], v1[i][1], v1[i][2], v1[i][3]} * xs;
@@ -896,9 +904,9 @@ template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, int RB>
 __global__ __launch_bounds__(64 * (C / (32 * MI * RB)) * WGN * KG) void unit_ring_f32_kernel(USArgs a) {
     (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, 1, RB, false>(a);
 }
-template <int C, int WGN, int MI, int KG, int CB, bool SNAKE>
-__global__ __launch_bounds__(64 * (C / (32 * MI)) * WGN * KG) void unit_bf3_kernel(USArgs a) {
-    (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, 2, 1, false>(a);
+template <int C, int WGN, int MI, int KG, int CB, bool SNAKE, int RB>
+__global__ __launch_bounds__(64 * (C / (32 * MI * RB)) * WGN * KG) void unit_bf3_kernel(USArgs a) {
+    (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, 2, RB, false>(a);
 }
 
 // ar: 0 split16, 1 exact fp32 (ring), 2 bf16x3
@@ -916,9 +924,9 @@ static int us_launch(USArgs k, int B, bool snake, int ar, hipStream_t st) {
     void (*kern)(USArgs) = nullptr;
     int lds = G::LDS;
     if (ar == 2) {
-        // three operand planes: built where they fit the CU's LDS (one workgroup per slab)
-        if constexpr (RB == 1 && G3::LDS <= 160 * 1024) {
-            kern = snake ? unit_bf3_kernel<C, WGN, MI, KG, CB, true> : unit_bf3_kernel<C, WGN, MI, KG, CB, false>;
+        // three operand planes: built where they fit the CU's LDS
+        if constexpr (G3::LDS <= 160 * 1024) {
+            kern = snake ? unit_bf3_kernel<C, WGN, MI, KG, CB, true, RB> : unit_bf3_kernel<C, WGN, MI, KG, CB, false, RB>;
             lds = G3::LDS;
         } else {
             set_error("residual_unit(bf16x3): this width does not fit the CU's LDS as three planes");
@@ -939,12 +947,12 @@ static int us_launch(USArgs k, int B, bool snake, int ar, hipStream_t st) {
         // forward progress needs a whole group resident on one XCD at once:
         // RB workgroups of this geometry must fit that XCD's CUs (else the
         // caller runs the one-workgroup form)
-        static int fits[4] = {-1, -1, -1, -1};
-        int& f = fits[2 * f32 + snake];
+        static int fits[6] = {-1, -1, -1, -1, -1, -1};
+        int& f = fits[2 * ar + snake];
         if (f < 0) {
             int per_cu = 0, dev = 0, cus = 0;
             RAVE_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern),
-                                                                        G::NT, G::LDS));
+                                                                        G::NT, lds));
             RAVE_CHECK_HIP(hipGetDevice(&dev));
             RAVE_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
             f = (int64_t)per_cu * (cus / kXcds) >= RB ? 1 : 0;
@@ -1107,7 +1115,8 @@ static CoopLayout coop_layout(const rave_unit_args& a) {
     CoopLayout L;
     const int C = a.channels;
     if ((C != 256 && C != 512) || !coop_enabled() || a.batch <= 0 || a.t_len <= 0) return L;
-    if (a.precision != RAVE_PREC_SPLIT16 && a.precision != RAVE_PREC_F32_RING) return L;
+    if (a.precision != RAVE_PREC_SPLIT16 && a.precision != RAVE_PREC_F32_RING && a.precision != RAVE_PREC_BF16X3)
+        return L;
     const int64_t ng = (int64_t)ceil_div(a.t_len, kCoopBN) * a.batch;
     const int64_t ngp = ceil_div64(ng, 8) * 8;
     // counters live in the split-K ticket words (zero at rest, as the conv
@@ -1167,7 +1176,7 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
             reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && std::getenv("RAVE_UNIT_XV") == nullptr) ? 1 : 0;
     // cooperative form when the caller passed its workspace
     const CoopLayout L = coop_layout(a);
-    if (L.rb > 1 && a.workspace && ar != 2) {
+    if (L.rb > 1 && a.workspace) {
         k.flag_stride = L.stride;
         k.flags = reinterpret_cast<unsigned*>(a.workspace);
         k.tmo = k.flags + RAVE_SPLITK_STATUS_WORD;

@@ -961,7 +961,7 @@ COOP_CASES = [
 ]
 
 
-@pytest.mark.parametrize("precision", ["split16", "f32_ring"])
+@pytest.mark.parametrize("precision", ["split16", "f32_ring", "bf16x3"])
 @pytest.mark.parametrize("case", COOP_CASES, ids=[str(c) for c in COOP_CASES])
 def test_residual_unit_cooperative(N, dev, case, precision):
     """The cooperative fused unit (groups of C/128 workgroups handing act2(h) rows
@@ -975,6 +975,8 @@ def test_residual_unit_cooperative(N, dev, case, precision):
     prec = N.PRECISION[precision]
     if precision == "f32_ring" and T % 4:
         pytest.skip("fp32 ring units need whole 16-byte rows")
+    if precision == "bf16x3" and C == 512 and d > 4:
+        pytest.skip("the bf16x3 unit takes dilations <= 4 at C = 512 (three planes in LDS)")
     rng = np.random.default_rng(C + d + T)
     x = rng.standard_normal((B, C, T)).astype(np.float32)
     w1 = (rng.standard_normal((C, C, 3)) / np.sqrt(3 * C)).astype(np.float32)
