@@ -17,19 +17,21 @@
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}
+ONLY=${2:-all}      # all | bf3 (the f32_bf3 headline's passes only)
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 QUIET="--no-cpu-baseline --pipeline 1"
 timeout -k 10 300 python3 $R/bench.py --steps 10 --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
 echo "bench: $(head -c 400 $OUT/bench.json)"
-timeout -k 10 300 python3 $R/bench.py --steps 10 --warmup 3 --precision auto --no-f32 $QUIET \
-    > "$OUT/bench_auto.json" 2> "$OUT/bench_auto.err"
 gemm_rows() {   # counter CSVs are large; keep the GEMM-family rows only
     head -n 1 "$1" > "$1.gemm"
     grep -E 'conv1d|split_reduce|unit_kernel|unit_split|unit_ring|unit_bf3|stack_split|pqmf|encoder_head|decoder_tail' "$1" >> "$1.gemm" || true
     rm -f "$1"
 }
+if [ "$ONLY" = all ]; then
+timeout -k 10 300 python3 $R/bench.py --steps 10 --warmup 3 --precision auto --no-f32 $QUIET \
+    > "$OUT/bench_auto.json" 2> "$OUT/bench_auto.err"
 # ---------------------------------------------------------------- mixed mode (auto)
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
     python3 $R/bench.py --steps 10 --warmup 3 --precision auto --no-f32 $QUIET > "$OUT/bench_kt.json" 2> "$OUT/bench_kt.err"
@@ -81,6 +83,7 @@ python3 "$R/tools/rocprof_summary.py" --trace "$KT32" --fetch "$FE32" --write "$
 find "$OUT/kt_f32" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats_f32.csv" \;
 gemm_rows "$FE32"
 gemm_rows "$WR32"
+fi
 # ---------------------------------------------------------------- headline: f32_bf3
 timeout -k 10 300 python3 $R/bench.py --steps 10 --warmup 3 --precision f32_bf3 --no-f32 $QUIET \
     > "$OUT/bench_bf3.json" 2> "$OUT/bench_bf3.err"
