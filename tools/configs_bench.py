@@ -170,7 +170,7 @@ def c5(precision, steps, warmup, dev, B=16, Fz=64):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--precision", default="auto", choices=["f32", "f32_tuned", "split16", "auto"])
+    ap.add_argument("--precision", default="auto", choices=["f32", "f32_tuned", "f32_bf3", "split16", "auto"])
     ap.add_argument("--only", default="c3,c4,c5")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)

@@ -57,7 +57,9 @@ def main(path, bench=None):
                "gpu_cycles_per_launch": round(cyc / n),
                "mfma_utilisation": round(busy[f] / (cyc * SIMDS), 4) if cyc else None}
         if flop.get(f):
-            mult = 3.0 if f.endswith("split16") else 16.0   # fp32 MFMA: 1/16 of the f16 rate
+            # f16 MFMA passes per fp32 MAC: split16 3, bf16x3 6 (bf16 rate = f16 rate);
+            # the fp32 MFMA runs at 1/16 of the f16 rate
+            mult = 3.0 if f.endswith("split16") else 6.0 if f.endswith("bf16x3") else 16.0
             rec["expected_busy_per_launch"] = round(flop[f] * mult / FLOP_PER_SIMD_CYCLE)
             rec["busy_over_expected"] = round(busy[f] / n / rec["expected_busy_per_launch"], 3)
         out[f] = rec
