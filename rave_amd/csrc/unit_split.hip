@@ -1235,6 +1235,29 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
         if (C == 128) return go(IC<128>{}, IC<RAVE_F128_WGN>{}, IC<RAVE_F128_MI>{}, IC<1>{}, IC<RAVE_F128_CB>{}, IC<1>{});
         if (C == 256) return go(IC<256>{}, IC<RAVE_F256_WGN>{}, IC<1>{}, IC<1>{}, IC<RAVE_F256_CB>{}, IC<1>{});
     }
+    // bf16x3: its own geometry knobs (A/B builds; the defaults are the split form's)
+#ifndef RAVE_B64_WGN
+#define RAVE_B64_WGN RAVE_U64_WGN
+#endif
+#ifndef RAVE_B64_CB
+#define RAVE_B64_CB RAVE_U64_CB
+#endif
+#ifndef RAVE_B64_MI
+#define RAVE_B64_MI 1
+#endif
+#ifndef RAVE_B128_WGN
+#define RAVE_B128_WGN RAVE_U128_WGN
+#endif
+#ifndef RAVE_B128_CB
+#define RAVE_B128_CB 1
+#endif
+#ifndef RAVE_B128_MI
+#define RAVE_B128_MI 1
+#endif
+    if (ar == 2) {
+        if (C == 64) return go(IC<64>{}, IC<RAVE_B64_WGN>{}, IC<RAVE_B64_MI>{}, IC<1>{}, IC<RAVE_B64_CB>{}, IC<1>{});
+        if (C == 128) return go(IC<128>{}, IC<RAVE_B128_WGN>{}, IC<RAVE_B128_MI>{}, IC<1>{}, IC<RAVE_B128_CB>{}, IC<1>{});
+    }
     if (C == 64) return go(IC<64>{}, IC<RAVE_U64_WGN>{}, IC<1>{}, IC<1>{}, IC<RAVE_U64_CB>{}, IC<1>{});
 #ifndef RAVE_U128_KG
 #define RAVE_U128_KG 1
