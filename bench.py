@@ -188,9 +188,9 @@ DTYPE = {"f32": "fp32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32)",
          "f32_tuned": "fp32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32 on every op; per conv the faster of the "
                       "register-staged kernel and the LDS-DMA ring kernel, launch configurations and "
                       "fused/unfused units autotuned)",
-         "f32_bf3": "fp32 (every op exact-fp32 MFMA or, per fused unit where faster, fp32 on the bf16 matrix "
+         "f32_bf3": "fp32 (per conv / fused unit the faster of exact-fp32 MFMA and fp32 on the bf16 matrix "
                     "cores: operands split exactly into 3 bf16 parts (24 significand bits), 6 of the 9 cross "
-                    "products (the 3 dropped are each < 2^-25 |a b|), fp32 accumulate)",
+                    "products (the 3 dropped are each < 2^-25 |a b|), fp32 accumulate; edges exact-fp32 MFMA)",
          "split16": "fp32 I/O, split-f16 GEMMs (3 f16 MFMA passes hi*hi+hi*lo+lo*hi on ~22-bit operands, "
                     "fp32 accumulate)",
          "auto": "fp32 I/O; per op the faster of exact-fp32 MFMA and split-f16 GEMMs (3 f16 MFMA passes on "
