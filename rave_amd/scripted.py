@@ -102,7 +102,11 @@ class ScriptedRAVE(torch.nn.Module):
         tensors = [torch.from_numpy(np.ascontiguousarray(params[k], np.float32)) for k in params]
         tensors.append(torch.from_numpy(np.ascontiguousarray(hk, np.float32)))
         spk = torch.from_numpy(np.ascontiguousarray(speaker, np.float32).reshape(-1))
-        prec = N.PREC_AUTO if precision == "auto" else N.PRECISION[precision]
+        modes = {"auto": N.PREC_AUTO, "f32_tuned": N.PREC_F32_TUNED, "f32_bf3": N.PREC_F32_BF3,
+                 "f32": N.PREC_F32, "split16": N.PREC_SPLIT16}
+        if precision not in modes:
+            raise ValueError(f"precision must be one of {sorted(modes)}")
+        prec = modes[precision]
         self.engine = torch.classes.rave_amd.Engine(config_ints(cfg), float(cfg.leaky_slope), names, tensors, spk,
                                                     prec, int(block))
         self.hop = int(cfg.hop)

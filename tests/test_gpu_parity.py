@@ -1425,7 +1425,8 @@ def test_stream_conv_shapes_split16_vs_f32(N, dev, capacity):
 
 
 # ------------------------------------------------------------------ TorchScript (nn~) export
-def test_scripted_export_roundtrip_golden(dev, golden, tmp_path):
+@pytest.mark.parametrize("precision", ["f32", "f32_bf3"])
+def test_scripted_export_roundtrip_golden(dev, golden, tmp_path, precision):
     """ScriptedRAVE -> torch.jit.script -> save -> torch.jit.load (what nn~
     does with the .ts, scripts/export.py:618): the loaded module's encode /
     decode match the reference fixtures and its nn~ metadata is intact."""
@@ -1434,7 +1435,8 @@ def test_scripted_export_roundtrip_golden(dev, golden, tmp_path):
     from rave_amd.weights import init_params
     g = golden("v2")
     cfg = rcfg.v2()
-    m = ScriptedRAVE(cfg, init_params(cfg, seed=int(g["seed"])), g["speaker"], hk=_golden_hk(golden))
+    m = ScriptedRAVE(cfg, init_params(cfg, seed=int(g["seed"])), g["speaker"], hk=_golden_hk(golden),
+                     precision=precision)
     path = str(tmp_path / "rave_v2.ts")
     m.export_to_ts(path)
     ts = torch.jit.load(path)

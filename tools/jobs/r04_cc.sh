@@ -9,6 +9,9 @@ mkdir -p "$OUT"
 RAVE_AMD_LIB_VARIANT=exp timeout -k 10 300 python -u -m pytest -q --timeout 120 --timeout-method thread -m gpu \
     tests/test_gpu_parity.py -k "residual_unit and bf16x3" > "$OUT/pytest_exp.log" 2>&1
 rc=$?; tail -1 "$OUT/pytest_exp.log"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -m pytest -q --timeout 120 --timeout-method thread -m gpu \
+    tests/test_gpu_parity.py -k "scripted_export" > "$OUT/pytest_scripted.log" 2>&1
+rc=$?; tail -1 "$OUT/pytest_scripted.log"; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   for v in "" exp; do
     n=${v:-product}
