@@ -72,6 +72,8 @@ FAMILIES = {
                     PEAK_BF3_TFLOPS),
     "stack_split16": ("stack_split_kernel (3 residual units per launch), split-f16 MFMA 32x32x16",
                       PEAK_SPLIT16_TFLOPS),
+    "stack_bf16x3": ("stack_bf3_kernel (3 residual units per launch), fp32 as exact bf16x3 operands, bf16 MFMA "
+                     "32x32x16 (6 per fp32 MAC)", PEAK_BF3_TFLOPS),
     "pqmf_analysis_f32": ("pqmf_analysis_kernel, fp32 MFMA 16x16x4", PEAK_FP32_TFLOPS),
     "pqmf_synthesis_f32": ("pqmf_synthesis_kernel, fp32 MFMA 16x16x4", PEAK_FP32_TFLOPS),
     "pqmf_analysis_split16": ("pqmf_analysis_split_kernel, split-f16 MFMA 16x16x32 (3 per fp32 MAC)",
@@ -92,8 +94,8 @@ FAMILIES = {
 def op_family(kind: int, precision: int) -> str:
     from rave_amd import _native as N
     prec = "split16" if precision == N.PREC_SPLIT16 else "f32"
-    if kind in (N.OP_UNIT, N.OP_CONV) and precision == N.PREC_BF16X3:
-        return ("unit_" if kind == N.OP_UNIT else "conv_") + "bf16x3"
+    if kind in (N.OP_UNIT, N.OP_CONV, N.OP_STACK) and precision == N.PREC_BF16X3:
+        return {N.OP_UNIT: "unit_", N.OP_CONV: "conv_", N.OP_STACK: "stack_"}[kind] + "bf16x3"
     if kind == N.OP_CONV:
         return "conv_" + prec
     if kind == N.OP_UNIT:
@@ -158,30 +160,63 @@ def synth_batch(B, T, seed0):
     return np.stack(xs)[:, None, :].astype(np.float32)
 
 
+def host_info() -> dict:
+    """The host the CPU baseline ran on: CPU model, logical CPUs, 1-minute load."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        load = round(os.getloadavg()[0], 2)
+    except OSError:
+        load = None
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "loadavg_1min": load}
+
+
 def cpu_baseline(cfg, params, spk, B: int, T: int, seconds: float, threads: int):
     """The reference's CPU path -- its module graph on torch fp32 CPU (oneDNN
     convolutions), restated in oracle/torch_cpu.py and pinned to the reference
     fixtures by tests/test_torch_cpu_baseline.py -- on a bounded sample of the
     same workload: the whole (B, 1, T) encode+decode step, repeated for about
-    ``seconds`` of wall time (at least twice) on ``threads`` intra-op threads."""
+    ``seconds`` of wall time (at least twice) on ``threads`` intra-op threads,
+    then the same step on ONE thread (at least twice, about seconds / 2), with
+    the host's CPU model and load before and after, so that box-to-box swings of
+    the shared GPU hosts can be told apart from the code's."""
     import torch
     from oracle.torch_cpu import TorchCPURave
-    torch.set_num_threads(threads)
+    before = host_info()
     m = TorchCPURave(cfg, params, spk)
     x = torch.from_numpy(synth_batch(B, T, 0))
-    m.forward(x)   # warm-up (oneDNN primitive creation)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        m.forward(x)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and n >= 2:
-            break
+
+    def timed(nthreads, secs):
+        torch.set_num_threads(nthreads)
+        m.forward(x)   # warm-up (oneDNN primitive creation)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            m.forward(x)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= secs and n >= 2:
+                return n, el
+
+    n, el = timed(threads, seconds)
+    n1, el1 = timed(1, seconds / 2)
+    after = host_info()
+    torch.set_num_threads(threads)
     return {"value": round(n * B * T / el, 1), "unit": "samples/s", "cores": threads, "kind": "port",
             "ms_per_step": round(1e3 * el / n, 2),
+            "one_thread": {"value": round(n1 * B * T / el1, 1), "ms_per_step": round(1e3 * el1 / n1, 2),
+                           "steps": n1},
+            "host": {"cpu_model": before["cpu_model"], "os_cpu_count": before["os_cpu_count"],
+                     "loadavg_1min_before": before["loadavg_1min"], "loadavg_1min_after": after["loadavg_1min"]},
             "sample": f"{n} x v2 encode+decode of the bench step ({B} x {T} samples): the reference's "
                       f"module graph on torch {torch.__version__} fp32 CPU (oneDNN), {el:.1f} s wall, "
-                      f"torch.set_num_threads({threads})"}
+                      f"torch.set_num_threads({threads}); then {n1} steps on 1 thread ({el1:.1f} s)"}
 
 
 DTYPE = {"f32": "fp32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32)",
@@ -245,6 +280,35 @@ def pipelined(a, cfg, params, spk, precision, model, x, dev):
                     "(one engine instance each); reported beside, not as, the headline"}
 
 
+def timed_region(step, steps: int, warmup: int, world: int, sync, device):
+    """The contract's timed region: ``warmup`` untimed steps, then exactly
+    ``steps`` steps bracketed by sync + barrier on both sides; the elapsed time
+    is the MAX over ranks (all-reduced, so every rank returns it).  Returns
+    (seconds, the last step's output).  ``sync`` is torch.cuda.synchronize on
+    the GPU; the gloo tests pass a no-op and ``device`` cpu
+    (tests/test_distributed_gloo.py)."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    y = None
+    for _ in range(steps):
+        y = step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el, y
+
+
 def run_mode(a, cfg, params, spk, precision, x, dev, world, rank, log_ops):
     """Build the model in one arithmetic mode, time K steps (barrier +
     synchronize on both sides, max over ranks) and, unless --no-profile, the
@@ -286,22 +350,7 @@ def run_mode(a, cfg, params, spk, precision, x, dev, world, rank, log_ops):
             json.dump(eff, fh, indent=0)
     tuning_info = {"source": src, "sha16": tuning_hash(eff), "entries": len(eff),
                    "retimed": (len(eff) - len(tuning)) if tuning is not None else len(eff)}
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        y = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el, y = timed_region(step, a.steps, a.warmup, world, torch.cuda.synchronize, dev)
     if a.timing_only_variant:     # A/B of a timing-only kernel variant: results are not meaningful
         gather_check = {"checked": False, "reason": "timing-only kernel variant"}
     else:

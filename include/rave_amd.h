@@ -44,13 +44,16 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 16
+#define RAVE_ABI_VERSION 17
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 /* The last of those words is reserved: no conv ticket uses it.  A cooperative
  * fused unit (rave_unit_workspace) whose in-launch hand-off gave up sets it to
- * nonzero and leaves it set (sticky); whoever owns the workspace reads it and
- * zeroes it (the model engine does after every plan that holds such a unit). */
+ * nonzero and leaves it set (sticky); a direct caller that owns the workspace
+ * reads it and zeroes it.  The model engine does not use this word: it reads
+ * (and clears) the per-op host-mapped words it passes as rave_unit_args.status,
+ * so in its plans the workspace word may stay set after a reported give-up
+ * (harmless: no conv ticket uses it). */
 #define RAVE_SPLITK_STATUS_WORD (RAVE_SPLITK_TICKETS - 1)
 
 /* ---------------------------------------------------------------- status */
@@ -91,7 +94,9 @@ enum { RAVE_PREC_F32 = 0, RAVE_PREC_SPLIT16 = 1 };
  *                      16-byte aligned input rows):
  *                      every operand split exactly into three bf16 parts
  *                      (v = hi + mid + lo, 24 significand bits, the fp32 exponent
- *                      range: no row scales, no range guard); six
+ *                      range: no row scales, no range guard; hi rounds to nearest, so
+ *                      a finite |v| above ~3.39e38 rounds hi to inf and the output is
+ *                      non-finite -- the only ceiling below FLT_MAX); six
  *                      v_mfma_f32_32x32x16_bf16 products per K-step (all cross
  *                      products but mid*lo, lo*mid, lo*lo: each < 2^-25 |a b|) into one
  *                      fp32 accumulator.  Weights packed with rave_unit_bf3_pack_weight /
@@ -390,11 +395,15 @@ int rave_debug_coop(int64_t spin_limit, int force_giveup);
  * 32-column margin on each side), the stack output is written once.
  * y[:, :, t] = U3(U2(U1(x)))[:, :, t]; weights are rave_unit_split_pack_weight
  * images.  C in {64, 128}; dilation <= 16, pad_left <= 2*dilation.  x and y
- * must not overlap.  Other shapes return RAVE_ERR_UNSUPPORTED. */
+ * must not overlap.  Other shapes return RAVE_ERR_UNSUPPORTED.
+ * precision RAVE_PREC_BF16X3 (ABI 17): fp32 on the bf16 matrix cores (exact
+ * three-way operand split, as the fused unit's), weights rave_unit_bf3_pack_weight
+ * images; every unit's taps within 24 columns (pad_left <= 24, 2*dilation -
+ * pad_left <= 24). */
 #define RAVE_STACK_UNITS 3
 typedef struct rave_stack_args {
     int32_t channels, batch, t_len, act;
-    float leaky_slope; int32_t _pad0;
+    float leaky_slope; int32_t precision;   /* 0 / RAVE_PREC_SPLIT16 or RAVE_PREC_BF16X3 (ABI 17) */
     int32_t dilation[RAVE_STACK_UNITS], pad_left[RAVE_STACK_UNITS];
     const float* x; int64_t x_sb, x_sc;
     float* y;       int64_t y_sb, y_sc;

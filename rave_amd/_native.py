@@ -42,7 +42,7 @@ OP_UNIT = 11
 OP_STACK = 12
 OP_HEAD = 13
 OP_TAIL = 14
-ABI_VERSION = 16
+ABI_VERSION = 17
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 SPLITK_STATUS_WORD = SPLITK_TICKETS - 1   # RAVE_SPLITK_STATUS_WORD: the cooperative unit's give-up word
 
@@ -147,7 +147,7 @@ STACK_UNITS = 3
 
 class StackArgs(C.Structure):
     _fields_ = ([("channels", i32), ("batch", i32), ("t_len", i32), ("act", i32),
-                 ("leaky_slope", f32), ("_pad0", i32)]
+                 ("leaky_slope", f32), ("precision", i32)]
                 + [(f"dilation{u}", i32) for u in range(STACK_UNITS)]
                 + [(f"pad_left{u}", i32) for u in range(STACK_UNITS)]
                 + [("x", vp), ("x_sb", i64), ("x_sc", i64), ("y", vp), ("y_sb", i64), ("y_sc", i64)]

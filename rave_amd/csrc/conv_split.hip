@@ -948,15 +948,21 @@ struct SplitCfg {
 // with few rows and a long time axis (the edge convs, the C = 64 ConvT), so
 // that one round of workgroups covers the layer.  Only
 // the rows marked built are instantiated.  Split-K counts of wide-chunk tiles
-// are in staged chunks.
+// are in staged chunks.  Round 5 (build time): slots 3, 5, 7 and 13, which no
+// committed tuning (profiles/tuning/, every pinned and candidate file of rounds
+// 3-4) ever picked, are no longer built, and the 4-byte window DMA form (XV =
+// false: unaligned input rows, split16 only) is built for the KG = 1 tiles
+// (8-12), the heuristic's set.
 constexpr int kNumSplitTiles = 16;
 [[maybe_unused]] constexpr int kSplitTiles[kNumSplitTiles][7] = {   // BM, BN, WM, KG, WN, VCX, NS
     {64, 64, 32, 4, 64, 2, 3},   {64, 64, 32, 4, 64, 4, 3},   {128, 64, 32, 2, 64, 2, 3},  {32, 64, 32, 4, 64, 2, 3},
     {64, 64, 32, 4, 64, 4, 2},   {64, 128, 32, 2, 64, 2, 3},  {32, 64, 32, 4, 64, 4, 3},   {64, 64, 32, 2, 64, 2, 3},
     {32, 256, 32, 1, 64, 1, 3},  {64, 256, 32, 1, 64, 1, 3},  {128, 64, 32, 1, 64, 1, 3},  {64, 128, 32, 1, 64, 1, 3},
     {256, 64, 32, 1, 64, 1, 3},  {256, 64, 32, 2, 64, 1, 3},  {128, 64, 32, 2, 64, 1, 3},  {64, 128, 32, 2, 64, 1, 3}};
-[[maybe_unused]] constexpr bool kSplitTileBuilt[kNumSplitTiles] = {true,  true,  true,  true,  true,  true,  false, true,
-                                                  true,  true,  true,  true,  true,  true,  true,  true};
+[[maybe_unused]] constexpr bool kSplitTileBuilt[kNumSplitTiles] = {true,  true,  true,  false, true,  false, false, false,
+                                                  true,  true,  true,  true,  true,  false, true,  true};
+// the 4-byte window DMA form (unaligned rows) is built for the KG = 1 tiles only
+[[maybe_unused]] static constexpr bool split_tile_xv0(int ti) { return kSplitTiles[ti][3] == 1; }
 [[maybe_unused]] constexpr int kSplitDefaultTile = 10;
 
 // Calls f(IC<BM>, IC<BN>, IC<WM>, IC<KG>, IC<WN>, IC<VCX>, IC<NS>) for a built tile
@@ -967,15 +973,11 @@ static inline auto with_tile(int ti, Fn&& f) {
         case 0: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<2>{}, IC<3>{});
         case 1: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<4>{}, IC<3>{});
         case 2: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{}, IC<3>{});
-        case 3: return f(IC<32>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<2>{}, IC<3>{});
         case 4: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<4>{}, IC<64>{}, IC<4>{}, IC<2>{});
-        case 5: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{}, IC<3>{});
-        case 7: return f(IC<64>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<2>{}, IC<3>{});
         case 8: return f(IC<32>{}, IC<256>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});
         case 9: return f(IC<64>{}, IC<256>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});
         case 11: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});
         case 12: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});
-        case 13: return f(IC<256>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{}, IC<3>{});
         case 14: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{}, IC<3>{});
         case 15: return f(IC<64>{}, IC<128>{}, IC<32>{}, IC<2>{}, IC<64>{}, IC<1>{}, IC<3>{});
         default: return f(IC<128>{}, IC<64>{}, IC<32>{}, IC<1>{}, IC<64>{}, IC<1>{}, IC<3>{});   // 10
@@ -995,6 +997,9 @@ static int split_launch_xv(ConvKArgs k, hipStream_t st) {
     using G = SGeo<KT, BM, BN, WM, XV, KG, WN, VCX, NS, AR == 2 ? 3 : 2>;
     if constexpr (!G::VALID) {
         set_error("conv1d(split16): tile exceeds LDS or the vmcnt range");
+        return RAVE_ERR_UNSUPPORTED;
+    } else if constexpr (!XV && KG != 1) {
+        set_error("conv1d(split16): unaligned input rows run the KG = 1 tiles only");
         return RAVE_ERR_UNSUPPORTED;
     } else {
         if (k.XW > G::XW_MAX) {
@@ -1186,8 +1191,8 @@ static int split_prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
     return RAVE_OK;
 }
 
-static bool split_tile_ok(int taps, int ti, int M, int split_row, int np) {
-    return ti >= 0 && ti < kNumSplitTiles && split_fits(taps, ti, np) &&
+static bool split_tile_ok(int taps, int ti, int M, int split_row, int np, bool x_vec) {
+    return ti >= 0 && ti < kNumSplitTiles && split_fits(taps, ti, np) && (x_vec || split_tile_xv0(ti)) &&
            (split_row >= M || split_row % kSplitTiles[ti][2] == 0);   // a wave never straddles ConvT groups
 }
 
@@ -1198,7 +1203,7 @@ static int split_resolve(const rave_conv1d_args& a, const ConvKArgs& k, int taps
         return RAVE_OK;
     }
     ConfigCode cc;
-    RAVE_CHECK_ARG(decode_config(a.config, cc) && split_tile_ok(taps, cc.tile, k.M, k.split_row, split_planes(a.precision)) &&
+    RAVE_CHECK_ARG(decode_config(a.config, cc) && split_tile_ok(taps, cc.tile, k.M, k.split_row, split_planes(a.precision), k.x_vec) &&
                        split_count_distinct(cc.S, ceil_div(k.nchunks, kSplitTiles[cc.tile][5])),
                    "conv1d(split16): config not valid for these args (see rave_conv1d_configs)");
     c = {cc.tile, cc.S, cc.sep};
@@ -1216,7 +1221,7 @@ int conv1d_split_configs(const rave_conv1d_args& a, int32_t* cfgs, int max_cfgs)
         ++n;
     };
     for (int ti = 0; ti < kNumSplitTiles; ++ti) {
-        if (!split_tile_ok(taps, ti, k.M, k.split_row, split_planes(a.precision))) continue;
+        if (!split_tile_ok(taps, ti, k.M, k.split_row, split_planes(a.precision), k.x_vec)) continue;
         const int* t = kSplitTiles[ti];
         const int nw = tile_waves(ti);
         const int64_t ntiles = (int64_t)ceil_div(k.M, t[0]) * ceil_div(k.U, t[1]) * k.B;

@@ -409,6 +409,7 @@ struct Model {
     void unit_op(Plan& p, const Node& k3, const Node& k1, int B, int T, const View& src, const View& dst,
                  int x_len = 0, int res_shift = 0);
     rave_stack_args stack_desc(const std::vector<std::pair<const Node*, const Node*>>& run, int B, int T) const;
+    int stack_prec() const;
     bool use_stack(const std::vector<std::pair<const Node*, const Node*>>& run, int B, int T);
     void stack_op(Plan& p, const std::vector<std::pair<const Node*, const Node*>>& run, int B, int T,
                   const View& src, const View& dst);
@@ -516,7 +517,8 @@ rave_conv1d_args Model::conv_desc(const Node& n, int B, int t_in, const View& sr
     return a;
 }
 
-static std::string key_of(std::initializer_list<std::string> parts) {
+template <typename Parts>
+static std::string key_join(const Parts& parts) {
     std::string k;
     for (auto& p : parts) {
         if (!k.empty()) k += '|';
@@ -524,6 +526,8 @@ static std::string key_of(std::initializer_list<std::string> parts) {
     }
     return k;
 }
+static std::string key_of(std::initializer_list<std::string> parts) { return key_join(parts); }
+static std::string key_of(const std::vector<std::string>& parts) { return key_join(parts); }
 
 // (precision, launch config) of one conv op; with autotune every arithmetic and
 // every configuration rave_conv1d_configs lists is timed on scratch tensors of
@@ -533,8 +537,13 @@ static std::string key_of(std::initializer_list<std::string> parts) {
 std::pair<int, int> Model::conv_launch(const Node& n, const rave_conv1d_args& s, bool stream_form, bool timed,
                                        bool allow_ring) {
     auto& pack = stream_form ? w_pack_stream : w_pack;
-    const std::string key = key_of({"conv", n.name, std::to_string(stream_form), std::to_string(s.batch),
-                                    std::to_string(s.t_in)});
+    // (a choice made without the ring / bf16x3 kernels has a key of its own, so a
+    // one-shot plan's ring choice is never replayed on unaligned stream rows and a
+    // stream plan's restricted choice never limits a one-shot plan)
+    std::vector<std::string> kp = {"conv", n.name, std::to_string(stream_form), std::to_string(s.batch),
+                                   std::to_string(s.t_in)};
+    if (!allow_ring) kp.push_back("noring");
+    const std::string key = key_of(kp);
     if (!tuned.count(key) && (precs.size() > 1 || timed || autotune)) {
         const int B = s.batch;
         const int64_t nx = (int64_t)B * n.c_in * s.t_in, ny = (int64_t)B * n.c_out * s.t_out;
@@ -860,7 +869,7 @@ std::map<std::string, std::vector<std::pair<const Node*, const Node*>>> Model::s
         for (auto& pr : run) {
             const Node& k3 = *pr.first;
             ok = ok && k3.c_in == a0.c_in && k3.act == a0.act && k3.bias == a0.bias &&
-                 unit_pack.count({k3.name, RAVE_PREC_SPLIT16}) && !(ad_on && !k3.adain.empty());
+                 unit_pack.count({k3.name, stack_prec()}) && !(ad_on && !k3.adain.empty());
         }
         if (ok) {
             out[a0.name] = run;
@@ -872,9 +881,19 @@ std::map<std::string, std::vector<std::pair<const Node*, const Node*>>> Model::s
     return out;
 }
 
+// the stack's arithmetic: split16 where the model has it (auto / split16),
+// else bf16x3 (f32_bf3); -1: no stack form
+int Model::stack_prec() const {
+    if (std::find(precs.begin(), precs.end(), (int)RAVE_PREC_SPLIT16) != precs.end()) return RAVE_PREC_SPLIT16;
+    if (std::find(precs.begin(), precs.end(), (int)RAVE_PREC_BF16X3) != precs.end()) return RAVE_PREC_BF16X3;
+    return -1;
+}
+
 rave_stack_args Model::stack_desc(const std::vector<std::pair<const Node*, const Node*>>& run, int B, int T) const {
     rave_stack_args s{};
     const Node& a0 = *run[0].first;
+    const int sp = stack_prec();
+    s.precision = sp;
     s.channels = a0.c_in;
     s.batch = B;
     s.t_len = T;
@@ -885,7 +904,7 @@ rave_stack_args Model::stack_desc(const std::vector<std::pair<const Node*, const
         const Node& k1 = *run[u].second;
         s.dilation[u] = k3.dilation;
         s.pad_left[u] = k3.pad_l;
-        s.weight[u] = aptr(unit_pack.at({k3.name, RAVE_PREC_SPLIT16}));
+        s.weight[u] = aptr(unit_pack.at({k3.name, sp}));
         s.bias1[u] = k3.bias ? aptr(bias_off.at(k3.name)) : nullptr;
         s.bias2[u] = k1.bias ? aptr(bias_off.at(k1.name)) : nullptr;
         s.alpha0[u] = k3.act == RAVE_ACT_SNAKE ? aptr(alpha_off.at(k3.alpha)) : nullptr;
@@ -895,9 +914,10 @@ rave_stack_args Model::stack_desc(const std::vector<std::pair<const Node*, const
 }
 
 // one rave_residual_stack launch instead of the units: always in split16-only
-// mode, else when it measures faster than the units' best
+// mode, else when it measures faster than the units' best (auto: split16
+// stacks; f32_bf3: bf16x3 stacks)
 bool Model::use_stack(const std::vector<std::pair<const Node*, const Node*>>& run, int B, int T) {
-    if (std::find(precs.begin(), precs.end(), (int)RAVE_PREC_SPLIT16) == precs.end()) return false;
+    if (stack_prec() < 0) return false;
     if (precs.size() == 1 && !autotune) return true;
     const std::string key = key_of({"stack", run[0].first->name, std::to_string(B), std::to_string(T)});
     if (!tuned.count(key)) {
@@ -936,7 +956,7 @@ void Model::stack_op(Plan& p, const std::vector<std::pair<const Node*, const Nod
     for (size_t u = 0; u < run.size(); ++u) {
         const Node& k3 = *run[u].first;
         const Node& k1 = *run[u].second;
-        View wv = arena_view(unit_pack.at({k3.name, RAVE_PREC_SPLIT16}));
+        View wv = arena_view(unit_pack.at({k3.name, s.precision}));
         View b1 = k3.bias ? arena_view(bias_off.at(k3.name)) : View{};
         View b2 = k1.bias ? arena_view(bias_off.at(k1.name)) : View{};
         View a0 = k3.act == RAVE_ACT_SNAKE ? arena_view(alpha_off.at(k3.alpha)) : View{};
@@ -947,7 +967,7 @@ void Model::stack_op(Plan& p, const std::vector<std::pair<const Node*, const Nod
         p.bind(o, S, S.alpha0[u], k3.act == RAVE_ACT_SNAKE ? &a0 : nullptr);
         p.bind(o, S, S.alpha2[u], k1.act == RAVE_ACT_SNAKE ? &a2 : nullptr);
     }
-    o.prec = RAVE_PREC_SPLIT16;
+    o.prec = s.precision;
     const double C_ = s.channels;
     o.flops = 2.0 * B * T * C_ * C_ * 4 * run.size();
     o.bytes = 4.0 * (2.0 * B * C_ * T + 4.0 * C_ * C_ * run.size());

@@ -16,6 +16,16 @@
 // receptive field of the centre columns stays inside the margin as long as
 // pad_2 + pad_3 <= 32 and (2 d_2 - pad_2) + (2 d_3 - pad_3) <= 32 (host check).
 // Sequence-boundary zero padding: planes hold 0 at columns outside [0, T).
+//
+// bf16x3 form (rave_stack_args.precision = RAVE_PREC_BF16X3; round 5): fp32 on
+// the bf16 matrix cores as unit_split.hip's BF body -- every operand split
+// exactly into hi + mid + lo bf16 (three LDS planes, three weight fragments per
+// K-step from rave_unit_bf3_pack_weight), six v_mfma_f32_32x32x16_bf16 per
+// K-step into one fp32 accumulator, no row scales and no range guard.  Three
+// planes of the split form's 32-row halo do not fit the CU's LDS at C = 64 with
+// 8 centre blocks, so this form keeps kSSBfHalo rows per side: every unit's
+// taps must stay inside it (pad_u <= kSSBfHalo and 2 d_u - pad_u <= kSSBfHalo;
+// host check).  The halo rows only ever feed margin columns.
 #include "common.h"
 
 #include <algorithm>
@@ -27,9 +37,24 @@ typedef _Float16 ss_h4 __attribute__((ext_vector_type(4)));
 typedef float ss_f32x8 __attribute__((ext_vector_type(8)));
 typedef float ss_f32x4 __attribute__((ext_vector_type(4)));
 typedef float ss_f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 ss_b8 __attribute__((ext_vector_type(8)));
+typedef __bf16 ss_b4 __attribute__((ext_vector_type(4)));
+
+// fp32 -> three bf16 parts with v == hi + mid + lo exactly (unit_split.hip)
+template <typename FV, typename BV>
+__device__ __forceinline__ void ss_bf3_split(const FV& v, BV& hi, BV& mid, BV& lo) {
+    hi = __builtin_convertvector(v, BV);
+    const FV r = v - __builtin_convertvector(hi, FV);
+    mid = __builtin_convertvector(r, BV);
+    lo = __builtin_convertvector(r - __builtin_convertvector(mid, FV), BV);
+}
 
 constexpr int kSSUnits = RAVE_STACK_UNITS;
 constexpr unsigned kSSOOB = 0xFFFFFFF0u;
+constexpr int kSSBfHalo = 24;
+#ifndef RAVE_SS_BF_R
+#define RAVE_SS_BF_R 2
+#endif                          // bf16x3: plane rows beyond the extended range, per side
 
 struct SSArgs {
     const float* x; float* y;
@@ -63,21 +88,24 @@ __device__ __forceinline__ float ss_act(float v, float slope, float alpha) {
 }
 
 // C channels (C/32 waves along rows, one 32-row block each); NB centre blocks
-// of 32 columns + 2 margin blocks, CB blocks per wave.
-template <int C, int NB, int CB> struct SSGeo {
+// of 32 columns + 2 margin blocks, CB blocks per wave; NP operand planes (2:
+// split16 hi / lo, 3: bf16x3 hi / lo / mid).
+template <int C, int NB, int CB, int NP = 2> struct SSGeo {
     static constexpr int WGM = C / 32, NBX = NB + 2, WGN = NBX / CB, NW = WGM * WGN, NT = 64 * NW;
     static constexpr int BN = 32 * NB;
-    static constexpr int OFF = 32;                     // plane row of extended column 0
-    static constexpr int XR = NBX * 32 + 64;           // plane rows: extended range + 32 each side
+    static constexpr int OFF = NP == 3 ? kSSBfHalo : 32;   // plane row of extended column 0
+    static constexpr int XR = NBX * 32 + 2 * OFF;      // plane rows: extended range + OFF each side
     static constexpr int PH = C + 8;                   // halves per row (conflict-free b128 reads)
     static constexpr int PLANE = XR * PH;              // halves per plane
     static constexpr int S1 = 3 * C / 16, S2 = C / 16, ST = S1 + S2, CG = C / 16;
-    static constexpr int R = 4;                        // weight ring depth (K-steps); divides ST
+    // weight ring depth (K-steps; divides ST).  bf16x3: 2 (three fragments per
+    // K-step; 10 waves leave 168 VGPRs per lane, and a 4-deep ring spilled)
+    static constexpr int R = NP == 3 ? RAVE_SS_BF_R : 4;
     static constexpr int G8 = C / 8;
     static constexpr int XT = (XR * G8 + NT - 1) / NT; // window staging tasks per thread
     static constexpr int TAB = kSSUnits * 6 * C;       // per unit: rs1 b1 a2 rs2 b2 a0
     // + range-guard votes (16 B) and wave maxima (16 floats)
-    static constexpr int VOTE = 2 * PLANE * 2 + TAB * 4, VRED = VOTE + 16;
+    static constexpr int VOTE = NP * PLANE * 2 + TAB * 4, VRED = VOTE + 16;
     static constexpr int LDS = VRED + 64;
     static_assert(NBX % CB == 0 && ST % R == 0 && NT <= 1024, "geometry");
 };
@@ -87,16 +115,20 @@ template <int C, int NB, int CB> struct SSGeo {
 // hi half) makes the workgroup run the stack again with GUARD = true, whose
 // window / seams / between-unit planes vote and re-stage scaled.  Returns false
 // when the unguarded pass found one (the guarded pass rewrites its stores).
-template <int C, int NB, int CB, bool SNAKE, bool GUARD>
+// BF (bf16x3): one pass, no guard code at all (the operands keep the fp32
+// exponent range).
+template <int C, int NB, int CB, bool SNAKE, bool GUARD, bool BF = false>
 __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
-    using G = SSGeo<C, NB, CB>;
-    constexpr bool GV = GUARD && RAVE_SPLIT_GUARD != 0;
+    constexpr int NPW = BF ? 3 : 2;                    // operand planes / weight fragments per K-step
+    using G = SSGeo<C, NB, CB, NPW>;
+    constexpr bool GV = GUARD && !BF && RAVE_SPLIT_GUARD != 0;
     constexpr int NT = G::NT, PH = G::PH, XR = G::XR, G8 = G::G8, XT = G::XT, R = G::R;
     constexpr int S1 = G::S1, ST = G::ST, CG = G::CG, OFF = G::OFF;
     extern __shared__ __attribute__((aligned(16))) char lds[];
     _Float16* ph = reinterpret_cast<_Float16*>(lds);
     _Float16* pl = ph + G::PLANE;
-    float* tab = reinterpret_cast<float*>(lds + 4 * G::PLANE);
+    _Float16* pm = pl + G::PLANE;                      // BF: the mid plane
+    float* tab = reinterpret_cast<float*>(lds + NPW * G::PLANE * 2);
     unsigned char* vote = reinterpret_cast<unsigned char*>(lds + G::VOTE);
     float* vred = reinterpret_cast<float*>(lds + G::VRED);
 
@@ -140,8 +172,8 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
     }
 
     // ------------------------------------------------------------ weight ring (crosses units)
-    ss_h8 ring[R][2];
-    const unsigned abase = (unsigned)(wm * ST * 2) * 1024u + (unsigned)lane * 16u;
+    ss_h8 ring[R][NPW];
+    const unsigned abase = (unsigned)(wm * ST * NPW) * 1024u + (unsigned)lane * 16u;
     auto wrs_of = [&](int u) __attribute__((always_inline)) {
         const float* w = u == 0 ? a.w[0] : u == 1 ? a.w[1] : a.w[2];
         return ss_rsrc(w, u < kSSUnits ? a.w_bytes : 0);
@@ -152,9 +184,9 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
         const bool here = s < ST;
         const int ss = here ? s : s - ST;
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
+        for (int p = 0; p < NPW; ++p)
             ring[slot][p] = __builtin_bit_cast(ss_h8, __builtin_amdgcn_raw_buffer_load_b128(
-                here ? cur : nxt, abase + (unsigned)((ss * 2 + p) * 1024), 0, 0));
+                here ? cur : nxt, abase + (unsigned)((ss * NPW + p) * 1024), 0, 0));
     };
     {
         const auto w0 = wrs_of(0), w1 = wrs_of(1);
@@ -191,6 +223,16 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
                 const float al = SNAKE ? tab[5 * C + min(g * 8 + v, C - 1)] : 0.f;
                 v8[v] = ok ? ss_act<SNAKE>(rx[i][v], slope, al) * xs : 0.f;
             }
+            if constexpr (BF) {
+                ss_b8 hi, mid, lo;
+                ss_bf3_split(v8, hi, mid, lo);
+                if (e < XR * G8) {
+                    *reinterpret_cast<ss_b8*>(ph + w * PH + g * 8) = hi;
+                    *reinterpret_cast<ss_b8*>(pl + w * PH + g * 8) = lo;
+                    *reinterpret_cast<ss_b8*>(pm + w * PH + g * 8) = mid;
+                }
+                continue;
+            }
             cmax = fmaxf(cmax, absmax8(v8));
             const ss_h8 hi = __builtin_convertvector(v8, ss_h8);
             const ss_h8 lo = __builtin_convertvector((v8 - __builtin_convertvector(hi, ss_f32x8)) * 2048.0f, ss_h8);
@@ -205,22 +247,28 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
     const int col0 = wn * 32 * CB + l32;               // extended column of this lane
     const int mrow0 = 32 * wm + 4 * hh;
     float yv[CB][16];
+    auto load_y = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < CB; ++j) {
-        const int t = ext0 + col0 + 32 * j;
-        const bool ok = t >= 0 && t < a.T;
+        for (int j = 0; j < CB; ++j) {
+            const int t = ext0 + col0 + 32 * j;
+            const bool ok = t >= 0 && t < a.T;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int m = mrow0 + 8 * (r >> 2) + (r & 3);
-            yv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                xrs, ok ? (unsigned)(m * a.x_sc + t) * 4u : kSSOOB, 0, 0));
+            for (int r = 0; r < 16; ++r) {
+                const int m = mrow0 + 8 * (r >> 2) + (r & 3);
+                yv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                    xrs, ok ? (unsigned)(m * a.x_sc + t) * 4u : kSSOOB, 0, 0));
+            }
         }
-    }
+    };
+    // (bf16x3: after the window is staged -- its registers and the window's do
+    // not fit together at 10 waves; y is not read before unit 0's phase 2)
+    if constexpr (!BF) load_y();
     // unit 0's act0(x) window, under the range guard: one pass in the common
     // case, a second one as act0(x) * 2^-sh0 when a wave saw |act0(x)| >= 2^15
     int sh0 = 0;                                       // range-guard shift of the current unit's act0(y) planes
     {
         const float cmax = stage_window(1.0f);
+        if constexpr (BF) load_y();
         if constexpr (GV) vote_cast(vote, wave, cmax);
         __syncthreads();
         if (GV && __builtin_expect(vote_any<G::NW>(vote), 0)) {      // rare: a rolled re-staging loop
@@ -248,15 +296,16 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
         }
     }
 
-    struct BF {
-        ss_h8 h[CB], l[CB];
+    struct BFr {
+        ss_h8 h[CB], l[CB], m[BF ? CB : 1];
     };
-    auto read_b = [&](int row, int ch, BF& f) __attribute__((always_inline)) {
+    auto read_b = [&](int row, int ch, BFr& f) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < CB; ++j) {
             const int off = (row + j * 32) * PH + ch + 8 * hh;
             f.h[j] = *reinterpret_cast<const ss_h8*>(ph + off);
             f.l[j] = *reinterpret_cast<const ss_h8*>(pl + off);
+            if constexpr (BF) f.m[j] = *reinterpret_cast<const ss_h8*>(pm + off);
         }
     };
     ss_f32x16 acc[CB];
@@ -284,6 +333,14 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
                 ss_f32x4 w4;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) w4[e] = ok ? ss_act<SNAKE>(v[j][4 * g + e], slope, al[e]) * xs : 0.f;
+                if constexpr (BF) {
+                    ss_b4 hi, mid, lo;
+                    ss_bf3_split(w4, hi, mid, lo);
+                    *reinterpret_cast<ss_b4*>(ph + (OFF + col0 + 32 * j) * PH + m) = hi;
+                    *reinterpret_cast<ss_b4*>(pl + (OFF + col0 + 32 * j) * PH + m) = lo;
+                    *reinterpret_cast<ss_b4*>(pm + (OFF + col0 + 32 * j) * PH + m) = mid;
+                    continue;
+                }
 #pragma unroll
                 for (int e = 0; e < 4; ++e) cmax = fmaxf(cmax, fabsf(w4[e]));
                 const ss_h4 hv = __builtin_convertvector(w4, ss_h4);
@@ -316,8 +373,26 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
         const float* tu = tab + u * 6 * C;
         const int du = u == 0 ? a.d[0] : u == 1 ? a.d[1] : a.d[2];
         const int pu = u == 0 ? a.pad[0] : u == 1 ? a.pad[1] : a.pad[2];
-        auto step = [&](int s, const BF& f) __attribute__((always_inline)) {
+        auto step = [&](int s, const BFr& f) __attribute__((always_inline)) {
             const ss_h8 ah = ring[s % R][0], al = ring[s % R][1];
+            if constexpr (BF) {
+                const ss_b8 wh = __builtin_bit_cast(ss_b8, ah), wl = __builtin_bit_cast(ss_b8, al),
+                            wmd = __builtin_bit_cast(ss_b8, ring[s % R][NPW - 1]);
+                load_a(s % R, wcur, wnxt, s + R);        // refill (runs on into the next unit)
+                // smallest products first: lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi
+#pragma unroll
+                for (int j = 0; j < CB; ++j) {
+                    const ss_b8 xh = __builtin_bit_cast(ss_b8, f.h[j]), xl = __builtin_bit_cast(ss_b8, f.l[j]),
+                                xm = __builtin_bit_cast(ss_b8, f.m[j]);
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh, acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl, acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wmd, xm, acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wmd, xh, acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xm, acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh, acc[j], 0, 0, 0);
+                }
+                return;
+            }
             const ss_h8 a2 = ah * (_Float16)2048.0f;
             load_a(s % R, wcur, wnxt, s + R);            // refill (runs on into the next unit)
 #pragma unroll
@@ -330,7 +405,7 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
         // phase 1: h = W1 . window (taps at row shifts q*d - pad)
         {
             const int rowb = OFF - pu + col0;
-            BF f[2];
+            BFr f[2];
             read_b(rowb, 8 * 0, f[0]);
 #pragma unroll
             for (int s = 0; s < S1; ++s) {
@@ -363,7 +438,7 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
         }
         // phase 2: y += W2 . h
         {
-            BF f[2];
+            BFr f[2];
             read_b(OFF + col0, 0, f[0]);
 #pragma unroll
             for (int s = S1; s < ST; ++s) {
@@ -393,7 +468,7 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
 
     // unguarded pass: a non-finite centre sum -> run again guarded (flag here,
     // workgroup vote after the stores, which the guarded pass rewrites)
-    constexpr bool CHECK = !GUARD && RAVE_SPLIT_GUARD != 0;
+    constexpr bool CHECK = !GUARD && !BF && RAVE_SPLIT_GUARD != 0;
     bool bad = false;
     if constexpr (CHECK) {
 #pragma unroll
@@ -433,13 +508,18 @@ template <int C, int NB, int CB, bool SNAKE>
 __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_kernel(SSArgs a) {
     if (!stack_split_body<C, NB, CB, SNAKE, RAVE_SPLIT_GUARD == 0>(a)) (void)stack_split_body<C, NB, CB, SNAKE, true>(a);
 }
+template <int C, int NB, int CB, bool SNAKE>
+__global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_bf3_kernel(SSArgs a) {
+    (void)stack_split_body<C, NB, CB, SNAKE, false, true>(a);
+}
 
-template <int C, int NB, int CB>
+template <int C, int NB, int CB, bool BF = false>
 static int ss_launch(const SSArgs& k0, int B, bool snake, hipStream_t st) {
-    using G = SSGeo<C, NB, CB>;
+    using G = SSGeo<C, NB, CB, BF ? 3 : 2>;
     SSArgs k = k0;
     k.ntiles = ceil_div(k.T, G::BN);
-    auto kern = snake ? stack_split_kernel<C, NB, CB, true> : stack_split_kernel<C, NB, CB, false>;
+    void (*kern)(SSArgs) = BF ? (snake ? stack_bf3_kernel<C, NB, CB, true> : stack_bf3_kernel<C, NB, CB, false>)
+                              : (snake ? stack_split_kernel<C, NB, CB, true> : stack_split_kernel<C, NB, CB, false>);
     static bool attr[2] = {false, false};
     if (G::LDS > 65536 && !attr[snake]) {
         RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -448,7 +528,7 @@ static int ss_launch(const SSArgs& k0, int B, bool snake, hipStream_t st) {
     }
     static_assert(G::LDS <= 160 * 1024, "LDS budget");
     launch(kern, dim3(k.ntiles * B), dim3(G::NT), (uint32_t)G::LDS, st, k);
-    return launch_status("stack_split_kernel");
+    return launch_status(BF ? "stack_bf3_kernel" : "stack_split_kernel");
 }
 
 }  // namespace rave
@@ -469,6 +549,9 @@ extern "C" int rave_residual_stack(const rave_stack_args* p, void* stream) {
                    "residual_stack: unknown activation");
     const bool snake = p->act == RAVE_ACT_SNAKE;
     const bool has_bias = p->bias1[0] != nullptr;
+    RAVE_CHECK_ARG(p->precision == 0 || p->precision == RAVE_PREC_SPLIT16 || p->precision == RAVE_PREC_BF16X3,
+                   "residual_stack: precision must be RAVE_PREC_SPLIT16 or RAVE_PREC_BF16X3");
+    const bool bf = p->precision == RAVE_PREC_BF16X3;
     int reach_l = 0, reach_r = 0;
     for (int u = 0; u < kSSUnits; ++u) {
         const int d = p->dilation[u], pl = p->pad_left[u];
@@ -481,6 +564,10 @@ extern "C" int rave_residual_stack(const rave_stack_args* p, void* stream) {
             reach_l += pl;
             reach_r += 2 * d - pl;
         }
+        if (bf && (pl > kSSBfHalo || 2 * d - pl > kSSBfHalo)) {
+            set_error("residual_stack(bf16x3): a unit's taps reach past the 24-row plane halo (run the units separately)");
+            return RAVE_ERR_UNSUPPORTED;
+        }
     }
     if (reach_l > 32 || reach_r > 32) {
         set_error("residual_stack: units 2..3 reach past the 32-column margin (run the units separately)");
@@ -491,7 +578,8 @@ extern "C" int rave_residual_stack(const rave_stack_args* p, void* stream) {
     RAVE_CHECK_ARG(xb < (1ll << 31) && yb < (1ll << 31), "residual_stack: tensors beyond 2 GiB per item");
     SSArgs k{};
     k.x = p->x; k.y = p->y;
-    const int64_t frag = (int64_t)(C / 32) * (4 * C / 16) * 2 * 256;   // rave_unit_split_pack_weight
+    // rave_unit_split_pack_weight / rave_unit_bf3_pack_weight (fragments, then rs1, rs2)
+    const int64_t frag = (int64_t)(C / 32) * (4 * C / 16) * (bf ? 3 : 2) * 256;
     for (int u = 0; u < kSSUnits; ++u) {
         k.w[u] = p->weight[u];
         k.rs1[u] = p->weight[u] + frag;
@@ -523,6 +611,20 @@ extern "C" int rave_residual_stack(const rave_stack_args* p, void* stream) {
 #define RAVE_S128_NB 2
 #define RAVE_S128_CB 2
 #endif
+    // bf16x3 (three planes, 24-row halo): C = 64 keeps 8 centre blocks (146 KB of
+    // LDS); C = 128 fits 2 (152 KB)
+#ifndef RAVE_B64S_NB
+#define RAVE_B64S_NB 8
+#define RAVE_B64S_CB 2
+#endif
+#ifndef RAVE_B128S_NB
+#define RAVE_B128S_NB 2
+#define RAVE_B128S_CB 2
+#endif
+    if (bf) {
+        if (C == 64) return ss_launch<64, RAVE_B64S_NB, RAVE_B64S_CB, true>(k, p->batch, snake, st);
+        return ss_launch<128, RAVE_B128S_NB, RAVE_B128S_CB, true>(k, p->batch, snake, st);
+    }
     if (C == 64) return ss_launch<64, RAVE_S64_NB, RAVE_S64_CB>(k, p->batch, snake, st);
     return ss_launch<128, RAVE_S128_NB, RAVE_S128_CB>(k, p->batch, snake, st);
 }

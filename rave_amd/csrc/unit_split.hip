@@ -175,7 +175,9 @@ template <int C, int WGN, int MI, int KG = 1, int CB = 2, int RB = 1, int NP = 2
 // eight v_mfma_f32_32x32x2_f32 per 16-deep K-step (K-slot (s, half h) =
 // channel 8h + s), no range guard, row scales 1.
 //
-// BF (RAVE_PREC_BF16X3, RB == 1 only): fp32 on the bf16 matrix cores.  Every
+// BF (RAVE_PREC_BF16X3, both forms: one workgroup per slab, and the cooperative
+// groups at C = 256 / 512 whose exchanged act2(h) rows stay fp32 and are split by
+// each member into its own planes): fp32 on the bf16 matrix cores.  Every
 // operand v is split exactly as hi + mid + lo (bf16 each: 24 significand bits,
 // the fp32 exponent range, so no row scales and no range guard); three planes
 // (hi, lo, mid) in LDS and three weight fragments per K-step; six
@@ -909,6 +911,17 @@ __global__ __launch_bounds__(64 * (C / (32 * MI * RB)) * WGN * KG) void unit_bf3
     (void)unit_split_body<C, WGN, MI, KG, CB, SNAKE, 2, RB, false>(a);
 }
 
+// cooperative launches of this process that can run at once: its hardware
+// queues (GPU_MAX_HW_QUEUES; HIP's default 4)
+static int coop_max_queues() {
+    static const int q = [] {
+        const char* e = std::getenv("GPU_MAX_HW_QUEUES");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 ? v : 4;
+    }();
+    return q;
+}
+
 // ar: 0 split16, 1 exact fp32 (ring), 2 bf16x3
 template <int C, int WGN, int MI, int KG, int CB, int RB = 1>
 static int us_launch(USArgs k, int B, bool snake, int ar, hipStream_t st) {
@@ -944,9 +957,18 @@ static int us_launch(USArgs k, int B, bool snake, int ar, hipStream_t st) {
     }
     int grid = k.ntiles * B;
     if constexpr (RB > 1) {
-        // forward progress needs a whole group resident on one XCD at once:
-        // RB workgroups of this geometry must fit that XCD's CUs (else the
-        // caller runs the one-workgroup form)
+        // Forward progress needs a whole group resident on one XCD at once.  A
+        // launch's workgroups reach an XCD in order and a group's members are
+        // consecutive there, so at any moment a launch holds at most ONE partial
+        // group per XCD (RB - 1 slots).  With Q cooperative launches of this
+        // process in flight together (at most its hardware queues,
+        // GPU_MAX_HW_QUEUES, 4 by default: engines on several streams, bench's
+        // pipelined leg), the partial groups hold at most Q (RB - 1) of the XCD's
+        // workgroup slots; if the XCD has room for RB more, some group is whole,
+        // finishes and frees slots, and so on.  Kernels of other kinds only
+        // delay (they finish unconditionally).  So the cooperative form runs
+        // only where slots per XCD >= Q (RB - 1) + RB; else the caller runs the
+        // one-workgroup form.  (Other processes sharing the GPU are not counted.)
         static int fits[6] = {-1, -1, -1, -1, -1, -1};
         int& f = fits[2 * ar + snake];
         if (f < 0) {
@@ -955,7 +977,7 @@ static int us_launch(USArgs k, int B, bool snake, int ar, hipStream_t st) {
                                                                         G::NT, lds));
             RAVE_CHECK_HIP(hipGetDevice(&dev));
             RAVE_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            f = (int64_t)per_cu * (cus / kXcds) >= RB ? 1 : 0;
+            f = (int64_t)per_cu * (cus / kXcds) >= (int64_t)coop_max_queues() * (RB - 1) + RB ? 1 : 0;
         }
         if (!f) return kCoopNoFit;
         k.ngroups = grid;

@@ -152,3 +152,62 @@ def test_shard_bounds_cover_batch():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(size - 1))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def _bench_worker(rank, size, port, x_all, sizes, q):
+    """bench.py's own timed region (bench.timed_region: warmup, barrier +
+    sync, K steps, MAX over ranks) around a codes-mode ShardedRunner step with
+    unequal shards fixed up front, then the exchange self-check."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    try:
+        import time
+        from bench import timed_region
+        from rave_amd.distributed import ShardedRunner
+        lo = sum(sizes[:rank])
+        x = x_all[lo:lo + sizes[rank]]
+        runner = ShardedRunner(_OracleCodesModel(), mode="codes", shard_sizes=sizes)
+        held = []
+
+        def step():
+            if rank == 1:
+                time.sleep(0.05)                  # the slow rank sets the job's time
+            idx_all, y = runner.step(x)
+            held.append(idx_all)
+            return y
+
+        el, y = timed_region(step, 2, 1, size, lambda: None, torch.device("cpu"))
+        chk = runner.verify(x)
+        q.put((rank, el, held[-1].numpy(), y.numpy(), chk))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_timed_region_codes_unequal_shards():
+    """C4's codes mode at world size 2 with shards of 2 and 1 clips, through
+    bench.py's timed region: every rank reports the same (max) elapsed time,
+    which covers the slow rank's two timed steps; every rank holds the whole
+    batch's indices; each decodes its own rows; the exchange check passes."""
+    rng = np.random.default_rng(3)
+    x_all = torch.from_numpy((0.2 * rng.standard_normal((3, 1, 2048))).astype(np.float32))
+    sizes = [2, 1]
+    m = _OracleCodesModel()
+    idx_ref = m.encode_codes(x_all)
+    y_ref = m.decode_codes(idx_ref)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, x_all, sizes, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    els = [r[1] for r in res]
+    assert els[0] == els[1] and els[0] >= 2 * 0.05
+    for rank, _, idx_all, y, chk in res:
+        lo = sum(sizes[:rank])
+        np.testing.assert_array_equal(idx_all, idx_ref.numpy())
+        np.testing.assert_allclose(y, y_ref.numpy()[lo:lo + sizes[rank]], atol=1e-6)
+        assert chk["ok"] and chk["rows"] == 3 and chk["ranks"] == 2

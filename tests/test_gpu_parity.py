@@ -480,7 +480,7 @@ def test_v2_full_clip_vs_oracle(dev, precision):
     assert ey < TOL
 
 
-@pytest.mark.parametrize("precision", ["f32", "auto"])
+@pytest.mark.parametrize("precision", ["f32", "auto", "f32_bf3"])
 def test_discrete_codes_c4_shard_vs_oracle(dev, precision):
     """BASELINE config 4's per-GPU shard (8 x 65536 of the B=64 batch): the
     whole encode_codes -> decode_codes path, two clips checked against the
@@ -516,7 +516,7 @@ def test_discrete_codes_c4_shard_vs_oracle(dev, precision):
         assert ey < TOL
 
 
-@pytest.mark.parametrize("precision", ["f32", "auto"])
+@pytest.mark.parametrize("precision", ["f32", "auto", "f32_bf3"])
 def test_batch_independence_and_determinism(dev, precision):
     """At BASELINE config 2 size (16 x 65536), in the bench's precision mode too:
     each clip of the batch equals the same clip run alone (no cross-sample
@@ -610,7 +610,7 @@ def test_streaming_graph_equals_eager(dev):
         assert torch.equal(zg, ze) and torch.equal(yg, ye), i
 
 
-@pytest.mark.parametrize("precision", ["f32", "auto"])
+@pytest.mark.parametrize("precision", ["f32", "auto", "f32_bf3"])
 @pytest.mark.parametrize("graph", [True, False])
 def test_stream_v3_noise_adain_golden(dev, golden, precision, graph):
     """Streaming a causal v3 model with the noise synthesizer and AdaIN against
@@ -675,7 +675,7 @@ def test_engine_forward_and_device_noise(dev):
 
 
 # ------------------------------------------------------------------ v3 noise / AdaIN (BASELINE config 5)
-@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("precision", PRECISIONS + ["f32_bf3"])
 @pytest.mark.parametrize("name,capacity", [("v3_noise", None), ("v3_noise_small_layers", 8)])
 def test_v3_noise_golden(dev, golden, name, capacity, precision):
     """Snake + NoiseGeneratorV2 decode with the reference's injected uniform noise."""
@@ -722,7 +722,8 @@ def test_noise_synth_kernel_vs_oracle(dev, N):
     assert maxabs(got, ref) < 2e-6 * max(1.0, float(np.abs(ref).max()))
 
 
-def test_v3_noise_decode_c5_shard_vs_oracle(dev):
+@pytest.mark.parametrize("precision", ["f32", "f32_bf3"])
+def test_v3_noise_decode_c5_shard_vs_oracle(dev, precision):
     """BASELINE config 5 per-GPU shard geometry (16 x 64 latent frames) on two
     samples against the oracle, plus device-drawn noise statistics."""
     from oracle.rave_oracle import Oracle
@@ -731,7 +732,7 @@ def test_v3_noise_decode_c5_shard_vs_oracle(dev):
     from rave_amd.weights import init_params, init_speaker
     cfg = rcfg.v3_noise()
     params, spk = init_params(cfg, 3), init_speaker(cfg, 3)
-    m = RAVE(cfg, params, spk, device=dev)
+    m = RAVE(cfg, params, spk, device=dev, precision=precision)
     rng = np.random.default_rng(9)
     z = rng.standard_normal((16, cfg.dec_in, 64)).astype(np.float32)
     u = rng.uniform(0, 1, m.noise_shape(16, 64)).astype(np.float32)
@@ -745,7 +746,7 @@ def test_v3_noise_decode_c5_shard_vs_oracle(dev):
     assert torch.isfinite(y_rand).all() and float(d.max()) < 0.05   # noise is a small additive term
 
 
-@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("precision", PRECISIONS + ["f32_bf3"])
 def test_adain_style_transfer_golden(dev, golden, precision):
     """learn_y -> learn_x -> transfer -> learn_x(bs=1) against the reference's
     AdaIN run, including the device-resident buffers and counters."""
@@ -1146,16 +1147,20 @@ STACK_CASES = [
 ]
 
 
+@pytest.mark.parametrize("precision", ["split16", "bf16x3"])
 @pytest.mark.parametrize("case", STACK_CASES, ids=[str(c) for c in STACK_CASES])
-def test_residual_stack_kernel(N, dev, case):
+def test_residual_stack_kernel(N, dev, case, precision):
     """rave_residual_stack == the three units one after the other (oracle,
-    float64, and the split16 unit kernel run three times)."""
+    float64, and the unit kernel of the same arithmetic run three times): the
+    split16 stack, and the bf16x3 one the f32_bf3 plans run (round 5)."""
     from oracle.rave_oracle import conv1d, leaky_relu, snake
     C, dils, act, causal, B, T = case
+    prec = N.PRECISION[precision]
     rng = np.random.default_rng(C + sum(dils) + T)
     x = rng.standard_normal((B, C, T)).astype(np.float32)
     xd = torch.from_numpy(x).to(dev)
-    units, args = [], N.StackArgs(channels=C, batch=B, t_len=T, act=N.ACT[act], leaky_slope=0.2)
+    units, args = [], N.StackArgs(channels=C, batch=B, t_len=T, act=N.ACT[act], leaky_slope=0.2,
+                                  precision=prec)
     keep = []
     for u, d in enumerate(dils):
         w1 = (rng.standard_normal((C, C, 3)) / np.sqrt(3 * C)).astype(np.float32)
@@ -1166,7 +1171,7 @@ def test_residual_stack_kernel(N, dev, case):
         a2 = (1 + 0.3 * rng.standard_normal(C)).astype(np.float32)
         pad = (2 * d, 0) if causal else (d, d)
         units.append((w1, w2, b1, b2, a0, a2, d, pad))
-        tens = [torch.from_numpy(N.pack_unit_weight(w1, w2, C, precision=N.PREC_SPLIT16)).to(dev)] + \
+        tens = [torch.from_numpy(N.pack_unit_weight(w1, w2, C, precision=prec)).to(dev)] + \
                [torch.from_numpy(v).to(dev) for v in (b1, b2, a0, a2)]
         keep += tens
         setattr(args, f"dilation{u}", d)
@@ -1183,7 +1188,7 @@ def test_residual_stack_kernel(N, dev, case):
     for u, (w1, w2, b1, b2, a0, a2, d, pad) in enumerate(units):
         nxt = torch.empty_like(xd)
         ua = N.UnitArgs(channels=C, batch=B, t_len=T, dilation=d, pad_left=pad[0], act=N.ACT[act],
-                        leaky_slope=0.2, precision=N.PREC_SPLIT16, x=cur.data_ptr(), x_sb=C * T, x_sc=T,
+                        leaky_slope=0.2, precision=prec, x=cur.data_ptr(), x_sb=C * T, x_sc=T,
                         y=nxt.data_ptr(), y_sb=C * T, y_sc=T, weight=getattr(args, f"weight{u}"),
                         bias1=getattr(args, f"bias1{u}"), bias2=getattr(args, f"bias2{u}"),
                         alpha0=getattr(args, f"alpha0{u}"), alpha2=getattr(args, f"alpha2{u}"))
@@ -1200,6 +1205,28 @@ def test_residual_stack_kernel(N, dev, case):
     assert np.isfinite(got).all()
     assert maxabs(got, seq) <= 1e-5 * max(1.0, np.abs(seq).max())
     assert maxabs(got, ref) <= 2e-5 * max(1.0, np.abs(ref).max())
+    if precision == "bf16x3":      # fp32-class: the exact three-way split, no ~22-bit operands
+        print(f"\n[parity] stack bf16x3 {case}: rel err vs float64 {maxabs(got, ref) / np.abs(ref).max():.2e}")
+        assert maxabs(got, ref) <= 2e-6 * max(1.0, np.abs(ref).max())
+
+
+def test_residual_stack_bf16x3_halo_limit(N, dev):
+    """The bf16x3 stack keeps a 24-row plane halo: a unit whose taps reach
+    further is refused (RAVE_ERR_UNSUPPORTED), never computed wrong."""
+    C, B, T = 64, 1, 256
+    x = torch.zeros(B, C, T, device=dev)
+    y = torch.zeros_like(x)
+    w = torch.from_numpy(N.pack_unit_weight(np.zeros((C, C, 3), np.float32), np.zeros((C, C, 1), np.float32), C,
+                                            precision=N.PREC_BF16X3)).to(dev)
+    args = N.StackArgs(channels=C, batch=B, t_len=T, act=N.ACT["leaky"], leaky_slope=0.2,
+                       precision=N.PREC_BF16X3, x=x.data_ptr(), x_sb=C * T, x_sc=T, y=y.data_ptr(),
+                       y_sb=C * T, y_sc=T)
+    for u, d in enumerate((1, 3, 13)):
+        setattr(args, f"dilation{u}", d)
+        setattr(args, f"pad_left{u}", 2 * d)          # causal: 26 > 24 at d = 13
+        setattr(args, f"weight{u}", w.data_ptr())
+    rc = N.lib.rave_residual_stack(C_.byref(args), C_.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == N.RAVE_ERR_UNSUPPORTED
 
 
 # ------------------------------------------------------------------ streaming history shift

@@ -93,7 +93,7 @@ def test_noncausal_streaming_matches_oneshot_shifted(dev):
     assert float((ys[..., d + 1 + warm:] - y1[..., warm:y1.shape[-1] - d - 1]).abs().max()) > 1e-3
 
 
-@pytest.mark.parametrize("precision", ["f32", "auto"])
+@pytest.mark.parametrize("precision", ["f32", "auto", "f32_bf3"])
 def test_noncausal_v3_noise_adain_streaming_golden(dev, golden, precision):
     """Centred v3 + noise + AdaIN streamed against the reference's cached
     mode: the noise branch (padding (r, 0) convs, no AlignBranches) and the
@@ -129,7 +129,7 @@ def test_noncausal_v3_noise_adain_streaming_golden(dev, golden, precision):
 
 
 # ------------------------------------------------------------------ discrete (RVQ) streaming
-@pytest.mark.parametrize("precision", ["f32", "auto"])
+@pytest.mark.parametrize("precision", ["f32", "auto", "f32_bf3"])
 def test_discrete_streaming_golden(dev, golden, precision):
     """DiscreteScriptedRAVE streamed (scripts/export.py:503-517 under
     cc.use_cached_conv(True)): per-block indices equal the reference's outside

@@ -107,25 +107,11 @@ def c3(precision, blocks, warmup, dev):
 
 
 def sharded_steps(fn, steps, warmup):
-    """bench.py's contract: barrier + synchronize around exactly ``steps``
-    steps, the max over ranks."""
+    """bench.py's contract (bench.timed_region, the same code): barrier +
+    synchronize around exactly ``steps`` steps, the max over ranks."""
+    from bench import timed_region
     rank, size = world()
-    for _ in range(warmup):
-        fn()
-    torch.cuda.synchronize()
-    if size > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        fn()
-    torch.cuda.synchronize()
-    if size > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if size > 1:
-        t = torch.tensor([el], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el, _ = timed_region(fn, steps, warmup, size, torch.cuda.synchronize, torch.device("cuda"))
     return el / steps
 
 

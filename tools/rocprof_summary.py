@@ -33,6 +33,7 @@ FAMILIES = {
     "conv_bf16x3": (("conv1d_bf3_kernel",), ()),
     "unit_bf16x3": (("unit_bf3_kernel",), ()),
     "stack_split16": (("stack_split_kernel",), ()),
+    "stack_bf16x3": (("stack_bf3_kernel",), ()),
     "pqmf_analysis_f32": (("pqmf_analysis_kernel",), ()),
     "pqmf_synthesis_f32": (("pqmf_synthesis_kernel",), ()),
     "pqmf_analysis_split16": (("pqmf_analysis_split_kernel",), ()),
