@@ -48,6 +48,8 @@ typedef _Float16 e_h4 __attribute__((ext_vector_type(4)));
 typedef float e_f32x4 __attribute__((ext_vector_type(4)));
 typedef float e_f32x16 __attribute__((ext_vector_type(16)));
 typedef float e_f32x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 e_b8 __attribute__((ext_vector_type(8)));
+typedef __bf16 e_b4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ e_f32x8 e_ld8(const float* p) {    // 8 floats (two b128 LDS reads)
     const e_f32x4 u = *reinterpret_cast<const e_f32x4*>(p), v = *reinterpret_cast<const e_f32x4*>(p + 4);
@@ -96,12 +98,14 @@ __device__ __forceinline__ void e_split(float v, _Float16& hi, _Float16& lo) {
 
 // split-f16 conv weight image (rave_conv1d_split_pack_weight, 7 taps, stride 1):
 // [chunk of 16 in-channels][32-row block mb][tap][hi|lo][64 lanes][8 halves],
-// then one float row scale 2^-(e_m + 11) per padded row
+// then one float row scale 2^-(e_m + 11) per padded row.  bf16x3
+// (rave_conv1d_bf3_pack_weight): three planes per tap, [hi|lo|mid], scales 1.
 struct EdgeW {
     __amdgpu_buffer_rsrc_t rs;
     int mb_count;                                   // Mpad / 32
+    int np = 2;                                     // planes per tap
     __device__ unsigned off(int chunk, int mb, int tap, int plane, int lane) const {
-        return (unsigned)((((chunk * mb_count + mb) * kEdgeK7 + tap) * 2 + plane) * 1024 + lane * 16);
+        return (unsigned)((((chunk * mb_count + mb) * kEdgeK7 + tap) * np + plane) * 1024 + lane * 16);
     }
     __device__ e_h8 frag(int chunk, int mb, int tap, int plane, int lane) const {
         return __builtin_bit_cast(e_h8, __builtin_amdgcn_raw_buffer_load_b128(rs, off(chunk, mb, tap, plane, lane), 0, 0));
@@ -464,21 +468,35 @@ constexpr int kTSP = 24;                            // halves per synthesis row
 constexpr int kTPlane = 2 * kTXR * kTXP;            // halves of the two act(x) planes
 static_assert(2 * kTSW * kTSP <= kTPlane, "synthesis planes reuse the act(x) planes");
 constexpr int kTailLds = (2 * 16 * kEdgeFP + kTPlane) * 2 + 2 * kEdgeWaves * 4 + 16;
+// bf16x3 (AR = 2): three act(x) planes from byte 0, no filter in LDS during
+// the conv; after it (planes dead) the fp32 synthesis planes at 0, the K-split
+// partial tiles after them, and the fp32 filter at kTailBfFilt
+constexpr int kTailBfX = 3 * kTXR * kTXP * 2;                  // bytes of the three act(x) planes
+constexpr int kTailBfFilt = 61440;
+constexpr int kTailLdsBf = kTailBfX + 2 * kEdgeWaves * 4 + 16;
+static_assert(kTailBfFilt >= 2 * kTSW * kTSP * 2 + kEdgeWaves * 16 * 64 * 4 &&
+              kTailBfFilt + 16 * kEdgeFP * 4 <= kTailBfX, "bf16x3 tail LDS reuse");
 
-template <bool SNAKE, bool AM, bool F32>
+// AR: 0 split-f16, 1 exact fp32, 2 bf16x3 conv (fp32 on the bf16 matrix cores,
+// exact three-way operand split, six bf16 MFMAs per 16-deep K-step) with the
+// exact-fp32 synthesis
+template <bool SNAKE, bool AM, int AR>
 __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a, EdgeGeo geo) {
+    constexpr bool F32 = AR == 1, BF = AR == 2, FS = AR != 0;   // FS: fp32 synthesis stage
     const int tiles = geo.tiles;
     extern __shared__ __attribute__((aligned(16))) char e_smem[];
     _Float16* fh = reinterpret_cast<_Float16*>(e_smem);          // [16][kEdgeFP] synthesis filter
     _Float16* fl = fh + 16 * kEdgeFP;
-    _Float16* xh = fl + 16 * kEdgeFP;                              // [kTXR][kTXP] act(x)
+    _Float16* xh = BF ? fh : fl + 16 * kEdgeFP;                    // [kTXR][kTXP] act(x)
     _Float16* xl = xh + kTXR * kTXP;
+    _Float16* xm = xl + kTXR * kTXP;                               // BF: the mid plane
     _Float16* sh = xh;                                             // [kTSW][kTSP] (after the conv)
     _Float16* sl = xh + kTSW * kTSP;
-    float* red = reinterpret_cast<float*>(xh + kTPlane);
-    float* ff = reinterpret_cast<float*>(fh);                     // F32: [16][kEdgeFP]
+    float* red = reinterpret_cast<float*>(BF ? reinterpret_cast<char*>(e_smem) + kTailBfX
+                                             : reinterpret_cast<char*>(xh + kTPlane));
+    float* ff = reinterpret_cast<float*>(BF ? e_smem + kTailBfFilt : e_smem);   // FS: [16][kEdgeFP]
     float* xf = reinterpret_cast<float*>(xh);                     // F32: [kTXR][kTXP] act(x)
-    float* sf = xf;                                                // F32: [kTSW][kTSP] (after the conv)
+    float* sf = xf;                                                // FS: [kTSW][kTSP] (after the conv)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nmain = tiles * a.batch;
@@ -492,17 +510,29 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
 
     unsigned char* vote = reinterpret_cast<unsigned char*>(red + 2 * kEdgeWaves);
     // ---- the conv's first weight fragments (no data dependence): issued first
-    const EdgeW W{e_rsrc(a.weight, (int64_t)geo.w_bytes), geo.w_mb};
+    constexpr int NPW = BF ? 3 : 2;
+    const EdgeW W{e_rsrc(a.weight, (int64_t)geo.w_bytes), geo.w_mb, NPW};
     constexpr int KS = (kTC / 16) * kEdgeK7;          // 28 K-steps
     constexpr int RING = 4;
-    e_h8 wr[RING][2];
+    e_h8 wr[RING][NPW];
 #pragma unroll
     for (int s = 0; s < RING; ++s)
 #pragma unroll
-        for (int pl = 0; pl < 2; ++pl) wr[s][pl] = W.frag(s / kEdgeK7, 0, s % kEdgeK7, pl, lane);
+        for (int pl = 0; pl < NPW; ++pl) wr[s][pl] = W.frag(s / kEdgeK7, 0, s % kEdgeK7, pl, lane);
     // ---- synthesis filter image -> LDS (16-byte copies); act(x) in 4-channel
-    // groups (coalesced along time), split optimistically with a range vote
-    {
+    // groups (coalesced along time), split optimistically with a range vote.
+    // BF: the fp32 filter is held in registers through the conv (its LDS is
+    // the act(x) planes' until then) and stored after it
+    constexpr int FQ = (kEdgeFilterHalves / 8 + kEdgeNT - 1) / kEdgeNT;   // 16-byte pieces per thread
+    e_h8 fq[BF ? FQ : 1];
+    if constexpr (BF) {
+        const e_h8* src = reinterpret_cast<const e_h8*>(a.filter);
+#pragma unroll
+        for (int i = 0; i < FQ; ++i) {
+            const int k = tid + i * kEdgeNT;
+            if (k < kEdgeFilterHalves / 8) fq[i] = src[k];
+        }
+    } else {
         const e_h8* src = reinterpret_cast<const e_h8*>(a.filter);
         e_h8* dst = reinterpret_cast<e_h8*>(fh);
         for (int i = tid; i < kEdgeFilterHalves / 8; i += kEdgeNT) dst[i] = src[i];
@@ -546,6 +576,16 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
                     *reinterpret_cast<e_f32x4*>(xf + w * kTXP + 4 * cg) = v;
                     continue;
                 }
+                if constexpr (BF) {
+                    const e_b4 hi = __builtin_convertvector(v, e_b4);
+                    const e_f32x4 r = v - __builtin_convertvector(hi, e_f32x4);
+                    const e_b4 mid = __builtin_convertvector(r, e_b4);
+                    const e_b4 lo = __builtin_convertvector(r - __builtin_convertvector(mid, e_f32x4), e_b4);
+                    *reinterpret_cast<e_b4*>(xh + w * kTXP + 4 * cg) = hi;
+                    *reinterpret_cast<e_b4*>(xl + w * kTXP + 4 * cg) = lo;
+                    *reinterpret_cast<e_b4*>(xm + w * kTXP + 4 * cg) = mid;
+                    continue;
+                }
                 const e_h4 hi = __builtin_convertvector(v, e_h4);
                 const e_h4 lo = __builtin_convertvector((v - __builtin_convertvector(hi, e_f32x4)) * 2048.0f, e_h4);
                 *reinterpret_cast<e_h4*>(xh + w * kTXP + 4 * cg) = hi;
@@ -554,10 +594,10 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
         }
     };
     put_x(1.f);
-    if constexpr (!F32) vote_cast(vote, wave, xmax);
+    if constexpr (AR == 0) vote_cast(vote, wave, xmax);
     __syncthreads();
     float xs = 1.f;
-    if (!F32 && __builtin_expect(vote_any<kEdgeWaves>(vote), 0)) {
+    if (AR == 0 && __builtin_expect(vote_any<kEdgeWaves>(vote), 0)) {
         // rare: act(x) at 2^15 or beyond -- the window again as act(x) 2^-s
         xs = ldexpf(1.f, -__builtin_amdgcn_readfirstlane(split_shift(block_max<kEdgeWaves>(xmax, red))));
         put_x(xs);
@@ -576,8 +616,24 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = acl[r] = acc_x[r] = acl_x[r] = 0.f;
     const int xblk = kEdgeWaves + (wave >> 2), xchunk = wave & 3;
-    auto mfma3 = [&](int row, int ch, const e_h8& b2, const e_h8& bh8, const e_h8& bl8, e_f32x16& c0,
-                     e_f32x16& c1) __attribute__((always_inline)) {
+    auto mfma3 = [&](int row, int ch, const e_h8& b2, const e_h8& bh8, const e_h8& bl8, const e_h8& bm8,
+                     e_f32x16& c0, e_f32x16& c1) __attribute__((always_inline)) {
+        if constexpr (BF) {
+            // smallest products first (A = act(x) part, B = weight part): lo*hi, hi*lo,
+            // mid*mid, mid*hi, hi*mid, hi*hi -- all cross products but mid*lo, lo*mid, lo*lo
+            const int xo = row * kTXP + 16 * ch + 8 * h;
+            const e_b8 xh8 = *reinterpret_cast<const e_b8*>(xh + xo), xl8 = *reinterpret_cast<const e_b8*>(xl + xo),
+                       xm8 = *reinterpret_cast<const e_b8*>(xm + xo);
+            const e_b8 wh = __builtin_bit_cast(e_b8, bh8), wl = __builtin_bit_cast(e_b8, bl8),
+                       wm = __builtin_bit_cast(e_b8, bm8);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl8, wh, c0, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh8, wl, c0, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xm8, wm, c0, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xm8, wh, c0, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh8, wm, c0, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh8, wh, c0, 0, 0, 0);
+            return;
+        }
         if constexpr (F32) {
             const e_f32x8 x8 = e_ld8(xf + row * kTXP + 16 * ch + 8 * h);
             const e_f32x8 w8 = EdgeW::f32(bh8, bl8);
@@ -597,19 +653,27 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
         const int ch = s / kEdgeK7, q = s - ch * kEdgeK7;
-        const e_h8 bh8 = wr[s % RING][0], bl8 = wr[s % RING][1];
+        const e_h8 bh8 = wr[s % RING][0], bl8 = wr[s % RING][1], bm8 = wr[s % RING][NPW - 1];
         if (s + RING < KS) {
             const int s2 = s + RING;
 #pragma unroll
-            for (int pl = 0; pl < 2; ++pl) wr[s % RING][pl] = W.frag(s2 / kEdgeK7, 0, s2 % kEdgeK7, pl, lane);
+            for (int pl = 0; pl < NPW; ++pl) wr[s % RING][pl] = W.frag(s2 / kEdgeK7, 0, s2 % kEdgeK7, pl, lane);
         }
         const e_h8 b2 = bh8 * (_Float16)2048.0f;
-        mfma3(32 * wave + l32 + q, ch, b2, bh8, bl8, acc, acl);
-        if (ch == xchunk) mfma3(32 * xblk + l32 + q, ch, b2, bh8, bl8, acc_x, acl_x);
+        mfma3(32 * wave + l32 + q, ch, b2, bh8, bl8, bm8, acc, acl);
+        if (ch == xchunk) mfma3(32 * xblk + l32 + q, ch, b2, bh8, bl8, bm8, acc_x, acl_x);
     }
     acc += acl;
     acc_x += acl_x;
     __syncthreads();                                 // act(x) planes dead
+    if constexpr (BF) {                              // the fp32 filter into its place (read after the epilogue's barrier)
+        e_h8* dst = reinterpret_cast<e_h8*>(ff);
+#pragma unroll
+        for (int i = 0; i < FQ; ++i) {
+            const int k = tid + i * kEdgeNT;
+            if (k < kEdgeFilterHalves / 8) dst[k] = fq[i];
+        }
+    }
     // the K-split blocks' partial tiles -> LDS (past the synthesis planes), summed
     // in chunk order by waves 0 (block 8) and 4 (block 9)
     float* part = reinterpret_cast<float*>(xh + 2 * kTSW * kTSP);
@@ -661,7 +725,7 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
             out = 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * out) + 1.0f);
             if ((c_out & 1) && !(f & 1)) out = -out;
             if (w < kTSW) {
-                if constexpr (F32) sf[w * kTSP + c_out] = ok ? out : 0.f;
+                if constexpr (FS) sf[w * kTSP + c_out] = ok ? out : 0.f;
                 else e_split(ok ? out : 0.f, sh[w * kTSP + c_out], sl[w * kTSP + c_out]);
             }
         }
@@ -682,7 +746,7 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
     for (int s = 0; s < kEdgeKW / 32; ++s) {
         const int ka = col * kEdgeFP + 32 * s + 8 * g;
         const int tap = 2 * s + (g >> 1);
-        if constexpr (F32) {
+        if constexpr (FS) {
             const e_f32x8 af = e_ld8(ff + ka);
 #pragma unroll
             for (int q = 0; q < BLK; ++q) {
@@ -727,13 +791,14 @@ using namespace rave;
 
 // rave_conv1d_split_pack_weight of a 7-tap stride-1 conv: chunks of 16
 // in-channels, Mpad = c_out rounded up to 128, fragments then row scales
-static EdgeGeo edge_geometry(const rave_edge_args& a, int frames_per_tile) {
+// (np: weight planes per tap -- 2, or 3 for the bf16x3 image)
+static EdgeGeo edge_geometry(const rave_edge_args& a, int frames_per_tile, int np = 2) {
     EdgeGeo g{};
     g.tiles = ceil_div(a.frames, frames_per_tile);
     const int nchunks = (a.conv_c_in + 15) / 16;
     const int mpad = ceil_div(a.conv_c_out, 128) * 128;
     g.w_mb = mpad / 32;
-    g.w_frag_floats = (int64_t)nchunks * g.w_mb * kEdgeK7 * 2 * 256;
+    g.w_frag_floats = (int64_t)nchunks * g.w_mb * kEdgeK7 * np * 256;
     g.w_bytes = (int)((g.w_frag_floats + mpad) * 4);
     g.y_vec = (reinterpret_cast<uintptr_t>(a.y) % 16 == 0) && a.y_sb % 4 == 0 && a.y_sc % 4 == 0;
     return g;
@@ -827,11 +892,14 @@ extern "C" int rave_decoder_tail_pack_filter_f32(const float* hki, int n_band, i
     return tail_pack(hki, n_band, taps, image, true);
 }
 
-// rave_edge_args.precision: 0 / RAVE_PREC_SPLIT16 (split-f16) or RAVE_PREC_F32_RING (exact fp32)
-static int edge_prec(const rave_edge_args& a, bool& f32) {
+// rave_edge_args.precision: 0 / RAVE_PREC_SPLIT16 (split-f16) or RAVE_PREC_F32_RING (exact fp32);
+// the tail also RAVE_PREC_BF16X3 (bf16x3 conv, exact-fp32 synthesis)
+static int edge_prec(const rave_edge_args& a, bool& f32, bool allow_bf3 = false) {
     f32 = a.precision == RAVE_PREC_F32_RING;
-    if (a.precision != 0 && a.precision != RAVE_PREC_SPLIT16 && !f32) {
-        set_error("edges: precision must be RAVE_PREC_SPLIT16 or RAVE_PREC_F32_RING");
+    if (a.precision != 0 && a.precision != RAVE_PREC_SPLIT16 && !f32 &&
+        !(allow_bf3 && a.precision == RAVE_PREC_BF16X3)) {
+        set_error(allow_bf3 ? "decoder_tail: precision must be RAVE_PREC_SPLIT16, RAVE_PREC_F32_RING or RAVE_PREC_BF16X3"
+                            : "encoder_head: precision must be RAVE_PREC_SPLIT16 or RAVE_PREC_F32_RING");
         return RAVE_ERR_ARG;
     }
     return RAVE_OK;
@@ -881,20 +949,23 @@ extern "C" int rave_decoder_tail(const rave_edge_args* p, void* stream) {
     RAVE_CHECK_ARG(reinterpret_cast<uintptr_t>(a.y) % 16 == 0 && a.y_sb % 4 == 0,
                    "decoder_tail: output must be 16-byte aligned");
     bool f32;
-    int rc = edge_prec(a, f32);
+    int rc = edge_prec(a, f32, true);
     if (rc != RAVE_OK) return rc;
-    const EdgeGeo g = edge_geometry(a, kTF);
+    const bool bf = a.precision == RAVE_PREC_BF16X3;
+    const int ar = bf ? 2 : f32 ? 1 : 0;
+    const EdgeGeo g = edge_geometry(a, kTF, bf ? 3 : 2);
     const dim3 grid(g.tiles * a.batch);
     const bool snake = a.act == RAVE_ACT_SNAKE, am = a.mode == 1;
-    auto pick = [&](auto f32t) {
-        constexpr bool FF = decltype(f32t)::value != 0;
-        return snake ? (am ? decoder_tail_kernel<true, true, FF> : decoder_tail_kernel<true, false, FF>)
-                     : (am ? decoder_tail_kernel<false, true, FF> : decoder_tail_kernel<false, false, FF>);
+    auto pick = [&](auto art) {
+        constexpr int AR = decltype(art)::value;
+        return snake ? (am ? decoder_tail_kernel<true, true, AR> : decoder_tail_kernel<true, false, AR>)
+                     : (am ? decoder_tail_kernel<false, true, AR> : decoder_tail_kernel<false, false, AR>);
     };
-    auto kern = f32 ? pick(EdgeN<1>{}) : pick(EdgeN<0>{});
-    static bool attr[8] = {false, false, false, false, false, false, false, false};
-    rc = edge_lds_attr(kern, kTailLds, attr[4 * f32 + 2 * snake + am]);
+    auto kern = ar == 2 ? pick(EdgeN<2>{}) : ar == 1 ? pick(EdgeN<1>{}) : pick(EdgeN<0>{});
+    const int lds = bf ? kTailLdsBf : kTailLds;
+    static bool attr[12] = {false, false, false, false, false, false, false, false, false, false, false, false};
+    rc = edge_lds_attr(kern, lds, attr[4 * ar + 2 * snake + am]);
     if (rc != RAVE_OK) return rc;
-    launch(kern, grid, dim3(kEdgeNT), (uint32_t)kTailLds, as_stream(stream), a, g);
+    launch(kern, grid, dim3(kEdgeNT), (uint32_t)lds, as_stream(stream), a, g);
     return launch_status("decoder_tail_kernel");
 }

@@ -431,6 +431,8 @@ struct Model {
     void head_op(Plan& p, int B, int T, const View& x, const View& y, const View* fill_z);
     rave_edge_args tail_desc(int B, int F) const;
     bool use_tail(int B, int F);
+    int tail_pick(int B, int F);
+    bool tail_ok(int ep, int B, int F);
     void tail_op(Plan& p, int B, int F, const View& x, const View& y, const View* noise);
     void rvq_encode_op(Plan& p, int B, int Fz, const View& lat, const View& idx);
     void rvq_decode_op(Plan& p, int B, int Fz, const View& idx, const View& z);
@@ -1350,9 +1352,30 @@ void Model::head_op(Plan& p, int B, int T, const View& x, const View& y, const V
     o.bytes = 4.0 * ((double)B * T + (double)B * n.c_out * F);
 }
 
-bool Model::use_tail(int B, int F) {
-    const int ep = edge_prec();
-    const int64_t filt = ep == RAVE_PREC_F32_RING ? tail_filt32_off : tail_filt_off;
+// the fused tail's arithmetic for (B, F), or -1 for the two separate ops: the
+// model's edge arithmetic, and in f32_bf3 models also the bf16x3 conv form
+// (exact-fp32 synthesis), whichever is timed faster
+int Model::tail_pick(int B, int F) {
+    std::vector<int> cands = {edge_prec()};
+    if (edge_prec() == RAVE_PREC_F32_RING && std::find(precs.begin(), precs.end(), (int)RAVE_PREC_BF16X3) != precs.end())
+        cands.push_back(RAVE_PREC_BF16X3);
+    int best = -1;
+    double bms = 1e30;
+    for (int ep : cands) {
+        if (!tail_ok(ep, B, F)) continue;
+        const double ms = tuned.at(key_of({"tail", std::to_string(ep), std::to_string(B), std::to_string(F)})).second;
+        if (best < 0 || ms < bms) {
+            best = ep;
+            bms = ms;
+        }
+    }
+    return best;
+}
+
+bool Model::use_tail(int B, int F) { return tail_pick(B, F) >= 0; }
+
+bool Model::tail_ok(int ep, int B, int F) {
+    const int64_t filt = ep == RAVE_PREC_SPLIT16 ? tail_filt_off : tail_filt32_off;
     if (!edges_enabled() || ep < 0 || filt < 0) return false;
     const Node& n = g.decoder.back();
     if (!w_pack.count({n.name, ep})) return false;
@@ -1420,14 +1443,15 @@ void Model::tail_op(Plan& p, int B, int F, const View& x, const View& y, const V
     a.y_sb = y.sb;
     a.n_sb = noise ? noise->sb : 0;
     a.n_sc = noise ? noise->sc : 0;
-    const int ep = edge_prec();
+    const int ep = tail_pick(B, F);
+    if (ep < 0) fail(RAVE_ERR_STATE, "decoder tail: no fused form for this shape");
     a.precision = ep;
     PlanOp& o = p.add(RAVE_OP_TAIL, a, "decoder_tail:" + n.name + "+pqmf_synthesis");
     rave_edge_args& A = *reinterpret_cast<rave_edge_args*>(o.op.u.raw);
     View wv = arena_view(w_pack.at({n.name, ep}));
     View bv = n.bias ? arena_view(bias_off.at(n.name)) : View{};
     View av = n.act == RAVE_ACT_SNAKE ? arena_view(alpha_off.at(n.alpha)) : View{};
-    View hv = arena_view(ep == RAVE_PREC_F32_RING ? tail_filt32_off : tail_filt_off);
+    View hv = arena_view(ep == RAVE_PREC_SPLIT16 ? tail_filt_off : tail_filt32_off);
     p.bind(o, A, A.x, &x);
     p.bind(o, A, A.y, &y);
     p.bind(o, A, A.weight, &wv);

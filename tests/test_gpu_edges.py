@@ -95,7 +95,7 @@ def test_encoder_head(N, dev, golden, causal, F, B, scale, nb, prec):
     assert np.isnan(zz[:, :64]).all()            # the latent rows are the encoder's, untouched
 
 
-@pytest.mark.parametrize("prec", ["split16", "f32_ring"])
+@pytest.mark.parametrize("prec", ["split16", "f32_ring", "bf16x3"])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("am,act,noise", [(True, "leaky", False), (False, "snake", True), (True, "snake", True)])
 @pytest.mark.parametrize("F,B", [(600, 2), (4096, 2), (100, 1)])
@@ -125,7 +125,8 @@ def test_decoder_tail(N, dev, golden, causal, am, act, noise, F, B, prec):
     xd = torch.from_numpy(x).to(dev)
     y = torch.full((B, 1, 16 * F), float("nan"), device=dev)
     bd, ad = (torch.from_numpy(v).to(dev) for v in (b, alpha))
-    hd = torch.from_numpy(N.pack_edge_filter(hki, head=False, f32=P == N.PREC_F32_RING)).to(dev)
+    # (bf16x3: the conv on the bf16 matrix cores, the synthesis on the exact-fp32 filter image)
+    hd = torch.from_numpy(N.pack_edge_filter(hki, head=False, f32=P in (N.PREC_F32_RING, N.PREC_BF16X3))).to(dev)
     nd = torch.from_numpy(nz).to(dev) if noise else None
     a = N.EdgeArgs(batch=B, frames=F, conv_c_in=ci, conv_c_out=co, conv_kernel=k, conv_pad_left=cpad[0],
                    pqmf_taps=hki.shape[-1], pqmf_pad_left=spad[0], mode=1 if am else 2, act=N.ACT[act],
@@ -138,6 +139,8 @@ def test_decoder_tail(N, dev, golden, causal, am, act, noise, F, B, prec):
     assert np.isfinite(got).all()
     err = maxabs(got, ref)
     assert err <= 2e-5 * max(1.0, float(np.abs(ref).max())), err
+    if prec != "split16":                  # fp32-class arithmetics
+        assert err <= 2e-6 * max(1.0, float(np.abs(ref).max())), err
 
 
 def test_edges_refuse_unsupported(N):
@@ -150,7 +153,8 @@ def test_edges_refuse_unsupported(N):
 
 
 @pytest.mark.parametrize("cfg_name,precision", [("v2", "split16"), ("v3_noise", "split16"), ("v2", "f32_tuned"),
-                                                ("v3_noise", "f32_tuned")])
+                                                ("v3_noise", "f32_tuned"), ("v2", "f32_bf3"),
+                                                ("v3_noise", "f32_bf3")])
 def test_model_uses_edges_and_matches_oracle(dev, golden, cfg_name, precision):
     """A split16 model lays both fused edges into its plans (an exact-fp32
     f32_tuned model: where they time faster than the separate ops), and its

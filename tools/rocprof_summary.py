@@ -42,6 +42,7 @@ FAMILIES = {
     "tail_split16": (("decoder_tail_kernel",), ()),
     "head_f32": ((), ()),
     "tail_f32": ((), ()),
+    "tail_bf16x3": ((), ()),
 }
 _KERNEL_FAMILY = {}
 for _fam, (_mains, _helpers) in FAMILIES.items():
@@ -80,9 +81,18 @@ def kernel_name(demangled: str) -> str:
     return m.group(1) if m else demangled.split("(")[0][:60]
 
 
+_TAIL_AR = re.compile(r"decoder_tail_kernel<[^<>]*,\s*([012])>")
+
+
 def classify(demangled: str):
     """(family or bare kernel name, is the family's main launch)."""
     k = kernel_name(demangled)
+    if k == "decoder_tail_kernel":
+        # round 5: the last template argument is the arithmetic (0 split16, 1 exact
+        # fp32, 2 bf16x3 conv + exact-fp32 synthesis); older builds had a bool there
+        m = _TAIL_AR.search(demangled)
+        if m:
+            return ({"0": "tail_split16", "1": "tail_f32", "2": "tail_bf16x3"}[m.group(1)], True)
     return _KERNEL_FAMILY.get(k, (k, False))
 
 
