@@ -82,6 +82,14 @@ __device__ __forceinline__ int xcd_major(int lin, int grid) {
 // Cache-policy bits of the layer-output stores (buffer instruction aux field;
 // 16 = sc1, write-through).  Default: plain stores (the line stays in the
 // writing XCD's L2 for the next kernel's reads).
+// bf16x3 conv weight image (RAVE_BF3_W4, round 5): 0 = three bf16 planes per
+// K-step (6 bytes per weight); 1 = the exact-fp32 ring image (4 bytes per
+// weight, rave_conv1d_ring_pack_weight's layout), split into hi / mid / lo in
+// registers after each fragment load (conv_split.hip, edge_split.hip's tail)
+#ifndef RAVE_BF3_W4
+#define RAVE_BF3_W4 0
+#endif
+
 #ifndef RAVE_YAUX
 #define RAVE_YAUX 0
 #endif

@@ -152,10 +152,12 @@ __device__ __forceinline__ u32x4_t raw_rsrc(const void* p, int bytes) {
 // family's VC virtual channels -- more K-steps per barrier and per window DMA
 // round, and enough of them for four K-groups on the short-N layers (C >= 512
 // at 64-128 frames), which would otherwise need split-K slabs in HBM.
-// NP: operand planes per staged buffer and weight fragments per K-step (2: the
-// split16 (hi, lo) pair or one fp32 plane in its bytes; 3: bf16x3 hi, lo, mid)
+// NP: operand planes per staged buffer (2: the split16 (hi, lo) pair or one
+// fp32 plane in its bytes; 3: bf16x3 hi, lo, mid); NPW: 16-byte weight
+// fragment loads per K-step and 32-row block (NP, or 2 for the bf16x3 kernel on
+// the fp32 weight image, RAVE_BF3_W4)
 template <int KT, int BM, int BN, int WM, bool XV = true, int KG = 1, int WN_ = 4096 / WM, int VCX = 1, int NS_ = 3,
-          int NP = 2>
+          int NP = 2, int NPW = (NP == 3 && RAVE_BF3_W4) ? 2 : NP>
 struct SGeo {
     using F = SFam<KT>;
     static constexpr int Q = F::Q, S = F::S, VC0 = F::VC, VC = VC0 * VCX;
@@ -171,7 +173,7 @@ struct SGeo {
     static constexpr int XW_MAX = BN + (Q - 1) * F::DMAX + (KT == 2 ? 1 : 0);
     static constexpr int PH = VC + 8;                        // halves per plane row (conflict-free b128)
     static constexpr int XPLANE = XW_MAX * PH * 2;           // bytes per f16 plane
-    static constexpr int WR = KS0 * NJ * NP;                 // weight fragment loads per wave per chunk (max)
+    static constexpr int WR = KS0 * NJ * NPW;                // weight fragment loads per wave per chunk (max)
     // raw window rows: XV = 16-byte pieces from a 4-sample-aligned start (row
     // stride rounded up to 4 samples), else 4-byte pieces
     static constexpr int RS_MAX = XV ? ((XW_MAX * S + 3 + 3) / 4) * 4 : XW_MAX * S;
@@ -189,8 +191,8 @@ struct SGeo {
     // of K-steps to land (NS = 2 trades that for room for wider chunks)
     static constexpr int NS = NS_;
     // hand-counted vmcnt waits (kernel body): prologue, end of chunk, weights
-    static constexpr int WAIT_PRO = (NS - 1) * XI + NP * KS0 * NJ;
-    static constexpr int WAIT_END = (NS - 1) * NP * KS0 * NJ + (NS - 2) * XI;
+    static constexpr int WAIT_PRO = (NS - 1) * XI + NPW * KS0 * NJ;
+    static constexpr int WAIT_END = (NS - 1) * NPW * KS0 * NJ + (NS - 2) * XI;
     static constexpr int WAIT_MAX = WAIT_PRO > WAIT_END ? WAIT_PRO : WAIT_END;
     static constexpr int ALPHA = 4096;                       // Snake alphas (<= 1024 channels)
     static constexpr int EROW = WN + 4;                      // epilogue transpose row stride (floats)
@@ -209,6 +211,7 @@ struct SGeo {
     static_assert(KG == 1 || KG == 2 || KG == 4, "K-groups");
     // a configuration is built only if its hand-counted waits fit the vmcnt
     // field, its LDS fits the CU and every K-group has a K-step
+    static constexpr int NPW_ = NPW;
     static constexpr bool VALID = WAIT_MAX <= 63 && WR + XI <= 63 && LDS_ALL <= 160 * 1024 && ks_of(KG - 1) >= 1 &&
                                   (NS == 2 || NS == 3);
 };
@@ -231,6 +234,8 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
     constexpr bool F32 = AR == 1, BF = AR == 2;
     constexpr int NP = BF ? 3 : 2;
     using G = SGeo<KT, BM, BN, WM, XV, KG, WN_, VCX, NS, NP>;
+    constexpr int NPW = G::NPW_;                     // weight fragment loads per K-step and row block
+    constexpr bool W4 = BF && NPW == 2;              // bf16x3 on the fp32 weight image
     constexpr int S = G::S, CPC = G::CPC, PH = G::PH;
     constexpr int NT = G::NT, NW = G::NW, NWT = G::NWT, WGM = G::WGM, G8 = G::G8, XT = G::XT;
     constexpr int NI = G::NI, NJ = G::NJ, WN = G::WN;
@@ -291,8 +296,8 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
     const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
     const u32x4_t wrs = raw_rsrc(a.w, a.w_bytes);
     // packed weights: [packed chunk][32-row block][KSC0 K-steps][hi|lo][64 lanes][8 halves]
-    const unsigned wcstride = (unsigned)(a.MB * KSC0 * NP) * 1024u;
-    const unsigned wbase = (unsigned)((mw / 32) * KSC0 * NP) * 1024u + (unsigned)lane * 16u;
+    const unsigned wcstride = (unsigned)(a.MB * KSC0 * NPW) * 1024u;
+    const unsigned wbase = (unsigned)((mw / 32) * KSC0 * NPW) * 1024u + (unsigned)lane * 16u;
     const uint32_t lds0 = lds_addr(smem);
     char* planes = smem + G::NS * G::STAGE;
     float* alpha_s = reinterpret_cast<float*>(smem + G::NS * G::STAGE + 2 * NP * G::XPLANE);
@@ -351,16 +356,16 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
     // this wave's weight fragments: register ring, one chunk ahead (chunks past
     // the packed image read zeros)
     // (slot = this group's local K-step; st = the chunk's K-step)
-    u32x4_t wr[G::KS0][NJ][NP];
+    u32x4_t wr[G::KS0][NJ][NPW];
     // (staged chunk c, K-step st = sub-chunk u, packed K-step s0)
     auto load_w = [&](int c, int slot, int st) __attribute__((always_inline)) {
         const int u = st / KSC0, s0 = st - u * KSC0;
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
-            for (int pl = 0; pl < NP; ++pl)
+            for (int pl = 0; pl < NPW; ++pl)
                 wr[slot][j][pl] = bload16(wrs, wbase + (unsigned)(c * VCX + u) * wcstride +
-                                                   (unsigned)(((j * KSC0 + s0) * NP + pl) * 1024));
+                                                   (unsigned)(((j * KSC0 + s0) * NPW + pl) * 1024));
     };
     // raw window of a stage -> activation (* xs) -> (hi, lo) f16 planes; returns
     // max |act| of the task's values (the range guard's vote input)
@@ -507,7 +512,7 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
         constexpr bool guarded = decltype(guardtag)::value != 0;
         constexpr int KS = G::ks_of(GG);                // own K-steps per chunk
         constexpr int ST0 = G::st_of(GG);               // first own K-step
-        constexpr int WR = KS * NJ * NP, XI = G::XI;
+        constexpr int WR = KS * NJ * NPW, XI = G::XI;
 #pragma unroll
         for (int i = 0; i < NS; ++i) issue(c_begin + i, i);
 #pragma unroll
@@ -547,12 +552,27 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
                 // chunk's weights, this chunk's window DMA and this chunk's earlier refills
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
-                    if constexpr (BF) wait_vm_regs3<WR - NP * NJ + XI>(wr[k][j][0], wr[k][j][1], wr[k][j][2]);
-                    else wait_vm_regs<WR - NP * NJ + XI>(wr[k][j][0], wr[k][j][1]);
+                    if constexpr (BF && !W4) wait_vm_regs3<WR - NPW * NJ + XI>(wr[k][j][0], wr[k][j][1], wr[k][j][2]);
+                    else wait_vm_regs<WR - NPW * NJ + XI>(wr[k][j][0], wr[k][j][1]);
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 const AFrag& g = f[k & 1];
                 if constexpr (BF) {
+                    // the weight parts: from the image, or (W4) split from its 8 fp32 values
+                    s_b8 wh[NJ], wl[NJ], wmd[NJ];
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        if constexpr (W4) {
+                            const s_f32x4 u0 = __builtin_bit_cast(s_f32x4, wr[k][j][0]);
+                            const s_f32x4 u1 = __builtin_bit_cast(s_f32x4, wr[k][j][1]);
+                            s_bf3_split(s_f32x8{u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]}, wh[j], wmd[j],
+                                        wl[j]);
+                        } else {
+                            wh[j] = __builtin_bit_cast(s_b8, wr[k][j][0]);
+                            wl[j] = __builtin_bit_cast(s_b8, wr[k][j][1]);
+                            wmd[j] = __builtin_bit_cast(s_b8, wr[k][j][NPW - 1]);
+                        }
+                    }
                     // smallest products first: (x, w) = hi*lo, lo*hi, mid*mid, hi*mid, mid*hi, hi*hi
 #pragma unroll
                     for (int i = 0; i < NI; ++i)
@@ -560,8 +580,7 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
                         for (int j = 0; j < NJ; ++j) {
                             const s_b8 xh8 = __builtin_bit_cast(s_b8, g.h[i]), xl8 = __builtin_bit_cast(s_b8, g.l[i]),
                                        xm8 = __builtin_bit_cast(s_b8, g.m[i]);
-                            const s_b8 wh8 = __builtin_bit_cast(s_b8, wr[k][j][0]), wl8 = __builtin_bit_cast(s_b8, wr[k][j][1]),
-                                       wm8 = __builtin_bit_cast(s_b8, wr[k][j][2]);
+                            const s_b8 wh8 = wh[j], wl8 = wl[j], wm8 = wmd[j];
                             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh8, wl8, acc[i][j], 0, 0, 0);
                             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl8, wh8, acc[i][j], 0, 0, 0);
                             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xm8, wm8, acc[i][j], 0, 0, 0);
@@ -1089,6 +1108,8 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(ConvKArgs a) {
 // combine) when the output alone cannot give every SIMD a wave.
 // operand planes / weight fragments per K-step of an arithmetic (bf16x3: three)
 static int split_planes(int precision) { return precision == RAVE_PREC_BF16X3 ? 3 : 2; }
+// 16-byte weight fragments per K-step and row block in the packed image
+static int split_wplanes(int precision) { return precision == RAVE_PREC_BF16X3 && !RAVE_BF3_W4 ? 3 : 2; }
 static inline int tile_waves(int ti) {   // waves per workgroup
     const int* t = kSplitTiles[ti];
     return (t[0] / t[2]) * (t[1] / t[4]) * t[3];
@@ -1177,7 +1198,7 @@ static int split_prepare(const rave_conv1d_args& a, ConvKArgs& k, int& taps) {
     k.nchunks = ceil_div(a.c_in, split_cpc(taps));
     k.Mpad = ceil_div(k.M, 128) * 128;
     k.MB = k.Mpad / 32;
-    const int64_t frag_floats = (int64_t)k.nchunks * k.MB * split_ksc(taps) * split_planes(a.precision) * 256;
+    const int64_t frag_floats = (int64_t)k.nchunks * k.MB * split_ksc(taps) * split_wplanes(a.precision) * 256;
     RAVE_CHECK_ARG(frag_floats * 4 < (1ll << 31), "conv1d(split16): packed weight beyond 2 GiB");
     k.w_bytes = (int)(frag_floats * 4);
     k.rscale = a.weight + frag_floats;                 // after the fragments
@@ -1350,7 +1371,7 @@ extern "C" int64_t rave_conv1d_split_packed_size(int c_in, int c_out, int kernel
 
 extern "C" int64_t rave_conv1d_bf3_packed_size(int c_in, int c_out, int kernel, int stride, int dilation,
                                                int transposed) {
-    return split_packed_floats(c_in, c_out, kernel, stride, dilation, transposed, 3);
+    return split_packed_floats(c_in, c_out, kernel, stride, dilation, transposed, RAVE_BF3_W4 ? 2 : 3);
 }
 
 // host fp32 -> bf16, round to nearest even (finite weights)
@@ -1466,8 +1487,9 @@ extern "C" int rave_conv1d_ring_pack_weight(const float* w, int c_in, int c_out,
     return split_pack(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift, packed, 1);
 }
 
+// (RAVE_BF3_W4: the bf16x3 kernels read the exact-fp32 image and split it in registers)
 extern "C" int rave_conv1d_bf3_pack_weight(const float* w, int c_in, int c_out, int kernel, int stride,
                                            int dilation, int transposed, int out_shift, float* packed) {
-    return split_pack(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift, packed, 2);
+    return split_pack(w, c_in, c_out, kernel, stride, dilation, transposed, out_shift, packed, RAVE_BF3_W4 ? 1 : 2);
 }
 #endif  // RAVE_SPLIT_KT

@@ -510,7 +510,7 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
 
     unsigned char* vote = reinterpret_cast<unsigned char*>(red + 2 * kEdgeWaves);
     // ---- the conv's first weight fragments (no data dependence): issued first
-    constexpr int NPW = BF ? 3 : 2;
+    constexpr int NPW = BF && !RAVE_BF3_W4 ? 3 : 2;   // weight fragments per tap (W4: fp32 image)
     const EdgeW W{e_rsrc(a.weight, (int64_t)geo.w_bytes), geo.w_mb, NPW};
     constexpr int KS = (kTC / 16) * kEdgeK7;          // 28 K-steps
     constexpr int RING = 4;
@@ -624,8 +624,18 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
             const int xo = row * kTXP + 16 * ch + 8 * h;
             const e_b8 xh8 = *reinterpret_cast<const e_b8*>(xh + xo), xl8 = *reinterpret_cast<const e_b8*>(xl + xo),
                        xm8 = *reinterpret_cast<const e_b8*>(xm + xo);
-            const e_b8 wh = __builtin_bit_cast(e_b8, bh8), wl = __builtin_bit_cast(e_b8, bl8),
-                       wm = __builtin_bit_cast(e_b8, bm8);
+            e_b8 wh, wl, wm;
+            if constexpr (RAVE_BF3_W4) {     // the fp32 image's 8 values -> hi / mid / lo
+                const e_f32x8 w8 = EdgeW::f32(bh8, bl8);
+                wh = __builtin_convertvector(w8, e_b8);
+                const e_f32x8 r = w8 - __builtin_convertvector(wh, e_f32x8);
+                wm = __builtin_convertvector(r, e_b8);
+                wl = __builtin_convertvector(r - __builtin_convertvector(wm, e_f32x8), e_b8);
+            } else {
+                wh = __builtin_bit_cast(e_b8, bh8);
+                wl = __builtin_bit_cast(e_b8, bl8);
+                wm = __builtin_bit_cast(e_b8, bm8);
+            }
             c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl8, wh, c0, 0, 0, 0);
             c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh8, wl, c0, 0, 0, 0);
             c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xm8, wm, c0, 0, 0, 0);
@@ -953,7 +963,7 @@ extern "C" int rave_decoder_tail(const rave_edge_args* p, void* stream) {
     if (rc != RAVE_OK) return rc;
     const bool bf = a.precision == RAVE_PREC_BF16X3;
     const int ar = bf ? 2 : f32 ? 1 : 0;
-    const EdgeGeo g = edge_geometry(a, kTF, bf ? 3 : 2);
+    const EdgeGeo g = edge_geometry(a, kTF, bf && !RAVE_BF3_W4 ? 3 : 2);
     const dim3 grid(g.tiles * a.batch);
     const bool snake = a.act == RAVE_ACT_SNAKE, am = a.mode == 1;
     auto pick = [&](auto art) {

@@ -26,7 +26,7 @@ timeout -k 10 300 python3 $R/bench.py --steps 10 --warmup 3 > "$OUT/bench.json" 
 echo "bench: $(head -c 400 $OUT/bench.json)"
 gemm_rows() {   # counter CSVs are large; keep the GEMM-family rows only
     head -n 1 "$1" > "$1.gemm"
-    grep -E 'conv1d|split_reduce|unit_kernel|unit_split|unit_ring|unit_bf3|stack_split|pqmf|encoder_head|decoder_tail' "$1" >> "$1.gemm" || true
+    grep -E 'conv1d|split_reduce|unit_kernel|unit_split|unit_ring|unit_bf3|stack_split|stack_bf3|pqmf|encoder_head|decoder_tail' "$1" >> "$1.gemm" || true
     rm -f "$1"
 }
 if [ "$ONLY" = all ]; then
