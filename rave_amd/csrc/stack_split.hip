@@ -50,6 +50,24 @@ __device__ __forceinline__ void ss_bf3_split(const FV& v, BV& hi, BV& mid, BV& l
 }
 
 constexpr int kSSUnits = RAVE_STACK_UNITS;
+
+#ifdef RAVE_STAMPS
+// diagnostic build only: 8 clock stamps per workgroup (tools/stack_bench.py --stamps):
+// 0 start, 1 window staged, 2/3/4 after unit 0/1/2 (running sums in registers),
+// 5 after the stores, 7 wall clock at the start
+__device__ unsigned long long* g_ss_stamps = nullptr;
+#define SS_STAMP(k)                                                                            \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && g_ss_stamps) {                                                 \
+            g_ss_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime();                  \
+            if ((k) == 0) g_ss_stamps[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();  \
+        }                                                                                      \
+    } while (0)
+#else
+#define SS_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
 constexpr unsigned kSSOOB = 0xFFFFFFF0u;
 constexpr int kSSBfHalo = 24;
 #ifndef RAVE_SS_BF_R
@@ -133,6 +151,7 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
     float* vred = reinterpret_cast<float*>(lds + G::VRED);
 
     const int tid = threadIdx.x;
+    SS_STAMP(0);
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave % G::WGM, wn = wave / G::WGM;
@@ -296,6 +315,7 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
         }
     }
 
+    SS_STAMP(1);
     struct BFr {
         ss_h8 h[CB], l[CB], m[BF ? CB : 1];
     };
@@ -460,6 +480,7 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
                     yv[j][4 * g + e] = acc[j][4 * g + e] * rs[e] + bb[e] + yv[j][4 * g + e];
         }
         zero_acc();
+        SS_STAMP(2 + u);
         if (u + 1 < kSSUnits) {
             __syncthreads();                           // h dead
             sh0 = guarded_planes(yv, tu + 6 * C + 5 * C, true);    // next unit's act0(y)
@@ -493,6 +514,7 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
                                                   ok ? (unsigned)(m * a.y_sc + t) * 4u : kSSOOB, 0, RAVE_YAUX);
         }
     }
+    SS_STAMP(5);
     if constexpr (CHECK) {
         vote_cast_any(vote, wave, bad);
         __syncthreads();
@@ -536,6 +558,13 @@ static int ss_launch(const SSArgs& k0, int B, bool snake, hipStream_t st) {
 using namespace rave;
 
 extern "C" int rave_stack_supported(int channels) { return channels == 64 || channels == 128; }
+
+#ifdef RAVE_STAMPS
+extern "C" int rave_diag_stack_stamps(void* p) {
+    RAVE_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ss_stamps), &p, sizeof(p)));
+    return RAVE_OK;
+}
+#endif
 
 extern "C" int rave_residual_stack(const rave_stack_args* p, void* stream) {
     RAVE_CHECK_ARG(p, "residual_stack: null args");

@@ -77,7 +77,7 @@ def run_unit(name, B, iters, dev):
         name = name + "_coop"
     st = C_.c_void_p(torch.cuda.current_stream().cuda_stream)
     stamps = None
-    if STAMPS and PREC in (N.PREC_SPLIT16, N.PREC_F32_RING):
+    if STAMPS and PREC in (N.PREC_SPLIT16, N.PREC_F32_RING, N.PREC_BF16X3):
         stamps = torch.zeros(8 * 200000, dtype=torch.int64, device=dev)
         N.check(N.lib.rave_diag_unit_stamps(C_.c_void_p(stamps.data_ptr())))
     for _ in range(3):
