@@ -69,6 +69,9 @@ __device__ __forceinline__ void bf3_split(const FV& v, BV& hi, BV& mid, BV& lo) 
 }
 
 constexpr int kUSMaxDil = 16;
+#ifndef RAVE_COOP_SC1
+#define RAVE_COOP_SC1 1
+#endif
 #ifndef RAVE_US_R
 #define RAVE_US_R 3
 #endif
@@ -200,6 +203,10 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
     constexpr bool F32 = AR == 1, BF = AR == 2;      // arithmetic: 0 split16, 1 fp32, 2 bf16x3
     constexpr int NPW = BF ? 3 : 2;                  // operand planes / weight fragments per K-step
     using G = USGeo<C, WGN, MI, KG, CB, RB, NPW>;
+    // cooperative form with one workgroup per CU (its LDS rules out a second):
+    // the hand-off reads the exchange by sc1 loads instead of an agent acquire
+    // (RAVE_COOP_SC1=0 keeps the acquire: A/B)
+    constexpr bool SC1X = RB > 1 && RAVE_COOP_SC1 != 0 && 2 * G::LDS > 160 * 1024;
     constexpr bool GV = GUARD && AR == 0 && RAVE_SPLIT_GUARD != 0;   // votes inside the body
     static_assert(RB == 1 || GUARD || AR != 0, "the cooperative split16 form runs guarded");
     constexpr int NT = G::NT, PH = G::PH, G8 = G::G8, XT = G::XT, R = G::R;
@@ -363,9 +370,16 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
             const int t = ta + 4 * kb;
             const bool ok = (e < ntv) && t >= 0 && t < a.XL;
 #pragma unroll
-            for (int v = 0; v < 8; ++v)
+            for (int v = 0; v < 8; ++v) {
+#ifdef RAVE_EXP_NOWIN
+                // timing-only A/B variant (wrong results, never shipped): no window
+                // loads -- bounds what hiding the prologue's loads could buy
+                rx[i][v] = us_f32x4{0.01f * v, 0.02f * i, ok ? 0.5f : 0.f, 0.25f};
+#else
                 rx[i][v] = __builtin_bit_cast(us_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                     xrs, ok ? (unsigned)((g * 8 + v) * a.x_sc + t) * 4u : kUSOOB, 0, 0));
+#endif
+            }
         }
         prefetch_ring();
         if constexpr (SNAKE) {
@@ -716,8 +730,14 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
                 __builtin_amdgcn_s_sleep(2);
             }
             if (a.force_giveup) ok = false;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // one workgroup per CU (SC1X): the exchanged bytes are read by sc1 loads
+            // below, which replace the agent acquire (MI355X_MICROARCH.md, hand-off
+            // table row 1: sc1 stores drained before the counter add, an sc1 poll,
+            // sc1 loads behind the barrier this wave joins); else the acquire
+            if constexpr (!SC1X) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             if (lane == 0) {
                 vote[0] = ok ? 0 : 1;
                 if (!ok) {
@@ -748,9 +768,15 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
                 const int w = e / NG;
                 int g = e - w * NG;
                 if (!all && g >= rb * G::G8R) g += G::G8R;
-                const float* src = a.xch + xslot + w * C + g * 8;
-                v0[i] = *reinterpret_cast<const us_f32x4*>(src);
-                v1[i] = *reinterpret_cast<const us_f32x4*>(src + 4);
+                if constexpr (SC1X) {
+                    const unsigned off = (xslot + (unsigned)(w * C + g * 8)) * 4u;
+                    v0[i] = __builtin_bit_cast(us_f32x4, __builtin_amdgcn_raw_buffer_load_b128(xcrs, off, 0, 16));
+                    v1[i] = __builtin_bit_cast(us_f32x4, __builtin_amdgcn_raw_buffer_load_b128(xcrs, off + 16u, 0, 16));
+                } else {
+                    const float* src = a.xch + xslot + w * C + g * 8;
+                    v0[i] = *reinterpret_cast<const us_f32x4*>(src);
+                    v1[i] = *reinterpret_cast<const us_f32x4*>(src + 4);
+                }
             }
 #pragma unroll
             for (int i = 0; i < NTK; ++i) {
