@@ -16,8 +16,10 @@ arithmetic on every conv / unit GEMM with the committed launch choices
 matrix cores with every operand split exactly into three bf16 parts (24
 significand bits, the fp32 exponent range) and six of the nine cross products
 (the three dropped are each below 2^-25 of the product), fp32 accumulation.
-Its error against a float64 reference is at or below the exact-fp32 kernels'
-(tests/test_gpu_parity.py::test_residual_unit_bf16x3_is_fp32_class).  The
+Its error against a float64 reference is within 1.5x (+1e-7 of the output
+scale) of the exact-fp32 MFMA kernels' on the same inputs, and the two differ by
+<= 1e-6 of the output scale (tests/test_gpu_parity.py::
+test_residual_unit_bf16x3_is_fp32_class, test_conv_bf16x3_is_fp32_class).  The
 same invocation then times, on the same input, ``f32_exact`` (``--precision
 f32_tuned``: exact fp32 MFMA on every op) and ``split16_auto`` (per op the
 faster of exact fp32 and split-f16 GEMMs on ~22-bit f16 hi/lo operands), each

@@ -167,6 +167,39 @@ def test_conv_layer(N, dev, case, split, precision):
     assert maxabs(got, ref) <= 2e-5 * max(1.0, np.abs(ref).max())
 
 
+# v2's conv shapes at bench size (T % 4 == 0): the strided down-convs, a ConvT,
+# a C = 512 k3 and the k1 with residual
+BF3_CONV_CASES = [CONV_CASES[i] for i in (4, 5, 8, 12)] + CONV_CASES[-2:]
+
+
+@pytest.mark.parametrize("case", BF3_CONV_CASES, ids=[str(c[:8]) for c in BF3_CONV_CASES])
+def test_conv_bf16x3_is_fp32_class(N, dev, case):
+    """The bf16x3 conv (conv1d_bf3_kernel) against the exact-fp32 ring conv on
+    the same inputs: its error against the float64 oracle is within 1.5x (+1e-7
+    of the output scale) of the exact-fp32 MFMA kernel's, and the two differ by
+    fp32 ulps of the output scale (<= 1e-6), not by bf16 rounding (~4e-3)."""
+    c_in, c_out, k, s, d, transposed, act, has_res, B, T = case
+    x, w, b, alpha, res, pad, ref = conv_case(case)
+    x = 4.0 * x                                  # operands well past 1
+    from oracle.rave_oracle import conv1d, conv_transpose1d, leaky_relu, snake
+    xa = x.astype(np.float64)
+    xa = leaky_relu(xa) if act == "leaky" else snake(xa, alpha.reshape(-1, 1)) if act == "snake" else xa
+    ref = conv_transpose1d(xa, w, s, s // 2, b) if transposed else conv1d(xa, w, b, s, d, pad)
+    if has_res:
+        ref = ref + res
+    outs = {p: run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act, True,
+                        N.PRECISION[p]) for p in ("f32_ring", "bf16x3")}
+    scale = float(np.abs(ref).max())
+    e_ring = maxabs(outs["f32_ring"], ref) / scale
+    e_bf3 = maxabs(outs["bf16x3"], ref) / scale
+    d_rb = maxabs(outs["bf16x3"], outs["f32_ring"]) / scale
+    print(f"\n[bf16x3] conv {case[:8]}: rel err vs float64 ring {e_ring:.2e} bf16x3 {e_bf3:.2e}; "
+          f"bf16x3 vs ring {d_rb:.2e}")
+    assert np.isfinite(outs["bf16x3"]).all()
+    assert e_bf3 <= 1.5 * e_ring + 1e-7
+    assert d_rb <= 1e-6
+
+
 CONFIG_CASES = [CONV_CASES[i] for i in (1, 2, 4, 5, 8, 9, 11, 12, 14)] + CONV_CASES[-2:]
 
 
