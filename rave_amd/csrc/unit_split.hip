@@ -98,6 +98,20 @@ __device__ unsigned long long* g_us_stamps = nullptr;
     do {            \
     } while (0)
 #endif
+// US_AT(k, kc): stamp slot k in the diagnostic build, slot kc in the cooperative-detail
+// one (-DRAVE_STAMPS_COOP: 0 start, 1 window staged, 2 phase 1, 3 published, 4 own
+// phase-2 steps done, 5 poll done, 6 partner rows staged); -1 = no stamp there
+#ifdef RAVE_STAMPS_COOP
+#define US_AT(k, kc)                \
+    do {                            \
+        if ((kc) >= 0) US_STAMP(kc); \
+    } while (0)
+#else
+#define US_AT(k, kc)               \
+    do {                           \
+        if ((k) >= 0) US_STAMP(k); \
+    } while (0)
+#endif
 constexpr unsigned kUSOOB = 0xFFFFFFF0u;
 constexpr int kXcds = 8;                      // gfx950: blocks dealt round-robin over 8 XCDs
 constexpr int kCoopNoFit = 1;                 // us_launch: a group does not fit one XCD
@@ -220,7 +234,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
     unsigned char* vote = reinterpret_cast<unsigned char*>(lds + G::VOTE);
     float* vred = reinterpret_cast<float*>(lds + G::VRED);
 
-    US_STAMP(0);
+    US_AT(0, 0);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -386,7 +400,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
             store_tab();
             __syncthreads();                         // the per-row table (Snake alphas) is in LDS
         }
-        if (RB == 1) US_STAMP(6);
+        if (RB == 1) US_AT(6, -1);
 #pragma unroll
         for (int i = 0; i < XTV; ++i) {
             const int e = tid + i * NT;
@@ -462,7 +476,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
             __syncthreads();
         }
     }
-    US_STAMP(1);
+    US_AT(1, 1);
 
     // ------------------------------------------------------------ K loop (both phases)
     // DA (cooperative form, one wave per SIMD): alternate K-steps accumulate into
@@ -634,7 +648,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
     fold_acc();
     combine();
     __syncthreads();                                 // window (and hand-off area) dead
-    US_STAMP(2);
+    US_AT(2, 2);
 
     // ------------------------------------------------------------ seam: h = act2(h*rs1 + b1) -> planes
     // (phase 1 ran on act0(x) 2^-sh0: its scale 2^sh0 rides on rs1; xs = the
@@ -714,8 +728,9 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
         // phase 2 over the member's own rows while the others finish publishing
         constexpr int OWN = S1 + CG / RB;
         zero_acc();
-        US_STAMP(3);
+        US_AT(3, 3);
         kloop(IC<0>{}, IC<S1>{}, IC<OWN>{});
+        US_AT(-1, 4);
         if (wave == 0) {
             unsigned spins = 0;
             bool ok = true;
@@ -747,7 +762,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
             }
         }
         __syncthreads();
-        US_STAMP(6);
+        US_AT(6, 5);
         gave_up = __builtin_amdgcn_readfirstlane(vote[0]) != 0;
         // group-wide range guard: the members' maxima (vector sc1 loads, not the scalar path)
         float gmax = 0.f;
@@ -829,12 +844,13 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
             stage_rows(IC<0>{}, 1.0f);
             __syncthreads();
         }
+        US_AT(-1, 6);
         depart();
         kloop(IC<0>{}, IC<OWN>{}, IC<ST>{});
     }
     if constexpr (RB == 1) {
         zero_acc();
-        US_STAMP(3);
+        US_AT(3, 3);
         if (KG == 1 || kg == 0) kloop(IC<0>{}, IC<S1 / KG>{}, IC<ST / KG>{});
         else kloop(IC<1>{}, IC<S1 / KG>{}, IC<ST / KG>{});
     }
@@ -872,7 +888,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
     }
     if (KG == 2 && kg == 1) return true;             // (no barrier follows)
 
-    US_STAMP(4);
+    US_AT(4, -1);
     // ------------------------------------------------------------ epilogue: y*rs2 + b2 + x
     // every residual load issued before the first store (one exposed latency)
     {
@@ -912,7 +928,7 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
                 }
             }
     }
-    US_STAMP(5);
+    US_AT(5, -1);
     if constexpr (CHECK && KG == 1) {
         if (vote_rerun()) return false;
     }
