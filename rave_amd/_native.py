@@ -428,11 +428,11 @@ def check(rc: int, what: str = "") -> None:
 
 def conv_configs(args: "ConvArgs") -> list:
     """Launch configurations valid for ``args`` (rave_conv1d_configs), without 0."""
-    buf = (i32 * 256)()
-    n = int(lib.rave_conv1d_configs(C.byref(args), buf, 256))
+    buf = (i32 * 1024)()
+    n = int(lib.rave_conv1d_configs(C.byref(args), buf, 1024))
     if n < 0:
         check(n, "conv1d_configs")
-    return [int(buf[i]) for i in range(min(n, 256))]
+    return [int(buf[i]) for i in range(min(n, 1024))]
 
 
 def conv_chunk(c_in, kernel, stride, dilation, transposed) -> int:

@@ -570,10 +570,10 @@ std::pair<int, int> Model::conv_launch(const Node& n, const rave_conv1d_args& s,
             base.weight = aptr(pack.at({n.name, pr}));
             cands.push_back({pr, 0});
             if (autotune || precs.size() > 1) {
-                int32_t buf[512];
-                const int cnt = rave_conv1d_configs(&base, buf, 512);
+                int32_t buf[1024];
+                const int cnt = rave_conv1d_configs(&base, buf, 1024);
                 check_rc(cnt < 0 ? cnt : RAVE_OK, "conv1d_configs " + n.name);
-                for (int i = 0; i < std::min(cnt, 512); ++i) cands.push_back({pr, buf[i]});
+                for (int i = 0; i < std::min(cnt, 1024); ++i) cands.push_back({pr, buf[i]});
             }
         }
         int64_t nws = 0;
