@@ -131,7 +131,7 @@ typedef struct rave_conv1d_args {
     int32_t transposed;     /* 0/1; kernel == 2*stride when set                  */
     int32_t out_shift;      /* transposed only                                   */
     int32_t act;            /* RAVE_ACT_*                                        */
-    float   leaky_slope;    /* 0.2                                               */
+    float   leaky_slope;    /* 0.2 (<= 1 for the split16 / fp32-ring / bf16x3 kernels) */
     int32_t batch;
     int32_t t_in;           /* input length (columns of x)                       */
     int32_t t_out;          /* output length (columns of y)                      */
@@ -339,7 +339,7 @@ int rave_adain(const rave_adain_args* a, void* stream);
 typedef struct rave_unit_args {
     int32_t channels, batch, t_len, dilation;
     int32_t pad_left, act;
-    float leaky_slope; int32_t precision;   /* RAVE_PREC_* */
+    float leaky_slope; int32_t precision;   /* slope <= 1; RAVE_PREC_* */
     const float* x; int64_t x_sb, x_sc;
     float* y;       int64_t y_sb, y_sc;
     const float* weight;
@@ -403,7 +403,7 @@ int rave_debug_coop(int64_t spin_limit, int force_giveup);
 #define RAVE_STACK_UNITS 3
 typedef struct rave_stack_args {
     int32_t channels, batch, t_len, act;
-    float leaky_slope; int32_t precision;   /* 0 / RAVE_PREC_SPLIT16 or RAVE_PREC_BF16X3 (ABI 17) */
+    float leaky_slope; int32_t precision;   /* slope <= 1; 0 / RAVE_PREC_SPLIT16 or RAVE_PREC_BF16X3 (ABI 17) */
     int32_t dilation[RAVE_STACK_UNITS], pad_left[RAVE_STACK_UNITS];
     const float* x; int64_t x_sb, x_sc;
     float* y;       int64_t y_sb, y_sc;

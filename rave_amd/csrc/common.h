@@ -117,6 +117,38 @@ __device__ __forceinline__ float sin_squared(float x) {
 
 // Split-f16 range guard (RAVE_PREC_SPLIT16).  An operand v is carried as
 // hi = f16(v), lo = f16((v - hi) * 2^11), which needs |v| < 2^15.  Kernels
+// bf16x3 operand split (every kernel's RAVE_PREC_BF16X3 path): v == hi + mid + lo
+// exactly, each a bf16 (RNE: the remainders v - hi and v - hi - mid are exact in
+// fp32).  Worked in pairs: one v_cvt_pk_bf16_f32 per part and pair, the parts
+// back to fp32 by a shift / mask of the packed word (bf16 -> fp32 is exact), the
+// remainders by packed fp32 subtracts -- about half the VALU instructions of the
+// element-wise form, bit for bit the same parts.  FV: 4 or 8 floats, BV: as many
+// bf16.
+template <typename FV, typename BV>
+__device__ __forceinline__ void bf3_split_pk(const FV& v, BV& hi, BV& mid, BV& lo) {
+    constexpr int N = (int)(sizeof(FV) / 4);
+    static_assert((N == 4 || N == 8) && sizeof(BV) == 2 * sizeof(FV) / 4, "bf3_split_pk: 4 or 8 values");
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    typedef unsigned uw __attribute__((ext_vector_type(N / 2)));
+    uw h, m, l;
+#pragma unroll
+    for (int p = 0; p < N / 2; ++p) {
+        const f2 x = {v[2 * p], v[2 * p + 1]};
+        const unsigned hw = __builtin_bit_cast(unsigned, __builtin_convertvector(x, b2));
+        const f2 hf = {__builtin_bit_cast(float, hw << 16), __builtin_bit_cast(float, hw & 0xFFFF0000u)};
+        const f2 r = x - hf;
+        const unsigned mw = __builtin_bit_cast(unsigned, __builtin_convertvector(r, b2));
+        const f2 mf = {__builtin_bit_cast(float, mw << 16), __builtin_bit_cast(float, mw & 0xFFFF0000u)};
+        h[p] = hw;
+        m[p] = mw;
+        l[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(r - mf, b2));
+    }
+    hi = __builtin_bit_cast(BV, h);
+    mid = __builtin_bit_cast(BV, m);
+    lo = __builtin_bit_cast(BV, l);
+}
+
 // convert optimistically and vote per wave on max |v| >= kSplitLimit; a staged
 // operand block that fails is re-converted as v * 2^-s (s = split_shift of its
 // workgroup-wide max, so |v 2^-s| < 2^14) and the GEMM's accumulator (or the

@@ -46,10 +46,7 @@ typedef float s_f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 s_b8 __attribute__((ext_vector_type(8)));
 // fp32 x 8 -> three bf16 parts with v == hi + mid + lo exactly (each remainder exact in fp32)
 __device__ __forceinline__ void s_bf3_split(const s_f32x8& v, s_b8& hi, s_b8& mid, s_b8& lo) {
-    hi = __builtin_convertvector(v, s_b8);
-    const s_f32x8 r = v - __builtin_convertvector(hi, s_f32x8);
-    mid = __builtin_convertvector(r, s_b8);
-    lo = __builtin_convertvector(r - __builtin_convertvector(mid, s_f32x8), s_b8);
+    bf3_split_pk(v, hi, mid, lo);
 }
 
 // (taps after polyphase Q, phases S, virtual channels per chunk VC, max row shift)
@@ -253,6 +250,13 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
             if (k == 0) a.stamps[wg_lin * 8 + 7] = __builtin_amdgcn_s_memrealtime();
         }
     };
+    // cycle accumulators of wave 0 in the K loop: the weight waits (slot 5) and
+    // the chunk-end window wait + barrier (slot 6)
+    unsigned long long acc_ww = 0, acc_we = 0;
+    auto now = []() { return __builtin_amdgcn_s_memtime(); };
+    auto stamp_sum = [&](int k, unsigned long long v) {
+        if (tid == 0 && a.stamps) a.stamps[wg_lin * 8 + k] = v;
+    };
 #else
     auto stamp = [](int) {};
 #endif
@@ -401,7 +405,7 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
                         const float al = alpha_s[min(ci0 + vc / S, a.c_in - 1)];
                         val = val + (1.0f / (al + 1e-9f)) * sin_squared(al * val);
                     } else {
-                        val = val > 0.f ? val : val * slope;
+                        val = fmaxf(val, val * slope);     // leaky ReLU, slope <= 1 (host check)
                     }
                     v8[v] = val * xs;
                 }
@@ -550,11 +554,17 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
                 if (k + 1 < KS) read_a(pb, ST0 + k + 1, f[(k + 1) & 1]);   // next reads in flight
                 // weights of (c, k): issued one chunk ago; younger: the rest of that
                 // chunk's weights, this chunk's window DMA and this chunk's earlier refills
+#ifdef RAVE_STAMPS
+                const unsigned long long tw0 = now();
+#endif
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
                     if constexpr (BF && !W4) wait_vm_regs3<WR - NPW * NJ + XI>(wr[k][j][0], wr[k][j][1], wr[k][j][2]);
                     else wait_vm_regs<WR - NPW * NJ + XI>(wr[k][j][0], wr[k][j][1]);
                 }
+#ifdef RAVE_STAMPS
+                acc_ww += now() - tw0;
+#endif
                 __builtin_amdgcn_sched_barrier(0);
                 const AFrag& g = f[k & 1];
                 if constexpr (BF) {
@@ -639,8 +649,14 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
             }
             // window c+2 landed: younger are, per chunk since its issue, the
             // weight refills and the next windows
+#ifdef RAVE_STAMPS
+            const unsigned long long te0 = now();
+#endif
             wait_vm<(NS - 1) * WR + (NS - 2) * XI>();
             __syncthreads();
+#ifdef RAVE_STAMPS
+            acc_we += now() - te0;
+#endif
             stage = s1;
             if (c == c_begin) stamp(2);
         }
@@ -686,6 +702,10 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
         }
     }
     stamp(3);
+#ifdef RAVE_STAMPS
+    stamp_sum(5, acc_ww);
+    stamp_sum(6, acc_we);
+#endif
     if constexpr (KG >= 2) {
         // groups 1.. hand their partial tiles to group 0 through LDS (ring and
         // planes are dead); group 0 adds them in group order (fixed: bitwise
@@ -1275,6 +1295,7 @@ int conv1d_split(const rave_conv1d_args& a, void* stream) {
     int rc = split_prepare(a, k, taps);
     if (rc != RAVE_OK) return rc;
     RAVE_CHECK_ARG(a.act != RAVE_ACT_SNAKE || a.c_in <= 1024, "conv1d(split16): Snake on more than 1024 channels");
+    RAVE_CHECK_ARG(a.act != RAVE_ACT_LEAKY || a.leaky_slope <= 1.0f, "conv1d(split): leaky slope above 1");
     SplitCfg c;
     rc = split_resolve(a, k, taps, c);
     if (rc != RAVE_OK) return rc;

@@ -577,10 +577,8 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
                     continue;
                 }
                 if constexpr (BF) {
-                    const e_b4 hi = __builtin_convertvector(v, e_b4);
-                    const e_f32x4 r = v - __builtin_convertvector(hi, e_f32x4);
-                    const e_b4 mid = __builtin_convertvector(r, e_b4);
-                    const e_b4 lo = __builtin_convertvector(r - __builtin_convertvector(mid, e_f32x4), e_b4);
+                    e_b4 hi, mid, lo;
+                    bf3_split_pk(v, hi, mid, lo);
                     *reinterpret_cast<e_b4*>(xh + w * kTXP + 4 * cg) = hi;
                     *reinterpret_cast<e_b4*>(xl + w * kTXP + 4 * cg) = lo;
                     *reinterpret_cast<e_b4*>(xm + w * kTXP + 4 * cg) = mid;

@@ -43,10 +43,7 @@ typedef __bf16 ss_b4 __attribute__((ext_vector_type(4)));
 // fp32 -> three bf16 parts with v == hi + mid + lo exactly (unit_split.hip)
 template <typename FV, typename BV>
 __device__ __forceinline__ void ss_bf3_split(const FV& v, BV& hi, BV& mid, BV& lo) {
-    hi = __builtin_convertvector(v, BV);
-    const FV r = v - __builtin_convertvector(hi, FV);
-    mid = __builtin_convertvector(r, BV);
-    lo = __builtin_convertvector(r - __builtin_convertvector(mid, FV), BV);
+    bf3_split_pk(v, hi, mid, lo);
 }
 
 constexpr int kSSUnits = RAVE_STACK_UNITS;
@@ -101,7 +98,7 @@ __device__ __forceinline__ float ss_act(float v, float slope, float alpha) {
         const float r = 1.0f / (alpha + 1e-9f);
         return v + r * sin_squared(alpha * v);
     } else {
-        return v > 0.f ? v : v * slope;     // slope 1 == no activation
+        return fmaxf(v, v * slope);         // leaky ReLU for slope <= 1 (host check); slope 1 == none
     }
 }
 
@@ -574,6 +571,7 @@ extern "C" int rave_residual_stack(const rave_stack_args* p, void* stream) {
         return RAVE_ERR_UNSUPPORTED;
     }
     RAVE_CHECK_ARG(p->x && p->y && p->batch > 0 && p->t_len > 0, "residual_stack: empty shape or null tensor");
+    RAVE_CHECK_ARG(p->act != RAVE_ACT_LEAKY || p->leaky_slope <= 1.0f, "residual_stack: leaky slope above 1");
     RAVE_CHECK_ARG(p->act == RAVE_ACT_LEAKY || p->act == RAVE_ACT_SNAKE || p->act == RAVE_ACT_NONE,
                    "residual_stack: unknown activation");
     const bool snake = p->act == RAVE_ACT_SNAKE;

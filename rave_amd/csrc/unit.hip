@@ -371,6 +371,7 @@ extern "C" int rave_residual_unit(const rave_unit_args* p, void* stream) {
     RAVE_CHECK_ARG(a.act == RAVE_ACT_LEAKY || a.act == RAVE_ACT_SNAKE || a.act == RAVE_ACT_NONE,
                    "residual_unit: bad activation");
     RAVE_CHECK_ARG(a.act != RAVE_ACT_SNAKE || (a.alpha0 && a.alpha2), "residual_unit: snake needs alphas");
+    RAVE_CHECK_ARG(a.act != RAVE_ACT_LEAKY || a.leaky_slope <= 1.0f, "residual_unit: leaky slope above 1");
     RAVE_CHECK_ARG(a.x != a.y, "residual_unit: y must not alias x (other slabs still read it)");
     {
         // cached form: the window and the shifted residual stay inside x's valid columns

@@ -62,10 +62,7 @@ typedef __bf16 us_b4 __attribute__((ext_vector_type(4)));
 // the 24-bit significand; each remainder is exact in fp32)
 template <typename FV, typename BV>
 __device__ __forceinline__ void bf3_split(const FV& v, BV& hi, BV& mid, BV& lo) {
-    hi = __builtin_convertvector(v, BV);
-    const FV r = v - __builtin_convertvector(hi, FV);
-    mid = __builtin_convertvector(r, BV);
-    lo = __builtin_convertvector(r - __builtin_convertvector(mid, FV), BV);
+    bf3_split_pk(v, hi, mid, lo);
 }
 
 constexpr int kUSMaxDil = 16;
@@ -153,7 +150,7 @@ __device__ __forceinline__ float us_act(float v, float slope, float alpha) {
         const float r = 1.0f / (alpha + 1e-9f);
         return v + r * sin_squared(alpha * v);
     } else {
-        return v > 0.f ? v : v * slope;     // slope 1 == no activation
+        return fmaxf(v, v * slope);         // leaky ReLU for slope <= 1 (host check); slope 1 == none
     }
 }
 

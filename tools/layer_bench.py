@@ -44,13 +44,18 @@ PREC = 0
 STAMPS = os.environ.get("RAVE_AMD_DIAG_LIB") == "1"
 
 
-def stamp_report(s_):
+def stamp_report(s_, sums=False):
+    """sums: conv stamps -- slots 0-4 are clock stamps, 5 and 6 wave 0's summed
+    cycles in the K loop's weight waits and chunk-end window waits + barriers."""
     s_ = s_[s_[:, 7] != 0].astype(np.float64)
     if not len(s_):
         return
     rt = (s_[:, 7] - s_[:, 7].min()) * 10.0 / 1e3   # us (100 MHz)
     q = lambda v: f"{np.median(v):7.0f} [{np.percentile(v, 10):6.0f},{np.percentile(v, 90):6.0f}]"
-    last = max(k for k in range(7) if (s_[:, k] != 0).all())
+    last = max(k for k in range(5 if sums else 7) if (s_[:, k] != 0).all())
+    if sums:
+        print(f"   K loop of wave 0, cycles: weight waits {q(s_[:, 5])}  chunk-end waits+barrier {q(s_[:, 6])}",
+              flush=True)
     segs = "  ".join(f"s{k}-{k + 1} {q(s_[:, k + 1] - s_[:, k])}" for k in range(last))
     print(f"   WGs={len(s_)}  cycles median [p10,p90]: {segs}  total {q(s_[:, last] - s_[:, 0])}; "
           f"WG start spread {rt.max():.1f} us", flush=True)
@@ -167,7 +172,7 @@ def run(name, B, iters, dev, config=0):
         stamps.zero_()
         N.check(N.lib.rave_conv1d(C.byref(a), st))
         torch.cuda.synchronize()
-        stamp_report(stamps.view(-1, 8).cpu().numpy())
+        stamp_report(stamps.view(-1, 8).cpu().numpy(), sums=True)
     return ms
 
 
