@@ -389,10 +389,11 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
                 // timing-only A/B variant (wrong results, never shipped): the planes
                 // arrive ready-made, as a producer-side split would deliver them --
                 // one 16-byte copy per plane row piece instead of act + split
-                if constexpr (AR == 0) {
+                if constexpr (AR == 0 || AR == 2) {
                     const s_h8 r8 = *reinterpret_cast<const s_h8*>(raw + (g * 8 / S) * RS + off0 + w * S);
                     *reinterpret_cast<s_h8*>(xh + w * PH + g * 8) = r8;
                     *reinterpret_cast<s_h8*>(xl + w * PH + g * 8) = r8;
+                    if constexpr (AR == 2) *reinterpret_cast<s_h8*>(xm + w * PH + g * 8) = r8;
                     return m;
                 }
 #endif
