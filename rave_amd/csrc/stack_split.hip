@@ -104,9 +104,13 @@ __device__ __forceinline__ float ss_act(float v, float slope, float alpha) {
 
 // C channels (C/32 waves along rows, one 32-row block each); NB centre blocks
 // of 32 columns + 2 margin blocks, CB blocks per wave; NP operand planes (2:
-// split16 hi / lo, 3: bf16x3 hi / lo / mid).
-template <int C, int NB, int CB, int NP = 2> struct SSGeo {
-    static constexpr int WGM = C / 32, NBX = NB + 2, WGN = NBX / CB, NW = WGM * WGN, NT = 64 * NW;
+// split16 hi / lo, 3: bf16x3 hi / lo / mid).  WX > 0 (round 5): WX column waves
+// with CB or CB - 1 blocks each (the first QF take CB), so that the SIMDs, each
+// holding two waves of different column waves, carry equal block counts (C = 64,
+// NB = 8, CB = 3, WX = 4: 3 + 2 blocks per SIMD pair of waves, 8 waves).
+template <int C, int NB, int CB, int NP = 2, int WX = 0> struct SSGeo {
+    static constexpr int WGM = C / 32, NBX = NB + 2, WGN = WX > 0 ? WX : NBX / CB, NW = WGM * WGN, NT = 64 * NW;
+    static constexpr int QF = WX > 0 ? NBX - WX * (CB - 1) : WGN;   // column waves with CB blocks
     static constexpr int BN = 32 * NB;
     static constexpr int OFF = NP == 3 ? kSSBfHalo : 32;   // plane row of extended column 0
     static constexpr int XR = NBX * 32 + 2 * OFF;      // plane rows: extended range + OFF each side
@@ -122,7 +126,7 @@ template <int C, int NB, int CB, int NP = 2> struct SSGeo {
     // + range-guard votes (16 B) and wave maxima (16 floats)
     static constexpr int VOTE = NP * PLANE * 2 + TAB * 4, VRED = VOTE + 16;
     static constexpr int LDS = VRED + 64;
-    static_assert(NBX % CB == 0 && ST % R == 0 && NT <= 1024, "geometry");
+    static_assert((WX > 0 ? (QF > 0 && QF <= WX) : NBX % CB == 0) && ST % R == 0 && NT <= 1024, "geometry");
 };
 
 // Range guard in two passes, as unit_split.hip: GUARD = false runs no guard
@@ -132,10 +136,10 @@ template <int C, int NB, int CB, int NP = 2> struct SSGeo {
 // when the unguarded pass found one (the guarded pass rewrites its stores).
 // BF (bf16x3): one pass, no guard code at all (the operands keep the fp32
 // exponent range).
-template <int C, int NB, int CB, bool SNAKE, bool GUARD, bool BF = false>
+template <int C, int NB, int CB, bool SNAKE, bool GUARD, bool BF = false, int WX = 0>
 __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
     constexpr int NPW = BF ? 3 : 2;                    // operand planes / weight fragments per K-step
-    using G = SSGeo<C, NB, CB, NPW>;
+    using G = SSGeo<C, NB, CB, NPW, WX>;
     constexpr bool GV = GUARD && !BF && RAVE_SPLIT_GUARD != 0;
     constexpr int NT = G::NT, PH = G::PH, XR = G::XR, G8 = G::G8, XT = G::XT, R = G::R;
     constexpr int S1 = G::S1, ST = G::ST, CG = G::CG, OFF = G::OFF;
@@ -260,12 +264,18 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
         return cmax;
     };
     // running sum y (fp32): lane column col0 + 32j, rows mrow0 + 8(r>>2) + (r&3)
-    const int col0 = wn * 32 * CB + l32;               // extended column of this lane
+    // this wave's column blocks: nbw of them from extended block blk0 (uniform
+    // geometry: CB from wn * CB)
+    constexpr bool VAR = G::QF != G::WGN;
+    const int nbw = VAR ? (wn < G::QF ? CB : CB - 1) : CB;
+    const int blk0 = VAR ? (wn < G::QF ? wn * CB : G::QF * CB + (wn - G::QF) * (CB - 1)) : wn * CB;
+    const int col0 = blk0 * 32 + l32;                  // extended column of this lane
     const int mrow0 = 32 * wm + 4 * hh;
     float yv[CB][16];
     auto load_y = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < CB; ++j) {
+            if (VAR && j >= nbw) break;
             const int t = ext0 + col0 + 32 * j;
             const bool ok = t >= 0 && t < a.T;
 #pragma unroll
@@ -319,6 +329,7 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
     auto read_b = [&](int row, int ch, BFr& f) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < CB; ++j) {
+            if (VAR && j >= nbw) break;
             const int off = (row + j * 32) * PH + ch + 8 * hh;
             f.h[j] = *reinterpret_cast<const ss_h8*>(ph + off);
             f.l[j] = *reinterpret_cast<const ss_h8*>(pl + off);
@@ -345,6 +356,7 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
             if constexpr (SNAKE) al = *reinterpret_cast<const ss_f32x4*>(al_tab + m);
 #pragma unroll
             for (int j = 0; j < CB; ++j) {
+                if (VAR && j >= nbw) break;
                 const int t = ext0 + col0 + 32 * j;
                 const bool ok = !mask || (t >= 0 && t < a.T);
                 ss_f32x4 w4;
@@ -399,6 +411,7 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
                 // smallest products first: lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi
 #pragma unroll
                 for (int j = 0; j < CB; ++j) {
+                    if (VAR && j >= nbw) break;
                     const ss_b8 xh = __builtin_bit_cast(ss_b8, f.h[j]), xl = __builtin_bit_cast(ss_b8, f.l[j]),
                                 xm = __builtin_bit_cast(ss_b8, f.m[j]);
                     acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh, acc[j], 0, 0, 0);
@@ -491,7 +504,7 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
     if constexpr (CHECK) {
 #pragma unroll
         for (int j = 0; j < CB; ++j) {
-            const int blk = wn * CB + j;
+            const int blk = blk0 + j;
             const bool ok = blk >= 1 && blk <= NB && ext0 + col0 + 32 * j < a.T;
 #pragma unroll
             for (int r = 0; r < 16; ++r) bad |= ok && !__builtin_isfinite(yv[j][r]);
@@ -501,7 +514,8 @@ __device__ __forceinline__ bool stack_split_body(const SSArgs& a) {
     const auto yrs = ss_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
 #pragma unroll
     for (int j = 0; j < CB; ++j) {
-        const int blk = wn * CB + j;                   // extended block: 1..NB are the centre
+        if (VAR && j >= nbw) break;
+        const int blk = blk0 + j;                      // extended block: 1..NB are the centre
         const int t = ext0 + col0 + 32 * j;
         const bool ok = blk >= 1 && blk <= NB && t < a.T;
 #pragma unroll
@@ -527,18 +541,20 @@ template <int C, int NB, int CB, bool SNAKE>
 __global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_split_kernel(SSArgs a) {
     if (!stack_split_body<C, NB, CB, SNAKE, RAVE_SPLIT_GUARD == 0>(a)) (void)stack_split_body<C, NB, CB, SNAKE, true>(a);
 }
-template <int C, int NB, int CB, bool SNAKE>
-__global__ __launch_bounds__(64 * (C / 32) * ((NB + 2) / CB)) void stack_bf3_kernel(SSArgs a) {
-    (void)stack_split_body<C, NB, CB, SNAKE, false, true>(a);
+template <int C, int NB, int CB, bool SNAKE, int WX>
+__global__ __launch_bounds__((SSGeo<C, NB, CB, 3, WX>::NT)) void stack_bf3_kernel(SSArgs a) {
+    (void)stack_split_body<C, NB, CB, SNAKE, false, true, WX>(a);
 }
 
-template <int C, int NB, int CB, bool BF = false>
+template <int C, int NB, int CB, bool BF = false, int WX = 0>
 static int ss_launch(const SSArgs& k0, int B, bool snake, hipStream_t st) {
-    using G = SSGeo<C, NB, CB, BF ? 3 : 2>;
+    using G = SSGeo<C, NB, CB, BF ? 3 : 2, WX>;
+    static_assert(BF || WX == 0, "split16 stacks: uniform geometry");
     SSArgs k = k0;
     k.ntiles = ceil_div(k.T, G::BN);
-    void (*kern)(SSArgs) = BF ? (snake ? stack_bf3_kernel<C, NB, CB, true> : stack_bf3_kernel<C, NB, CB, false>)
-                              : (snake ? stack_split_kernel<C, NB, CB, true> : stack_split_kernel<C, NB, CB, false>);
+    void (*kern)(SSArgs) = nullptr;
+    if constexpr (BF) kern = snake ? stack_bf3_kernel<C, NB, CB, true, WX> : stack_bf3_kernel<C, NB, CB, false, WX>;
+    else kern = snake ? stack_split_kernel<C, NB, CB, true> : stack_split_kernel<C, NB, CB, false>;
     static bool attr[2] = {false, false};
     if (G::LDS > 65536 && !attr[snake]) {
         RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -639,17 +655,23 @@ extern "C" int rave_residual_stack(const rave_stack_args* p, void* stream) {
 #define RAVE_S128_CB 2
 #endif
     // bf16x3 (three planes, 24-row halo): C = 64 keeps 8 centre blocks (146 KB of
-    // LDS); C = 128 fits 2 (152 KB)
+    // LDS); C = 128 fits 2 (152 KB).  C = 64 (round 5): 8 waves, column waves of
+    // 3, 3, 2, 2 blocks (RAVE_B64S_WX = 4; 0 = 10 waves of 2 blocks, A/B)
 #ifndef RAVE_B64S_NB
 #define RAVE_B64S_NB 8
-#define RAVE_B64S_CB 2
+#endif
+#ifndef RAVE_B64S_WX
+#define RAVE_B64S_WX 4
+#endif
+#ifndef RAVE_B64S_CB
+#define RAVE_B64S_CB (RAVE_B64S_WX > 0 ? 3 : 2)
 #endif
 #ifndef RAVE_B128S_NB
 #define RAVE_B128S_NB 2
 #define RAVE_B128S_CB 2
 #endif
     if (bf) {
-        if (C == 64) return ss_launch<64, RAVE_B64S_NB, RAVE_B64S_CB, true>(k, p->batch, snake, st);
+        if (C == 64) return ss_launch<64, RAVE_B64S_NB, RAVE_B64S_CB, true, RAVE_B64S_WX>(k, p->batch, snake, st);
         return ss_launch<128, RAVE_B128S_NB, RAVE_B128S_CB, true>(k, p->batch, snake, st);
     }
     if (C == 64) return ss_launch<64, RAVE_S64_NB, RAVE_S64_CB>(k, p->batch, snake, st);
