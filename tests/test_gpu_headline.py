@@ -64,9 +64,9 @@ def headline(dev):
 
 
 def test_headline_plan_runs_bf16x3(headline):
-    """The plan under test is the headline's arithmetic: bf16x3 units and
-    convs, cooperative units at C = 256 / 512."""
-    assert headline["n_bf3"] >= 30, headline["n_bf3"]
+    """The plan under test is the headline's arithmetic: bf16x3 units, C = 64
+    residual stacks and convs, cooperative units at C = 512."""
+    assert headline["n_bf3"] >= 28, headline["n_bf3"]
     assert headline["n_coop"] >= 4, headline["n_coop"]
 
 
