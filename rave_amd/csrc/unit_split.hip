@@ -1297,11 +1297,14 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
         if (C == 256) return go(IC<256>{}, IC<RAVE_F256_WGN>{}, IC<1>{}, IC<1>{}, IC<RAVE_F256_CB>{}, IC<1>{});
     }
     // bf16x3: its own geometry knobs (A/B builds; the defaults are the split form's)
+// C = 64 (round 5): four 32-column waves per 32-row block (8 waves, 128 VGPRs: four
+// waves per SIMD at two workgroups per CU) against two 64-column waves (two per
+// SIMD): unit_64 17.5 -> 16.4 us (profiles/r05_aa)
 #ifndef RAVE_B64_WGN
-#define RAVE_B64_WGN RAVE_U64_WGN
+#define RAVE_B64_WGN 4
 #endif
 #ifndef RAVE_B64_CB
-#define RAVE_B64_CB RAVE_U64_CB
+#define RAVE_B64_CB 1
 #endif
 #ifndef RAVE_B64_MI
 #define RAVE_B64_MI 1
