@@ -186,6 +186,43 @@ def host_info() -> dict:
     return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "loadavg_1min": load}
 
 
+def usable_cpus() -> dict:
+    """The CPUs this process may actually use: the affinity mask and the cgroup
+    CPU quota (cgroup v2 cpu.max, or v1 cfs quota / period), beside the host's
+    logical CPU count.  On the shared GPU hosts the quota (16 CPUs of a 256-CPU
+    host) is what "all host cores" can mean for one process: 256 threads under
+    a 16-CPU quota measured 51 s per step, oversubscription, not a baseline."""
+    host = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = host
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+                q = float(fh.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+                per = float(fh.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    usable = min(host, aff, int(quota) if quota else host)
+    # the GPU boxes also state the per-process CPU share in OMP_NUM_THREADS (16)
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        usable = min(usable, int(share))
+    return {"host_logical_cpus": host, "affinity_cpus": aff,
+            "cgroup_cpu_quota": round(quota, 2) if quota else None,
+            "omp_num_threads": int(share) if share.isdigit() else None, "usable_cpus": max(1, usable)}
+
+
 def cpu_baseline(cfg, params, spk, B: int, T: int, seconds: float, threads: int):
     """The reference's CPU path -- its module graph on torch fp32 CPU (oneDNN
     convolutions), restated in oracle/torch_cpu.py and pinned to the reference
@@ -214,17 +251,146 @@ def cpu_baseline(cfg, params, spk, B: int, T: int, seconds: float, threads: int)
 
     n, el = timed(threads, seconds)
     n1, el1 = timed(1, seconds / 2)
+    # every CPU this process may use (BASELINE.md's plan: all host cores, the
+    # count stated): the affinity mask and cgroup quota bound it on a shared host
+    cpus = usable_cpus()
+    allc = cpus["usable_cpus"]
+    load_all = host_info()["loadavg_1min"]
+    if allc != threads:
+        na, ela = timed(allc, seconds / 2)
+    else:                                    # the main figure already used them all
+        na, ela = n, el
     after = host_info()
     torch.set_num_threads(threads)
     return {"value": round(n * B * T / el, 1), "unit": "samples/s", "cores": threads, "kind": "port",
             "ms_per_step": round(1e3 * el / n, 2),
             "one_thread": {"value": round(n1 * B * T / el1, 1), "ms_per_step": round(1e3 * el1 / n1, 2),
                            "steps": n1},
+            "all_host_cores": {"threads": allc, "value": round(na * B * T / ela, 1),
+                               "ms_per_step": round(1e3 * ela / na, 2), "steps": na,
+                               "loadavg_1min_before": load_all, **cpus,
+                               "note": "all CPUs the process may use (affinity and cgroup quota of the shared "
+                                       "host); the host's logical CPUs beyond the quota are other tenants'"},
             "host": {"cpu_model": before["cpu_model"], "os_cpu_count": before["os_cpu_count"],
                      "loadavg_1min_before": before["loadavg_1min"], "loadavg_1min_after": after["loadavg_1min"]},
             "sample": f"{n} x v2 encode+decode of the bench step ({B} x {T} samples): the reference's "
                       f"module graph on torch {torch.__version__} fp32 CPU (oneDNN), {el:.1f} s wall, "
-                      f"torch.set_num_threads({threads}); then {n1} steps on 1 thread ({el1:.1f} s)"}
+                      f"torch.set_num_threads({threads}); then {n1} steps on 1 thread ({el1:.1f} s); all usable CPUs: "
+                      f"{allc} ({na} steps, {ela:.1f} s)"}
+
+
+def _pinned(name: str, precision: str):
+    """(tuning list or None, its source) of a side config's committed launch choices."""
+    path = os.path.join(REPO, "profiles", "tuning", f"{name}_{precision}.json")
+    if not os.path.exists(path):
+        return None, "autotuned at plan build"
+    with open(path) as fh:
+        return json.load(fh), os.path.relpath(path, REPO)
+
+
+def _save_pinned(name: str, precision: str, model) -> None:
+    path = os.path.join(REPO, "profiles", "tuning", f"{name}_{precision}.json")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "w") as fh:
+        json.dump(model.tuning(), fh, indent=0)
+
+
+def side_configs(a, dev) -> dict:
+    """BASELINE configs 3, 4 and 5 on this GPU (N = 1 only), beside the config-2
+    headline, in the headline's arithmetic (f32_bf3) and in ``auto``; every
+    number from the same process as the headline:
+
+    * C3 -- v2 causal streaming, 2048-sample blocks, B = 1 (one nn~ stream):
+      host call -> synchronize latency of each block, median and p99 over
+      ``a.c3_blocks`` blocks after 8 warm-up blocks, each block a replayed
+      hipGraph, for decode and for encode+decode; kernel launches per block;
+    * C4 -- discrete encode_codes -> decode_codes of the per-GPU shard of 64
+      clips over 8 GPUs (8 x 65536), ms per shard (the RVQ-index all-gather is
+      an identity at N = 1);
+    * C5 -- v3 Snake + noise decode of the per-GPU shard of 128 (z 16 x 320 x 64
+      -> 16 x 65536), noise drawn on the device, ms per shard.
+
+    Synthetic inputs, seeded random-init weights.  Launch choices are pinned by
+    profiles/tuning/{c3,c4,c5}_<precision>.json where committed."""
+    import torch
+    from rave_amd import config as rcfg
+    from rave_amd.model import DECODE, DECODE_CODES, ENCODE_CODES, RAVE
+    from rave_amd.streaming import StreamingRAVE
+    from rave_amd.weights import init_params, init_speaker
+
+    def sync_ms(fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps * 1e3
+
+    out = {"note": "N = 1, synthetic inputs, random-init weights; C3 per-block latency = host call -> "
+                   "synchronize of one replayed block graph (plus its two staging copies)"}
+    for prec in ("f32_bf3", "auto"):
+        res = {}
+        # ---- C3
+        cfg = rcfg.causal()
+        tun, src = _pinned("c3", prec)
+        m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=prec, tuning=tun)
+        blk, warm, nb = 2048, 8, a.c3_blocks
+        gen = torch.Generator().manual_seed(0)
+        z = torch.randn(warm + nb, 1, cfg.dec_in, blk // cfg.hop, generator=gen).to(dev)
+        x = (0.2 * torch.randn(warm + nb, 1, 1, blk, generator=gen)).to(dev)
+        s = StreamingRAVE(m, batch=1, block=blk, graph=True)
+        c3 = {"workload": "v2 causal streaming, 2048-sample blocks, B = 1 (BASELINE configs[2])",
+              "tuning": src, "launches_per_block": {"encode": s.launches("encode"), "decode": s.launches("decode")}}
+        for name, fn in (("decode", lambda i: s.decode(z[i])), ("encode_decode", lambda i: s.forward(x[i]))):
+            s.reset()
+            lat = []
+            for i in range(warm + nb):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fn(i)
+                torch.cuda.synchronize()
+                if i >= warm:
+                    lat.append((time.perf_counter() - t0) * 1e3)
+            lat = np.array(lat)
+            c3[name] = {"median_ms": round(float(np.median(lat)), 4), "p99_ms": round(float(np.percentile(lat, 99)), 4),
+                        "x_realtime_at_p99": round(blk / SR * 1e3 / float(np.percentile(lat, 99)), 1)}
+        if a.save_tuning:
+            _save_pinned("c3", prec, m)
+        del s, m
+        res["c3"] = c3
+        # ---- C4
+        cfg = rcfg.discrete()
+        tun, src = _pinned("c4", prec)
+        m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=prec, tuning=tun)
+        B4, T4 = 8, 65536
+        x4 = (0.2 * torch.randn(B4, 1, T4, generator=torch.Generator().manual_seed(0))).to(dev)
+        ms = sync_ms(lambda: m.decode_codes(m.encode_codes(x4)), a.steps, max(2, a.warmup))
+        nl = len(m.ops(ENCODE_CODES, B4, T4)) + len(m.ops(DECODE_CODES, B4, T4 // cfg.hop))
+        res["c4"] = {"workload": f"discrete encode_codes -> decode_codes, {B4} x {T4} (BASELINE configs[3], per-GPU "
+                                 "shard of 64)", "tuning": src, "ms_per_shard": round(ms, 4),
+                     "samples_per_s": round(B4 * T4 / ms * 1e3, 1), "launches": nl}
+        if a.save_tuning:
+            _save_pinned("c4", prec, m)
+        del m
+        # ---- C5
+        cfg = rcfg.v3_noise()
+        tun, src = _pinned("c5", prec)
+        m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=prec, tuning=tun)
+        B5, F5 = 16, 64
+        z5 = torch.randn(B5, cfg.dec_in, F5, generator=torch.Generator().manual_seed(0)).to(dev)
+        ms = sync_ms(lambda: m.decode(z5), a.steps, max(2, a.warmup))
+        res["c5"] = {"workload": f"v3 Snake + noise decode, z ({B5}, {cfg.dec_in}, {F5}) -> ({B5}, 1, {F5 * cfg.hop}) "
+                                 "(BASELINE configs[4], per-GPU shard of 128)", "tuning": src,
+                     "ms_per_shard": round(ms, 4), "samples_per_s": round(B5 * F5 * cfg.hop / ms * 1e3, 1),
+                     "launches": len(m.ops(DECODE, B5, F5))}
+        if a.save_tuning:
+            _save_pinned("c5", prec, m)
+        del m
+        out[prec] = res
+        log(f"configs [{prec}]: {json.dumps(res)}")
+    return out
 
 
 DTYPE = {"f32": "fp32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32)",
@@ -543,6 +709,9 @@ def main():
                     help="torch CPU threads of the baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip BASELINE configs 3-5 (C3 streaming latency, C4 / C5 shards) beside the headline")
+    ap.add_argument("--c3-blocks", type=int, default=64, help="timed C3 blocks per measurement")
     ap.add_argument("--pipeline", type=int, default=3,
                     help="also time this many independent steps in flight on as many streams (N=1 only; "
                          "reported as 'pipelined' beside the headline; 1 = off)")
@@ -600,6 +769,10 @@ def main():
         fast["precision"] = "auto"
         del y_fast
 
+    side = None
+    if world == 1 and not a.no_configs:
+        side = side_configs(a, dev)
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(cfg, params, spk, B, T, a.cpu_seconds, a.cpu_threads)
@@ -626,6 +799,7 @@ def main():
             "pipelined": head.get("pipelined"),
             "f32_exact": exact,
             "split16_auto": fast,
+            "configs": side,
             "cpu_baseline": cpu,
         }
         for side in (exact, fast):                # keep the second mode's roofline compact

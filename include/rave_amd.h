@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RAVE_ABI_VERSION 17
+#define RAVE_ABI_VERSION 18
 /* int32 arrival counters at the head of every split-K workspace (rave_conv1d_args.partial) */
 #define RAVE_SPLITK_TICKETS 4096
 /* The last of those words is reserved: no conv ticket uses it.  A cooperative
@@ -792,6 +792,10 @@ int rave_stream_decode(rave_stream* s, const float* z, float* y, const float* no
 int rave_stream_encode_codes(rave_stream* s, const float* x, int64_t* idx, void* stream);
 int rave_stream_decode_codes(rave_stream* s, const int64_t* idx, float* y, const float* noise_u, void* stream);
 int rave_stream_delay(const rave_stream* s);
+/* Kernel launches one block issues (which 0 = encode, 1 = decode): the kernel
+ * nodes of the captured graph (RAVE_STREAM_GRAPH; the staging copies around a
+ * replay are not counted) or the plan's ops (eager).  Negative = status. */
+int rave_stream_launches(const rave_stream* s, int which);
 
 #ifdef __cplusplus
 }

@@ -42,7 +42,7 @@ OP_UNIT = 11
 OP_STACK = 12
 OP_HEAD = 13
 OP_TAIL = 14
-ABI_VERSION = 17
+ABI_VERSION = 18
 SPLITK_TICKETS = 4096       # RAVE_SPLITK_TICKETS: zeroed int32 counters at the head of a split-K workspace
 SPLITK_STATUS_WORD = SPLITK_TICKETS - 1   # RAVE_SPLITK_STATUS_WORD: the cooperative unit's give-up word
 
@@ -259,6 +259,7 @@ EXPORTS = [
     "rave_model_op_times", "rave_stream_create", "rave_stream_destroy", "rave_stream_reset",
     "rave_stream_encode", "rave_stream_decode", "rave_stream_encode_codes", "rave_stream_decode_codes",
     "rave_stream_delay",
+    "rave_stream_launches",
     "rave_fir", "rave_row_stats", "rave_attn_pool", "rave_linear", "rave_maxpool",
     "rave_encoder_head", "rave_decoder_tail", "rave_encoder_head_pack_filter", "rave_decoder_tail_pack_filter",
     "rave_encoder_head_pack_filter_f32", "rave_decoder_tail_pack_filter_f32",
@@ -365,6 +366,7 @@ def _load():
     lib.rave_stream_encode_codes.argtypes = [vp, vp, vp, vp]
     lib.rave_stream_decode_codes.argtypes = [vp, vp, vp, vp, vp]
     lib.rave_stream_delay.argtypes = [vp]
+    lib.rave_stream_launches.argtypes = [vp, C.c_int]
     # ABI self-check
     n = lib.rave_struct_sizes(None, 0)
     buf = (i64 * n)()

@@ -227,4 +227,24 @@ __device__ __forceinline__ float apply_act(float v, int act, float slope, float 
     return v;
 }
 
+// Shape limits of the fused residual stack (rave_residual_stack refuses the
+// rest with RAVE_ERR_UNSUPPORTED): units 2..n reach at most 32 margin columns
+// per side, and the bf16x3 form keeps a 24-row plane halo, so no unit's taps
+// may reach past 24 columns on either side.  The engine checks it before it
+// honours a tuned or pinned stack choice (stack_runs), so such a stack falls
+// back to its units instead of failing at launch.
+constexpr int kStackMargin = 32, kStackBf3Halo = 24;
+inline bool stack_shape_fits(bool bf16x3, const int* dilation, const int* pad_left, int units) {
+    int reach_l = 0, reach_r = 0;
+    for (int u = 0; u < units; ++u) {
+        const int d = dilation[u], pl = pad_left[u];
+        if (bf16x3 && (pl > kStackBf3Halo || 2 * d - pl > kStackBf3Halo)) return false;
+        if (u > 0) {
+            reach_l += pl;
+            reach_r += 2 * d - pl;
+        }
+    }
+    return reach_l <= kStackMargin && reach_r <= kStackMargin;
+}
+
 }  // namespace rave

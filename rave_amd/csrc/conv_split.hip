@@ -127,6 +127,12 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// Keeps a bload16 destination live (and in its register) up to this point:
+// placed after the wait that covers the load, it forbids hipcc to reuse the
+// register for anything else while the load may still write it (volatile asm
+// statements keep their order).  tools/ring_hazard_check.py checks the built
+// code object for any read, copy or write of a ring register before its wait.
+__device__ __forceinline__ void ring_keep(u32x4_t& a) { asm volatile("" : "+v"(a)); }
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
 }
@@ -533,8 +539,11 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
         // per chunk c: DMA window c+NS into window c's slot (split during chunk
         // c-1) | own K-steps (weights of c from the ring, refill with c+1) | split
         // window c+1 into the other plane pair | wait + barrier
+        // (a do-while: every split owns >= 1 chunk, S = ceil(nchunks / cps) on the
+        // host, so no zero-trip path leaves the ring's loads outstanding)
         int stage = 0;
-        for (int c = c_begin; c < c_end; ++c) {
+        int c = c_begin;
+        do {
             const int pb = (c - c_begin) & 1;
             const int s1 = stage + 1 == NS ? 0 : stage + 1;
             AFrag f[2];
@@ -660,7 +669,16 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
 #endif
             stage = s1;
             if (c == c_begin) stamp(2);
-        }
+        } while (++c < c_end);
+        // drain the ring (its last refills read past the image): the registers
+        // stay tied up to the wait, so nothing reuses them while a refill lands
+        wait_vm<0>();
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int pl = 0; pl < NPW; ++pl) ring_keep(wr[k][j][pl]);
     };
     // Range guard, two attempts: the first runs the plain K loop (no guard
     // code); an operand past the f16 range became inf in its hi half, so it
@@ -677,7 +695,6 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
                 else body(IC<3>{}, guardtag);
             }
         }
-        wait_vm<0>();                       // drain the ring (epilogue loads / a second attempt)
     };
     run_k(IC<0>{});
     if (RAVE_SPLIT_GUARD && AR == 0) {

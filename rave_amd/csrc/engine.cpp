@@ -868,11 +868,17 @@ std::map<std::string, std::vector<std::pair<const Node*, const Node*>>> Model::s
         const Node& a0 = *run[0].first;
         bool ok = rave_stack_supported(a0.c_in) != 0;
         for (size_t k = 0; k + 1 < U && ok; ++k) ok = run[k + 1].first->src == run[k].second->dst;
-        for (auto& pr : run) {
-            const Node& k3 = *pr.first;
+        int dil[RAVE_STACK_UNITS], padl[RAVE_STACK_UNITS];
+        for (size_t k = 0; k < U; ++k) {
+            const Node& k3 = *run[k].first;
             ok = ok && k3.c_in == a0.c_in && k3.act == a0.act && k3.bias == a0.bias &&
                  unit_pack.count({k3.name, stack_prec()}) && !(ad_on && !k3.adain.empty());
+            dil[k] = k3.dilation;
+            padl[k] = k3.pad_l;
         }
+        // the shapes the stack kernel takes (its margin, the bf16x3 plane halo):
+        // a tuned or pinned stack choice is only ever consulted for these
+        ok = ok && stack_shape_fits(stack_prec() == RAVE_PREC_BF16X3, dil, padl, (int)U);
         if (ok) {
             out[a0.name] = run;
             i += U;
@@ -2776,6 +2782,33 @@ extern "C" int rave_stream_decode_codes(rave_stream* h, const int64_t* idx, floa
         if (!s->codes) fail(RAVE_ERR_ARG, "decode_codes needs a discrete (RVQ) config");
         stream_dec(s, idx, y, noise_u, as_stream(stream));
     });
+}
+
+// kernel launches of one block: the kernel nodes of the captured graph (graph
+// mode; the two staging copies around a replay are not counted) or the plan's
+// ops (eager mode); which 0 = encode, 1 = decode
+extern "C" int rave_stream_launches(const rave_stream* h, int which) {
+    int n = 0;
+    int rc = guarded([&] {
+        Stream* s = stream_of(const_cast<rave_stream*>(h));
+        if (which != 0 && which != 1) fail(RAVE_ERR_ARG, "which must be 0 (encode) or 1 (decode)");
+        if (which == 0 ? !s->has_enc() : !s->has_dec()) fail(RAVE_ERR_STATE, "stream has no such direction");
+        hipGraph_t g = which == 0 ? s->enc_graph : s->dec_graph;
+        if (!g) {
+            n = (int)(which == 0 ? s->enc : s->dec)->ops.size();
+            return;
+        }
+        size_t cnt = 0;
+        RAVE_HIP_OR_THROW(hipGraphGetNodes(g, nullptr, &cnt));
+        std::vector<hipGraphNode_t> nodes(cnt);
+        RAVE_HIP_OR_THROW(hipGraphGetNodes(g, nodes.data(), &cnt));
+        for (size_t i = 0; i < cnt; ++i) {
+            hipGraphNodeType t;
+            RAVE_HIP_OR_THROW(hipGraphNodeGetType(nodes[i], &t));
+            n += t == hipGraphNodeTypeKernel ? 1 : 0;
+        }
+    });
+    return rc == RAVE_OK ? n : rc;
 }
 
 extern "C" int rave_stream_delay(const rave_stream* h) {

@@ -66,7 +66,7 @@ __device__ unsigned long long* g_ss_stamps = nullptr;
     } while (0)
 #endif
 constexpr unsigned kSSOOB = 0xFFFFFFF0u;
-constexpr int kSSBfHalo = 24;
+constexpr int kSSBfHalo = kStackBf3Halo;
 #ifndef RAVE_SS_BF_R
 #define RAVE_SS_BF_R 2
 #endif                          // bf16x3: plane rows beyond the extended range, per side
@@ -612,7 +612,7 @@ extern "C" int rave_residual_stack(const rave_stack_args* p, void* stream) {
             return RAVE_ERR_UNSUPPORTED;
         }
     }
-    if (reach_l > 32 || reach_r > 32) {
+    if (reach_l > kStackMargin || reach_r > kStackMargin) {
         set_error("residual_stack: units 2..3 reach past the 32-column margin (run the units separately)");
         return RAVE_ERR_UNSUPPORTED;
     }

@@ -112,6 +112,7 @@ __device__ unsigned long long* g_us_stamps = nullptr;
 constexpr unsigned kUSOOB = 0xFFFFFFF0u;
 constexpr int kXcds = 8;                      // gfx950: blocks dealt round-robin over 8 XCDs
 constexpr int kCoopNoFit = 1;                 // us_launch: a group does not fit one XCD
+constexpr int kCoopMaxRB = 4;                 // largest cooperative group (C = 512 / 128)
 
 struct USArgs {
     const float* x; float* y; const float* w; const float* rs1; const float* rs2;
@@ -216,8 +217,21 @@ __device__ __forceinline__ bool unit_split_body(const USArgs& a) {
     using G = USGeo<C, WGN, MI, KG, CB, RB, NPW>;
     // cooperative form with one workgroup per CU (its LDS rules out a second):
     // the hand-off reads the exchange by sc1 loads instead of an agent acquire
-    // (RAVE_COOP_SC1=0 keeps the acquire: A/B)
+    // (RAVE_COOP_SC1=0 keeps the acquire: A/B).  What this rests on is the
+    // guide's measured form (MI355X_MICROARCH.md, Valid forms, Consumer bullet
+    // (1)-(4), hand-off table row 1), every condition of which holds here:
+    // every byte of the exchange is stored sc1 (the seam's publish) and read
+    // only by sc1 buffer loads (stage_rows); each storing wave drains with
+    // vmcnt(0) before the workgroup barrier behind which ONE lane adds to the
+    // group's counter; ONE wave polls it with sc1 loads and the others load
+    // behind the barrier it then joins; hipMalloc'd workspace; one workgroup per
+    // CU (the predicate's LDS test).  Row 1 does not need the members on one
+    // XCD: the XCD-local dealing in us_launch (blocks b, b + 8, ... of a group)
+    // is for speed (the exchange stays in one L2) and for residency, not for
+    // visibility.  Forms with two workgroups per CU (split16 C = 256) keep the
+    // agent acquire, so both paths stay covered by the cooperative tests.
     constexpr bool SC1X = RB > 1 && RAVE_COOP_SC1 != 0 && 2 * G::LDS > 160 * 1024;
+    static_assert(!SC1X || 2 * G::LDS > 160 * 1024, "sc1 hand-off: one workgroup per CU only");
     constexpr bool GV = GUARD && AR == 0 && RAVE_SPLIT_GUARD != 0;   // votes inside the body
     static_assert(RB == 1 || GUARD || AR != 0, "the cooperative split16 form runs guarded");
     constexpr int NT = G::NT, PH = G::PH, G8 = G::G8, XT = G::XT, R = G::R;
@@ -1008,6 +1022,14 @@ static int us_launch(USArgs k, int B, bool snake, int ar, hipStream_t st) {
         // delay (they finish unconditionally).  So the cooperative form runs
         // only where slots per XCD >= Q (RB - 1) + RB; else the caller runs the
         // one-workgroup form.  (Other processes sharing the GPU are not counted.)
+        // Assumptions, stated: each hardware queue runs one kernel at a time
+        // toward this bound (HIP sets the AQL barrier bit on every dispatch of a
+        // stream), and the Q launches may be DIFFERENT cooperative kernels with
+        // different footprints (C = 256 RB = 2 beside C = 512 RB = 4, split16 /
+        // bf16x3 / fp32): a foreign partial group is charged a whole CU per member
+        // (the most one workgroup can hold) with the largest group size of any
+        // instantiation, kCoopMaxRB -- the second condition below.  Both hold on
+        // MI355X by a wide margin (C = 512: 32 >= 16 slots and 32 >= 16 CUs).
         static int fits[6] = {-1, -1, -1, -1, -1, -1};
         int& f = fits[2 * ar + snake];
         if (f < 0) {
@@ -1016,7 +1038,9 @@ static int us_launch(USArgs k, int B, bool snake, int ar, hipStream_t st) {
                                                                         G::NT, lds));
             RAVE_CHECK_HIP(hipGetDevice(&dev));
             RAVE_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            f = (int64_t)per_cu * (cus / kXcds) >= (int64_t)coop_max_queues() * (RB - 1) + RB ? 1 : 0;
+            const int64_t q = coop_max_queues();
+            f = ((int64_t)per_cu * (cus / kXcds) >= q * (RB - 1) + RB &&
+                 (int64_t)(cus / kXcds) >= q * (kCoopMaxRB - 1) + RB) ? 1 : 0;
         }
         if (!f) return kCoopNoFit;
         k.ngroups = grid;

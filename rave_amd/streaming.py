@@ -144,3 +144,11 @@ class StreamingRAVE:
     def decode_delay(self) -> int:
         """Samples by which streamed decoding lags one-shot decoding."""
         return int(N.lib.rave_stream_delay(self.handle))
+
+    def launches(self, which: str = "decode") -> int:
+        """Kernel launches of one block ("encode" or "decode"): the captured
+        graph's kernel nodes (graph mode) or the plan's ops (eager)."""
+        n = int(N.lib.rave_stream_launches(self.handle, {"encode": 0, "decode": 1}[which]))
+        if n < 0:
+            N.check(n, "stream_launches")
+        return n
