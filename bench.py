@@ -57,10 +57,12 @@ PEAK_F16_TFLOPS = 2516.6      # MI355X dense F16 MFMA (256 CU x 4 SIMD x 1024 FL
 PEAK_SPLIT16_TFLOPS = round(PEAK_F16_TFLOPS / 3, 1)
 # bf16x3 issues six bf16 MFMAs per fp32 multiply-accumulate (bf16 peak = f16 peak)
 PEAK_BF3_TFLOPS = round(PEAK_F16_TFLOPS / 6, 1)
-# the bf16x3 decoder tail mixes two roofs: its conv (64 -> 32, k7: 14336 MACs per
-# frame) at the bf16x3 peak and the synthesis (16 x 16 x 33: 8448 MACs per frame)
-# at the fp32 peak; its ceiling is the FLOP-weighted harmonic mean of the two
-PEAK_TAIL_BF3_TFLOPS = round((14336 + 8448) / (14336 / PEAK_BF3_TFLOPS + 8448 / PEAK_FP32_TFLOPS), 1)
+# (the bf16x3 decoder tail, since round 6 bf16x3 in its conv AND its synthesis,
+# has the bf16x3 roof; round 5's tail mixed in an exact-fp32 synthesis)
+# the bf16x3 encoder head mixes two roofs: its analysis (6 bands x 513 taps = 3078 MACs
+# per frame) at the bf16x3 peak, its conv (64 x 6 x 7 = 2688 MACs per frame) at the fp32
+# peak; its ceiling is the FLOP-weighted harmonic mean of the two
+PEAK_HEAD_BF3_TFLOPS = round((3078 + 2688) / (3078 / PEAK_BF3_TFLOPS + 2688 / PEAK_FP32_TFLOPS), 1)
 SR = 48000
 
 # GEMM-shaped kernel families of a step: name -> (kernels, peak in fp32-op TFLOP/s).
@@ -95,7 +97,10 @@ FAMILIES = {
     "tail_f32": ("decoder_tail_kernel<F32>: GeneratorV2's last conv + epilogue + PQMF synthesis, exact fp32 "
                  "MFMA 32x32x2 / 16x16x4", PEAK_FP32_TFLOPS),
     "tail_bf16x3": ("decoder_tail_kernel<BF16X3>: GeneratorV2's last conv in bf16x3 (bf16 MFMA 32x32x16, 6 per fp32 "
-                    "MAC) + epilogue + PQMF synthesis in exact fp32 (MFMA 16x16x4)", PEAK_TAIL_BF3_TFLOPS),
+                    "MAC) + epilogue + PQMF synthesis in bf16x3 (MFMA 16x16x32, 6 per fp32 MAC; round 6)",
+                    PEAK_BF3_TFLOPS),
+    "head_bf16x3": ("encoder_head_kernel<BF16X3>: PQMF analysis (phase-packed) in bf16x3 (bf16 MFMA 16x16x32, 6 per "
+                    "fp32 MAC) + EncoderV2's first conv in exact fp32 (MFMA 32x32x2)", PEAK_HEAD_BF3_TFLOPS),
 }
 
 
@@ -115,7 +120,7 @@ def op_family(kind: int, precision: int) -> str:
     if kind == N.OP_PQMF_SYNTHESIS:
         return "pqmf_synthesis_" + prec
     if kind == N.OP_HEAD:
-        return "head_" + prec
+        return "head_bf16x3" if precision == N.PREC_BF16X3 else "head_" + prec
     if kind == N.OP_TAIL:
         return "tail_bf16x3" if precision == N.PREC_BF16X3 else "tail_" + prec
     return "other"

@@ -442,8 +442,11 @@ int rave_residual_stack(const rave_stack_args* a, void* stream);
  * precision RAVE_PREC_F32_RING: exact fp32 (v_mfma_f32_16x16x4 / 32x32x2) with the
  * conv's rave_conv1d_ring_pack_weight image and a *_pack_filter_f32 filter image.
  * rave_decoder_tail also takes RAVE_PREC_BF16X3 (round 5): the conv in bf16x3 (its
- * rave_conv1d_bf3_pack_weight image), the synthesis in exact fp32 (the
- * rave_decoder_tail_pack_filter_f32 image).
+ * rave_conv1d_bf3_pack_weight image), the synthesis (since round 6) in bf16x3 too,
+ * split in-kernel from the rave_decoder_tail_pack_filter_f32 image.
+ * rave_encoder_head takes RAVE_PREC_BF16X3 (round 6, ABI 18): the analysis in
+ * bf16x3 (split in-kernel from the rave_encoder_head_pack_filter_f32 image), the
+ * conv in exact fp32 (the rave_conv1d_ring_pack_weight image).
  */
 typedef struct rave_edge_args {
     int32_t batch, frames;          /* PQMF frames (audio samples / 16)                    */

@@ -724,6 +724,83 @@ __device__ __forceinline__ void conv1d_split_body(const ConvKArgs& a) {
     stamp_sum(5, acc_ww);
     stamp_sum(6, acc_we);
 #endif
+#ifndef RAVE_CONV_KGPAR
+#define RAVE_CONV_KGPAR 1
+#endif
+    if constexpr (KG >= 2 && RAVE_CONV_KGPAR != 0) {
+        // Plain output (no ConvT interleave, no split-K slab, aligned rows), round 6:
+        // every K-group parks its partial tile in LDS in the row-major layout the
+        // stores read, and every wave -- not only group 0 -- finishes 1/KG of its
+        // tile's rows: the partials summed in group order (((p0 + p1) + p2) + p3,
+        // bitwise the group-0 reduction), row scale + bias, residual, 16-byte
+        // stores.  The reduction reads, residual loads and stores are spread over
+        // KG times as many waves.
+        if (!a.transposed && a.S == 1 && a.vec_y) {
+            constexpr int LPR = WN / 4;                  // lanes per row
+            constexpr int RPI = 64 / LPR;                // rows per instruction
+            constexpr int RW = WM / KG;                  // rows this wave finishes
+            static_assert(RW % RPI == 0, "K-group row shares");
+            const int rr = lane / LPR, cc = (lane % LPR) * 4;
+            const int n = n0 + wn * WN + cc;
+            const int rbase = kg * RW;
+            // row constants and residual of the wave's rows, in flight across the barriers
+            float rs_r[RW / RPI], bias_r[RW / RPI];
+            s_f32x4 rv[RW / RPI];
+            const __amdgpu_buffer_rsrc_t rrs = make_rsrc(a.res ? a.res + (int64_t)b * a.r_sb : a.y, a.res ? a.r_bytes : 0);
+#pragma unroll
+            for (int it = 0; it < RW / RPI; ++it) {
+                const int m = mw + rbase + it * RPI + rr;
+                rs_r[it] = m < a.Mpad ? a.rscale[m] : 0.f;
+                bias_r[it] = (a.bias && m < a.M) ? a.bias[m] : 0.f;
+                const bool ok = a.res && m < a.M && n + 3 < a.U;
+                rv[it] = __builtin_bit_cast(s_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                    rrs, ok ? (unsigned)(m * a.r_sc + n) * 4u : kOOB, 0, 0));
+            }
+            __syncthreads();                             // ring and planes dead
+            float* et = reinterpret_cast<float*>(smem) + wave * WM * G::EROW;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const s_f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                                           acc[i][j][4 * g + 3]};
+                        *reinterpret_cast<s_f32x4*>(et + (j * 32 + l32) * G::EROW + i * 32 + 8 * g + 4 * h) = v;
+                    }
+            __syncthreads();                             // every group's partial tile parked
+            const __amdgpu_buffer_rsrc_t yrs = make_rsrc(a.y + (int64_t)b * a.y_sb, a.y_bytes);
+#pragma unroll
+            for (int it = 0; it < RW / RPI; ++it) {
+                const int r = rbase + it * RPI + rr;
+                const int m = mw + r;
+                s_f32x4 v = *reinterpret_cast<const s_f32x4*>(reinterpret_cast<const float*>(smem) +
+                                                               (size_t)twave * WM * G::EROW + r * G::EROW + cc);
+#pragma unroll
+                for (int g = 1; g < KG; ++g)
+                    v += *reinterpret_cast<const s_f32x4*>(reinterpret_cast<const float*>(smem) +
+                                                           (size_t)(twave + g * NWT) * WM * G::EROW + r * G::EROW + cc);
+                v = v * rs_r[it] + bias_r[it];
+                if (m < a.M && n + 3 < a.U) {
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v + rv[it]), yrs,
+                                                           (unsigned)(m * a.y_sc + n) * 4u, 0, RAVE_YAUX);
+                } else {
+                    float vv[4];
+                    *reinterpret_cast<s_f32x4*>(vv) = v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const bool ok = m < a.M && n + e < a.U;
+                        const float rsd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                            rrs, ok ? (unsigned)(m * a.r_sc + n + e) * 4u : kOOB, 0, 0));
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, vv[e] + rsd), yrs,
+                                                              ok ? (unsigned)(m * a.y_sc + n + e) * 4u : kOOB, 0, RAVE_YAUX);
+                    }
+                }
+            }
+            stamp(4);
+            return;
+        }
+    }
     if constexpr (KG >= 2) {
         // groups 1.. hand their partial tiles to group 0 through LDS (ring and
         // planes are dead); group 0 adds them in group order (fixed: bitwise

@@ -147,23 +147,40 @@ __host__ __device__ constexpr int e_xi(int i) { return i + 8 * (i >> 7); }   // 
 constexpr int kHXP = e_xi(kHXS) + 8;                // halves per window plane
 constexpr int kHeadLds = (2 * 16 * kEdgeFP + 2 * kHXP + 2 * kHBR * kHBP) * 2 + 4 * kEdgeWaves * 4 + 16 +
                          kEdgeWaves * 64 * 4 * 4;        // + the split analysis block's partial sums
+// bf16x3 analysis (AR = 2, round 6): three bf16 planes of the filter and of the
+// audio window, the fp32 band planes and the exact-fp32 conv after them
+constexpr int kHeadBaBand = (3 * 16 * kEdgeFP + 3 * kHXP) * 2;   // bytes before the fp32 band planes
+static_assert(kHeadBaBand % 16 == 0, "band planes 16-byte aligned");
+constexpr int kHeadLdsBa = kHeadBaBand + kHBR * kHBP * 4 + 4 * kEdgeWaves * 4 + 16 + kEdgeWaves * 64 * 4 * 4;
 
-template <bool F32>
+// AR: 0 split-f16, 1 exact fp32, 2 bf16x3 analysis (fp32 on the bf16 matrix
+// cores: exact three-way split of the filter and of the audio, six
+// v_mfma_f32_16x16x32_bf16 per 32-deep K-step) with the exact-fp32 conv
+template <int AR>
 __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a, EdgeGeo geo) {
+    constexpr bool FC = AR != 0;                     // exact-fp32 band planes and conv
+    constexpr bool F32 = AR == 1, BA = AR == 2;      // analysis: exact fp32 / bf16x3
     const int tiles = geo.tiles;
     extern __shared__ __attribute__((aligned(16))) char e_smem[];
     _Float16* fh = reinterpret_cast<_Float16*>(e_smem);          // [16][kEdgeFP]
     _Float16* fl = fh + 16 * kEdgeFP;
     _Float16* xh = fl + 16 * kEdgeFP;                              // [kHXP] flat, padded
     _Float16* xl = xh + kHXP;
-    _Float16* bh = xl + kHXP;                                      // [kHBR][kHBP]
+    _Float16* bh = BA ? reinterpret_cast<_Float16*>(e_smem + kHeadBaBand) : xl + kHXP;   // [kHBR][kHBP]
     _Float16* bl = bh + kHBR * kHBP;
     float* red = reinterpret_cast<float*>(bl + kHBR * kHBP);
+    // BA: filter planes (hi, mid, lo) [16][kEdgeFP] and window planes (hi, mid, lo) [kHXP]
+    __bf16* gbh = reinterpret_cast<__bf16*>(e_smem);
+    __bf16* gbm = gbh + 16 * kEdgeFP;
+    __bf16* gbl = gbm + 16 * kEdgeFP;
+    __bf16* wbh = gbl + 16 * kEdgeFP;
+    __bf16* wbm = wbh + kHXP;
+    __bf16* wbl = wbm + kHXP;
     float* part = red + 4 * kEdgeWaves + 4;                        // [waves][64 lanes][4] (after the votes)
     // F32: one fp32 plane in the bytes of each (hi, lo) pair
     float* ff = reinterpret_cast<float*>(fh);                     // [16][kEdgeFP]
     float* xf = reinterpret_cast<float*>(xh);                     // [kHXP] flat, padded
-    float* bf = reinterpret_cast<float*>(bh);                     // [kHBR][kHBP]
+    float* bf = reinterpret_cast<float*>(bh);                     // FC: [kHBR][kHBP]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nmain = tiles * a.batch;
@@ -191,8 +208,18 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     // split optimistically (no scale) with a per-wave range vote
     {
         const e_h8* src = reinterpret_cast<const e_h8*>(a.filter);
-        e_h8* dst = reinterpret_cast<e_h8*>(fh);
-        for (int i = tid; i < kEdgeFilterHalves / 8; i += kEdgeNT) dst[i] = src[i];
+        if constexpr (BA) {      // the exact-fp32 image, split into three bf16 planes on the way in
+            for (int i = tid; i < kEdgeFilterHalves / 8; i += kEdgeNT) {
+                e_b4 hi, mid, lo;
+                bf3_split_pk(__builtin_bit_cast(e_f32x4, src[i]), hi, mid, lo);
+                *reinterpret_cast<e_b4*>(gbh + 4 * i) = hi;
+                *reinterpret_cast<e_b4*>(gbm + 4 * i) = mid;
+                *reinterpret_cast<e_b4*>(gbl + 4 * i) = lo;
+            }
+        } else {
+            e_h8* dst = reinterpret_cast<e_h8*>(fh);
+            for (int i = tid; i < kEdgeFilterHalves / 8; i += kEdgeNT) dst[i] = src[i];
+        }
     }
     const float f_unscale = a.filter[kEdgeFilterHalves / 2];        // 2^-(e + 11)
     constexpr int XT = (kHXS + kEdgeNT - 1) / kEdgeNT;             // 11
@@ -211,14 +238,25 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     for (int it = 0; it < XT; ++it) {
         const int i = tid + it * kEdgeNT;
         if (i < kHXS) {
-            if constexpr (F32) xf[e_xi(i)] = xv[it];
-            else e_split(xv[it], xh[e_xi(i)], xl[e_xi(i)]);
+            if constexpr (BA) {
+                const float v = xv[it];
+                const __bf16 hi = (__bf16)v;
+                const float r = v - (float)hi;
+                const __bf16 mid = (__bf16)r;
+                wbh[e_xi(i)] = hi;
+                wbm[e_xi(i)] = mid;
+                wbl[e_xi(i)] = (__bf16)(r - (float)mid);
+            } else if constexpr (F32) {
+                xf[e_xi(i)] = xv[it];
+            } else {
+                e_split(xv[it], xh[e_xi(i)], xl[e_xi(i)]);
+            }
         }
     }
-    if constexpr (!F32) vote_cast(vote, wave, xmax);
+    if constexpr (AR == 0) vote_cast(vote, wave, xmax);
     // band-plane channels 8..15 stay zero (the conv chunk is 16 channels wide)
     for (int i = tid; i < kHBR; i += kEdgeNT) {
-        if constexpr (F32) {
+        if constexpr (FC) {
             *reinterpret_cast<e_f32x4*>(bf + i * kHBP + 8) = e_f32x4{0.f, 0.f, 0.f, 0.f};
             *reinterpret_cast<e_f32x4*>(bf + i * kHBP + 12) = e_f32x4{0.f, 0.f, 0.f, 0.f};
         } else {
@@ -228,7 +266,7 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     }
     __syncthreads();
     float xs = 1.f;
-    if (!F32 && __builtin_expect(vote_any<kEdgeWaves>(vote), 0)) {
+    if (AR == 0 && __builtin_expect(vote_any<kEdgeWaves>(vote), 0)) {
         // rare: audio at 2^15 or beyond -- the window again as x 2^-s
         xs = ldexpf(1.f, -__builtin_amdgcn_readfirstlane(split_shift(block_max<kEdgeWaves>(xmax, red))));
 #pragma unroll
@@ -243,8 +281,31 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     // ---- analysis: block blk, column n = frame pair (frames 32 blk + 2n + p)
     const int g = lane >> 4, col = lane & 15;
     // three independent accumulator chains (one per product), summed at the end
+    // BA: the six bf16 products of one 32-deep K-step, smallest first (A = filter
+    // part, B = audio part): lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi
+    auto ba_step = [&](int blk, int s, e_f32x4& c) __attribute__((always_inline)) {
+        const int ka = col * kEdgeFP + 32 * s + 8 * g;
+        const int xi = e_xi(512 * blk + 32 * col + 32 * s + 8 * g);
+        const e_b8 fh8 = *reinterpret_cast<const e_b8*>(gbh + ka), fm8 = *reinterpret_cast<const e_b8*>(gbm + ka),
+                   fl8 = *reinterpret_cast<const e_b8*>(gbl + ka);
+        const e_b8 xh8 = *reinterpret_cast<const e_b8*>(wbh + xi), xm8 = *reinterpret_cast<const e_b8*>(wbm + xi),
+                   xl8 = *reinterpret_cast<const e_b8*>(wbl + xi);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl8, xh8, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh8, xl8, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm8, xm8, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm8, xh8, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh8, xm8, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh8, xh8, c, 0, 0, 0);
+    };
     auto analysis_block = [&](int blk, e_f32x4& acc) __attribute__((always_inline)) {
         e_f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0;
+        if constexpr (BA) {
+            // two chains (even / odd K-steps), summed at the end
+#pragma unroll
+            for (int s = 0; s < kEdgeKW / 32; ++s) ba_step(blk, s, (s & 1) ? c1 : c0);
+            acc = c0 + c1;
+            return;
+        }
         if constexpr (F32) {
 #pragma unroll
             for (int s = 0; s < kEdgeKW / 32; ++s) {
@@ -281,7 +342,9 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
         for (int j = 0; j < (kEdgeKW / 32 + kEdgeWaves - 1) / kEdgeWaves; ++j) {
             const int s = s0 + kEdgeWaves * j;
             if (s >= kEdgeKW / 32) break;               // (wave-uniform)
-            if constexpr (F32) {
+            if constexpr (BA) {
+                ba_step(blk, s, c0);
+            } else if constexpr (F32) {
                 const e_f32x8 af = e_ld8(ff + col * kEdgeFP + 32 * s + 8 * g);
                 const e_f32x8 xf8 = e_ld8(xf + e_xi(512 * blk + 32 * col + 32 * s + 8 * g));
 #pragma unroll
@@ -343,7 +406,7 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     }
     auto put_bands = [&](int blk, const e_f32x4& v, float bs) __attribute__((always_inline)) {
         const int row = 32 * blk + 2 * col + (g >> 1);
-        if constexpr (F32) {
+        if constexpr (FC) {
             *reinterpret_cast<e_f32x4*>(bf + row * kHBP + 4 * (g & 1)) = v;
             return;
         }
@@ -371,10 +434,10 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
     // band planes split optimistically, with a range vote (rare: a rescale by 2^-s)
     put_bands(wave, v0, 1.f);
     if (extra) put_bands(wave + kEdgeWaves, v1, 1.f);
-    if constexpr (!F32) vote_cast(vote + 8, wave, bmax);
+    if constexpr (AR == 0) vote_cast(vote + 8, wave, bmax);
     __syncthreads();
     float bs = 1.f;
-    if (!F32 && __builtin_expect(vote_any<kEdgeWaves>(vote + 8), 0)) {
+    if (AR == 0 && __builtin_expect(vote_any<kEdgeWaves>(vote + 8), 0)) {
         bs = ldexpf(1.f, -__builtin_amdgcn_readfirstlane(split_shift(block_max<kEdgeWaves>(bmax, red))));
         put_bands(wave, v0, bs);
         if (extra) put_bands(wave + kEdgeWaves, v1, bs);
@@ -392,7 +455,7 @@ __global__ __launch_bounds__(kEdgeNT) void encoder_head_kernel(rave_edge_args a,
 #pragma unroll
     for (int q = 0; q < kEdgeK7; ++q) {
         const int row = 32 * wave + l32 + q;
-        if constexpr (F32) {
+        if constexpr (FC) {
             // K pairs of input channels (2e, 2e + 1) on the two lane halves: ceil(c_in / 2)
             // MFMAs per tap instead of 8 (the image's lane half 1 holds channels 8-15, all
             // zero for the <= 8 bands here; lane half 0 holds channels 0-7)
@@ -476,13 +539,26 @@ constexpr int kTailBfFilt = 61440;
 constexpr int kTailLdsBf = kTailBfX + 2 * kEdgeWaves * 4 + 16;
 static_assert(kTailBfFilt >= 2 * kTSW * kTSP * 2 + kEdgeWaves * 16 * 64 * 4 &&
               kTailBfFilt + 16 * kEdgeFP * 4 <= kTailBfX, "bf16x3 tail LDS reuse");
+// bf16x3 synthesis (RAVE_TAIL_BF3_SYN, round 6): the synthesis on the bf16
+// matrix cores too -- three bf16 planes of the synthesis input at 0, the K-split
+// partial tiles after them, the filter's three bf16 planes at kTailBsFilt (split
+// in-kernel from the exact fp32 image); six v_mfma_f32_16x16x32_bf16 per 32-deep
+// K-step instead of eight v_mfma_f32_16x16x4_f32 per 4-deep one
+#ifndef RAVE_TAIL_BF3_SYN
+#define RAVE_TAIL_BF3_SYN 1
+#endif
+constexpr int kTailBsFilt = 75776;
+static_assert(kTailBsFilt >= 3 * kTSW * kTSP * 2 + kEdgeWaves * 16 * 64 * 4 &&
+              kTailBsFilt + 3 * 16 * kEdgeFP * 2 <= kTailBfX, "bf16x3 synthesis LDS reuse");
 
 // AR: 0 split-f16, 1 exact fp32, 2 bf16x3 conv (fp32 on the bf16 matrix cores,
 // exact three-way operand split, six bf16 MFMAs per 16-deep K-step) with the
 // exact-fp32 synthesis
 template <bool SNAKE, bool AM, int AR>
 __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a, EdgeGeo geo) {
-    constexpr bool F32 = AR == 1, BF = AR == 2, FS = AR != 0;   // FS: fp32 synthesis stage
+    constexpr bool F32 = AR == 1, BF = AR == 2;
+    constexpr bool BS = BF && RAVE_TAIL_BF3_SYN != 0;            // BS: bf16x3 synthesis stage
+    constexpr bool FS = AR != 0 && !BS;                          // FS: exact-fp32 synthesis stage
     const int tiles = geo.tiles;
     extern __shared__ __attribute__((aligned(16))) char e_smem[];
     _Float16* fh = reinterpret_cast<_Float16*>(e_smem);          // [16][kEdgeFP] synthesis filter
@@ -497,6 +573,13 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
     float* ff = reinterpret_cast<float*>(BF ? e_smem + kTailBfFilt : e_smem);   // FS: [16][kEdgeFP]
     float* xf = reinterpret_cast<float*>(xh);                     // F32: [kTXR][kTXP] act(x)
     float* sf = xf;                                                // FS: [kTSW][kTSP] (after the conv)
+    // BS: synthesis input planes [kTSW][kTSP] (hi, lo, mid) and filter planes [16][kEdgeFP] (hi, mid, lo)
+    __bf16* sbh = reinterpret_cast<__bf16*>(xh);
+    __bf16* sbl = sbh + kTSW * kTSP;
+    __bf16* sbm = sbl + kTSW * kTSP;
+    __bf16* fbh = reinterpret_cast<__bf16*>(e_smem + kTailBsFilt);
+    __bf16* fbm = fbh + 16 * kEdgeFP;
+    __bf16* fbl = fbm + 16 * kEdgeFP;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nmain = tiles * a.batch;
@@ -674,7 +757,19 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
     acc += acl;
     acc_x += acl_x;
     __syncthreads();                                 // act(x) planes dead
-    if constexpr (BF) {                              // the fp32 filter into its place (read after the epilogue's barrier)
+    if constexpr (BS) {                              // the filter as three bf16 planes (read after the epilogue's barrier)
+#pragma unroll
+        for (int i = 0; i < FQ; ++i) {
+            const int k = tid + i * kEdgeNT;
+            if (k < kEdgeFilterHalves / 8) {
+                e_b4 hi, mid, lo;
+                bf3_split_pk(__builtin_bit_cast(e_f32x4, fq[i]), hi, mid, lo);
+                *reinterpret_cast<e_b4*>(fbh + 4 * k) = hi;
+                *reinterpret_cast<e_b4*>(fbm + 4 * k) = mid;
+                *reinterpret_cast<e_b4*>(fbl + 4 * k) = lo;
+            }
+        }
+    } else if constexpr (BF) {                       // the fp32 filter into its place (read after the epilogue's barrier)
         e_h8* dst = reinterpret_cast<e_h8*>(ff);
 #pragma unroll
         for (int i = 0; i < FQ; ++i) {
@@ -684,7 +779,7 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
     }
     // the K-split blocks' partial tiles -> LDS (past the synthesis planes), summed
     // in chunk order by waves 0 (block 8) and 4 (block 9)
-    float* part = reinterpret_cast<float*>(xh + 2 * kTSW * kTSP);
+    float* part = reinterpret_cast<float*>(xh + (BS ? 3 : 2) * kTSW * kTSP);
 #pragma unroll
     for (int r = 0; r < 16; ++r) part[(wave * 16 + r) * 64 + lane] = acc_x[r];
     __syncthreads();
@@ -733,8 +828,19 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
             out = 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * out) + 1.0f);
             if ((c_out & 1) && !(f & 1)) out = -out;
             if (w < kTSW) {
-                if constexpr (FS) sf[w * kTSP + c_out] = ok ? out : 0.f;
-                else e_split(ok ? out : 0.f, sh[w * kTSP + c_out], sl[w * kTSP + c_out]);
+                if constexpr (BS) {
+                    const float v = ok ? out : 0.f;
+                    const __bf16 hi = (__bf16)v;
+                    const float r = v - (float)hi;
+                    const __bf16 mid = (__bf16)r;
+                    sbh[w * kTSP + c_out] = hi;
+                    sbm[w * kTSP + c_out] = mid;
+                    sbl[w * kTSP + c_out] = (__bf16)(r - (float)mid);
+                } else if constexpr (FS) {
+                    sf[w * kTSP + c_out] = ok ? out : 0.f;
+                } else {
+                    e_split(ok ? out : 0.f, sh[w * kTSP + c_out], sl[w * kTSP + c_out]);
+                }
             }
         }
     };
@@ -754,6 +860,26 @@ __global__ __launch_bounds__(kEdgeNT) void decoder_tail_kernel(rave_edge_args a,
     for (int s = 0; s < kEdgeKW / 32; ++s) {
         const int ka = col * kEdgeFP + 32 * s + 8 * g;
         const int tap = 2 * s + (g >> 1);
+        if constexpr (BS) {
+            // smallest products first (A = filter part, B = signal part): lo*hi, hi*lo,
+            // mid*mid, mid*hi, hi*mid, hi*hi
+            const e_b8 fh8 = *reinterpret_cast<const e_b8*>(fbh + ka), fm8 = *reinterpret_cast<const e_b8*>(fbm + ka),
+                       fl8 = *reinterpret_cast<const e_b8*>(fbl + ka);
+#pragma unroll
+            for (int q = 0; q < BLK; ++q) {
+                const int xi = (fb + 16 * q + col + tap) * kTSP + 8 * (g & 1);
+                const e_b8 bh8 = *reinterpret_cast<const e_b8*>(sbh + xi), bm8 = *reinterpret_cast<const e_b8*>(sbm + xi),
+                           bl8 = *reinterpret_cast<const e_b8*>(sbl + xi);
+                e_f32x4 c = sacc[q];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl8, bh8, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh8, bl8, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm8, bm8, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm8, bh8, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh8, bm8, c, 0, 0, 0);
+                sacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh8, bh8, c, 0, 0, 0);
+            }
+            continue;
+        }
         if constexpr (FS) {
             const e_f32x8 af = e_ld8(ff + ka);
 #pragma unroll
@@ -906,8 +1032,8 @@ static int edge_prec(const rave_edge_args& a, bool& f32, bool allow_bf3 = false)
     f32 = a.precision == RAVE_PREC_F32_RING;
     if (a.precision != 0 && a.precision != RAVE_PREC_SPLIT16 && !f32 &&
         !(allow_bf3 && a.precision == RAVE_PREC_BF16X3)) {
-        set_error(allow_bf3 ? "decoder_tail: precision must be RAVE_PREC_SPLIT16, RAVE_PREC_F32_RING or RAVE_PREC_BF16X3"
-                            : "encoder_head: precision must be RAVE_PREC_SPLIT16 or RAVE_PREC_F32_RING");
+        set_error(allow_bf3 ? "edge: precision must be RAVE_PREC_SPLIT16, RAVE_PREC_F32_RING or RAVE_PREC_BF16X3"
+                            : "edge: precision must be RAVE_PREC_SPLIT16 or RAVE_PREC_F32_RING");
         return RAVE_ERR_ARG;
     }
     return RAVE_OK;
@@ -928,16 +1054,20 @@ extern "C" int rave_encoder_head(const rave_edge_args* p, void* stream) {
         set_error("encoder_head: the fused analysis + first conv applies no input activation (act must be RAVE_ACT_NONE)");
         return RAVE_ERR_UNSUPPORTED;
     }
+    // RAVE_PREC_BF16X3: the analysis in bf16x3, the conv in exact fp32 (the
+    // exact-fp32 filter image and the ring weight image, as RAVE_PREC_F32_RING)
     bool f32;
-    int rc = edge_prec(a, f32);
+    int rc = edge_prec(a, f32, true);
     if (rc != RAVE_OK) return rc;
+    const int ar = a.precision == RAVE_PREC_BF16X3 ? 2 : f32 ? 1 : 0;
     const EdgeGeo g = edge_geometry(a, kHF);
-    static bool attr[2] = {false, false};
-    auto kern = f32 ? encoder_head_kernel<true> : encoder_head_kernel<false>;
-    rc = edge_lds_attr(kern, kHeadLds, attr[f32]);
+    static bool attr[3] = {false, false, false};
+    auto kern = ar == 2 ? encoder_head_kernel<2> : ar == 1 ? encoder_head_kernel<1> : encoder_head_kernel<0>;
+    const int lds = ar == 2 ? kHeadLdsBa : kHeadLds;
+    rc = edge_lds_attr(kern, lds, attr[ar]);
     if (rc != RAVE_OK) return rc;
     const int grid = g.tiles * a.batch;
-    launch(kern, dim3(grid), dim3(kEdgeNT), (uint32_t)kHeadLds, as_stream(stream), a, g);
+    launch(kern, dim3(grid), dim3(kEdgeNT), (uint32_t)lds, as_stream(stream), a, g);
     return launch_status("encoder_head_kernel");
 }
 

@@ -428,6 +428,8 @@ struct Model {
     // PQMF + edge-conv fusions (csrc/edge_split.hip), split-f16 only
     rave_edge_args head_desc(int B, int F) const;
     bool use_head(int B, int T);
+    int head_pick(int B, int T);
+    bool head_ok(int ep, int B, int T);
     void head_op(Plan& p, int B, int T, const View& x, const View& y, const View* fill_z);
     rave_edge_args tail_desc(int B, int F) const;
     bool use_tail(int B, int F);
@@ -1262,13 +1264,37 @@ static bool edges_enabled() {
     return !(e && e[0] == '0');
 }
 
-bool Model::use_head(int B, int T) {
-    const int ep = edge_prec();
-    const int64_t filt = ep == RAVE_PREC_F32_RING ? head_filt32_off : head_filt_off;
+// the fused head's arithmetic for (B, T), or -1 for the two separate ops: the
+// model's edge arithmetic, and in f32_bf3 models also the bf16x3 analysis form
+// (exact-fp32 conv), whichever is timed faster
+int Model::head_pick(int B, int T) {
+    std::vector<int> cands = {edge_prec()};
+    if (edge_prec() == RAVE_PREC_F32_RING && std::find(precs.begin(), precs.end(), (int)RAVE_PREC_BF16X3) != precs.end())
+        cands.push_back(RAVE_PREC_BF16X3);
+    int best = -1;
+    double bms = 1e30;
+    for (int ep : cands) {
+        if (!head_ok(ep, B, T)) continue;
+        const double ms = tuned.at(key_of({"head", std::to_string(ep), std::to_string(B), std::to_string(T)})).second;
+        if (best < 0 || ms < bms) {
+            best = ep;
+            bms = ms;
+        }
+    }
+    return best;
+}
+
+bool Model::use_head(int B, int T) { return head_pick(B, T) >= 0; }
+
+// the head's conv weight image: the ring image for the exact-fp32 and bf16x3 forms
+static int head_wprec(int ep) { return ep == RAVE_PREC_BF16X3 ? RAVE_PREC_F32_RING : ep; }
+
+bool Model::head_ok(int ep, int B, int T) {
+    const int64_t filt = ep == RAVE_PREC_SPLIT16 ? head_filt_off : head_filt32_off;
     if (!edges_enabled() || ep < 0 || filt < 0) return false;
     const Node& n = g.encoder.front();
     const int F = T / cfg.n_band;
-    if (!w_pack.count({n.name, ep})) return false;
+    if (!w_pack.count({n.name, head_wprec(ep)})) return false;
     if (cfg.n_band != 16 || n.kernel != 7 || n.stride != 1 || n.dilation != 1 || n.act != RAVE_ACT_NONE ||
         n.transposed || n.c_in > 8 || n.c_out > 64 || !n.adain.empty() || F * cfg.n_band != T)
         return false;
@@ -1282,7 +1308,7 @@ bool Model::use_head(int B, int T) {
         a.y = sc + nx + 64;
         a.y_sb = (int64_t)n.c_out * F;
         a.y_sc = F;
-        a.weight = aptr(w_pack.at({n.name, ep}));
+        a.weight = aptr(w_pack.at({n.name, head_wprec(ep)}));
         a.bias = n.bias ? aptr(bias_off.at(n.name)) : nullptr;
         a.filter = aptr(filt);
         a.precision = ep;
@@ -1338,13 +1364,14 @@ void Model::head_op(Plan& p, int B, int T, const View& x, const View& y, const V
         a.f_sb = fill_z->sb;
         a.f_sc = fill_z->sc;
     }
-    const int ep = edge_prec();
+    const int ep = head_pick(B, T);
+    if (ep < 0) fail(RAVE_ERR_STATE, "encoder head: no fused form for this shape");
     a.precision = ep;
     PlanOp& o = p.add(RAVE_OP_HEAD, a, "encoder_head:pqmf_analysis+" + n.name);
     rave_edge_args& A = *reinterpret_cast<rave_edge_args*>(o.op.u.raw);
-    View wv = arena_view(w_pack.at({n.name, ep}));
+    View wv = arena_view(w_pack.at({n.name, head_wprec(ep)}));
     View bv = n.bias ? arena_view(bias_off.at(n.name)) : View{};
-    View hv = arena_view(ep == RAVE_PREC_F32_RING ? head_filt32_off : head_filt_off);
+    View hv = arena_view(ep == RAVE_PREC_SPLIT16 ? head_filt_off : head_filt32_off);
     View sv = arena_view(spk_off);
     p.bind(o, A, A.x, &x);
     p.bind(o, A, A.y, &y);

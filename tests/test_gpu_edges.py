@@ -53,10 +53,13 @@ HEAD_CASES = [(600, 2, 1.0, 6), (4096, 3, 1.0, 6), (257, 1, 3e6, 6),
               (600, 2, 1.0, 5), (600, 1, 1.0, 8)]     # odd / full band counts: the fp32 conv's channel pairs
 
 
-@pytest.mark.parametrize("prec", ["split16", "f32_ring"])
+@pytest.mark.parametrize("prec", ["split16", "f32_ring", "bf16x3"])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("F,B,scale,nb", HEAD_CASES)
 def test_encoder_head(N, dev, golden, causal, F, B, scale, nb, prec):
+    """bf16x3 (round 6): the analysis on the bf16 matrix cores (filter and audio
+    split exactly into three bf16 parts), the conv in exact fp32 on the ring
+    image; held to the fp32-class bound as the bf16x3 tail."""
     from oracle.rave_oracle import conv1d, get_padding, reverse_half
     hkf, _ = _filters(golden)
     rng = np.random.default_rng(F + 7 * causal + nb)
@@ -70,13 +73,15 @@ def test_encoder_head(N, dev, golden, causal, F, B, scale, nb, prec):
     cpad = get_padding(k, causal=causal)
     ref = conv1d(bands, w.astype(np.float64), b.astype(np.float64), pad=cpad)
     P = N.PRECISION[prec]
-    packed = torch.from_numpy(N.pack_conv_weight(w, nb, co, k, 1, 1, 0, precision=P)).to(dev)
+    wprec = N.PREC_F32_RING if P == N.PREC_BF16X3 else P      # the bf16x3 head's conv: exact fp32, ring image
+    packed = torch.from_numpy(N.pack_conv_weight(w, nb, co, k, 1, 1, 0, precision=wprec)).to(dev)
     xd = torch.from_numpy(x).to(dev)
     y = torch.full((B, co, F), float("nan"), device=dev)
     spk = torch.from_numpy(rng.standard_normal(256).astype(np.float32)).to(dev)
     Fz = max(1, F // 64)
     z = torch.full((B, 320, Fz), float("nan"), device=dev)
-    hd = torch.from_numpy(N.pack_edge_filter(hkf, head=True, n_out_bands=nb, f32=P == N.PREC_F32_RING)).to(dev)
+    hd = torch.from_numpy(N.pack_edge_filter(hkf, head=True, n_out_bands=nb,
+                                             f32=P in (N.PREC_F32_RING, N.PREC_BF16X3))).to(dev)
     bd = torch.from_numpy(b).to(dev)
     a = N.EdgeArgs(batch=B, frames=F, conv_c_in=nb, conv_c_out=co, conv_kernel=k, conv_pad_left=cpad[0],
                    pqmf_taps=hkf.shape[-1], pqmf_pad_left=get_padding(hkf.shape[-1], causal=causal)[0],
@@ -90,6 +95,8 @@ def test_encoder_head(N, dev, golden, causal, F, B, scale, nb, prec):
     assert np.isfinite(got).all()
     err = maxabs(got, ref)
     assert err <= 2e-5 * float(np.abs(ref).max()), err
+    if prec == "bf16x3":                   # fp32-class arithmetic
+        assert err <= 2e-6 * max(1.0, float(np.abs(ref).max())), err
     zz = z.cpu().numpy()
     assert np.array_equal(zz[:, 64:], np.broadcast_to(spk.cpu().numpy()[None, :, None], (B, 256, Fz)))
     assert np.isnan(zz[:, :64]).all()            # the latent rows are the encoder's, untouched

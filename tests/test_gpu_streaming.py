@@ -241,6 +241,15 @@ def test_stream_direction_flags_and_row0(dev):
     full = StreamingRAVE(m, batch=1, block=2048)
     torch.cuda.synchronize()
     assert torch.equal(full.decode(full.encode(x)), y)
+    # rave_stream_launches (ABI 18): kernels per block; graph-captured kernel
+    # nodes cover the plan's ops (an op can add a split-K reduce), and a
+    # direction the stream lacks is refused
+    eager = StreamingRAVE(m, batch=1, block=2048, graph=False)
+    for w in ("encode", "decode"):
+        assert full.launches(w) >= eager.launches(w) >= 5
+    assert se.launches("encode") == full.launches("encode")
+    with pytest.raises(Exception):
+        se.launches("decode")
     # row0: learn on row 3 through the existing stream
     m.adain_row0 = 3
     m.adain.set_learn(learn_y=True)

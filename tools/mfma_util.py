@@ -60,9 +60,14 @@ def main(path, bench=None):
             # f16 MFMA passes per fp32 MAC: split16 3, bf16x3 6 (bf16 rate = f16 rate);
             # the fp32 MFMA runs at 1/16 of the f16 rate
             mult = 3.0 if f.endswith("split16") else 6.0 if f.endswith("bf16x3") else 16.0
-            if f == "tail_bf16x3":
-                # its conv (14336 MACs per frame) in bf16x3, its synthesis (8448) in fp32
+            if f == "tail_bf16x3" and d.get("tail_synthesis") == "f32":
+                # round 5's tail: its conv (14336 MACs per frame) in bf16x3, its synthesis
+                # (8448) in fp32 (since round 6 both in bf16x3: mult 6)
                 mult = (14336 * 6.0 + 8448 * 16.0) / (14336 + 8448)
+            if f == "head_bf16x3":
+                # its analysis (6 bands x 513 taps: 3078 MACs per frame) in bf16x3, its
+                # conv (64 x 6 x 7: 2688) in exact fp32
+                mult = (3078 * 6.0 + 2688 * 16.0) / (3078 + 2688)
             rec["expected_busy_per_launch"] = round(flop[f] * mult / FLOP_PER_SIMD_CYCLE)
             rec["busy_over_expected"] = round(busy[f] / n / rec["expected_busy_per_launch"], 3)
         out[f] = rec

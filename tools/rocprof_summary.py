@@ -43,6 +43,7 @@ FAMILIES = {
     "head_f32": ((), ()),
     "tail_f32": ((), ()),
     "tail_bf16x3": ((), ()),
+    "head_bf16x3": ((), ()),
 }
 _KERNEL_FAMILY = {}
 for _fam, (_mains, _helpers) in FAMILIES.items():
@@ -82,6 +83,7 @@ def kernel_name(demangled: str) -> str:
 
 
 _TAIL_AR = re.compile(r"decoder_tail_kernel<[^<>]*,\s*([012])>")
+_HEAD_AR = re.compile(r"encoder_head_kernel<\s*([012])\s*>")
 
 
 def classify(demangled: str):
@@ -93,6 +95,12 @@ def classify(demangled: str):
         m = _TAIL_AR.search(demangled)
         if m:
             return ({"0": "tail_split16", "1": "tail_f32", "2": "tail_bf16x3"}[m.group(1)], True)
+    if k == "encoder_head_kernel":
+        # round 6: the template argument is the arithmetic (0 split16, 1 exact fp32,
+        # 2 bf16x3 analysis + exact-fp32 conv); older builds had a bool there
+        m = _HEAD_AR.search(demangled)
+        if m:
+            return ({"0": "head_split16", "1": "head_f32", "2": "head_bf16x3"}[m.group(1)], True)
     return _KERNEL_FAMILY.get(k, (k, False))
 
 
