@@ -355,6 +355,10 @@ typedef struct rave_unit_args {
                            past x_len is padding (the one-shot form pads past t_len with zeros) */
     int32_t res_shift;  /* the residual of output column n is x column n + res_shift (0 one-shot;
                            cached: 2*dilation - the identity branch's delay, rave/blocks.py:32-46) */
+    int32_t coop_rb;    /* cooperative group size (ABI 18): 0 = C / 128 (2 at C = 256, 4 at 512);
+                           4 at C = 256 = the wide group (its weights stream through twice the
+                           CUs: short inputs, e.g. streaming blocks); workspace size depends on it */
+    int32_t reserved0;
 } rave_unit_args;
 int64_t rave_unit_packed_size(int channels);
 int rave_unit_pack_weight(const float* w1, const float* w2, int channels, float* packed);

@@ -139,7 +139,8 @@ class UnitArgs(C.Structure):
                 ("x", vp), ("x_sb", i64), ("x_sc", i64),
                 ("y", vp), ("y_sb", i64), ("y_sc", i64),
                 ("weight", vp), ("bias1", vp), ("bias2", vp), ("alpha0", vp), ("alpha2", vp),
-                ("workspace", vp), ("status", vp), ("x_len", i32), ("res_shift", i32)]
+                ("workspace", vp), ("status", vp), ("x_len", i32), ("res_shift", i32),
+                ("coop_rb", i32), ("reserved0", i32)]
 
 
 STACK_UNITS = 3

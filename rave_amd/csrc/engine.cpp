@@ -402,7 +402,7 @@ struct Model {
     void conv_op(Plan& p, const Node& n, int B, int t_in, const View& src, const View& dst, const View* res);
     double unit_time(const Node& k3, const Node& k1, int B, int T);
     int unit_pick(const Node& k3, int B, int T, bool timed);
-    bool unit_coop(const Node& k3, int B, int T);
+    int unit_coop(const Node& k3, int B, int T);
     bool fuse_unit(const Node& k3, const Node& k1, int B, int T);
     double unit_best_ms(const Node& k3, const Node& k1, int B, int T);
     rave_unit_args unit_desc(const Node& k3, const Node& k1, int B, int T, int prec) const;
@@ -720,6 +720,8 @@ int Model::unit_pick(const Node& k3, int B, int T, bool timed) {
         for (int pr : cands) {
             rave_unit_args q = unit_desc(k3, *k1, B, T, pr);
             nws = std::max(nws, rave_unit_workspace(&q));
+            q.coop_rb = 4;                                // the wide group at C = 256
+            nws = std::max(nws, rave_unit_workspace(&q));
         }
         float* sc = scratch_buf(2 * n_el + 128 + nws);
         float* ws = nws > 0 ? sc + 2 * n_el + 128 : nullptr;   // (64-float aligned)
@@ -733,8 +735,11 @@ int Model::unit_pick(const Node& k3, int B, int T, bool timed) {
             u.x_sb = u.y_sb = (int64_t)k3.c_in * T;
             u.x_sc = u.y_sc = T;
             // both forms where the cooperative one exists (one workgroup per slab /
-            // groups of workgroups sharing a slab): value = precision | coop << 8
-            for (int coop = 0; coop <= (rave_unit_workspace(&u) > 0 ? 1 : 0); ++coop) {
+            // groups of workgroups sharing a slab), and at C = 256 the wide group
+            // (coop 2: groups of 4, round 6): value = precision | coop << 8
+            const int ncoop = rave_unit_workspace(&u) > 0 ? (k3.c_in == 256 ? 2 : 1) : 0;
+            for (int coop = 0; coop <= ncoop; ++coop) {
+                u.coop_rb = coop == 2 ? 4 : 0;
                 u.workspace = coop ? ws : nullptr;
                 const double ms = time_native([&](hipStream_t st) { return rave_residual_unit(&u, st); });
                 if (ms >= 0 && ms < best) {
@@ -748,10 +753,11 @@ int Model::unit_pick(const Node& k3, int B, int T, bool timed) {
     return (int)tuned.at(key).first & 255;
 }
 
-bool Model::unit_coop(const Node& k3, int B, int T) {
+// the cooperative form the tuning chose: 0 none, 1 groups of C / 128, 2 the wide group
+int Model::unit_coop(const Node& k3, int B, int T) {
     const std::string key = key_of({"unit", k3.name, std::to_string(B), std::to_string(T)});
     auto it = tuned.find(key);
-    return it != tuned.end() && ((int)it->second.first >> 8) != 0;
+    return it != tuned.end() ? ((int)it->second.first >> 8) : 0;
 }
 
 // Residual(DilatedUnit) as the fused kernel (true) or as its two convs (false):
@@ -799,7 +805,9 @@ void Model::unit_op(Plan& p, const Node& k3, const Node& k1, int B, int T, const
     u.y_sc = dst.sc;
     const std::string label = k3.name.substr(0, k3.name.rfind(".net.")) + ".unit";
     // cooperative form (when timed faster): the plan's split-K buffer
-    const int64_t nws = unit_coop(k3, B, T) ? rave_unit_workspace(&u) : 0;
+    const int coop = unit_coop(k3, B, T);
+    u.coop_rb = coop == 2 ? 4 : 0;
+    const int64_t nws = coop ? rave_unit_workspace(&u) : 0;
     if (nws < 0) fail(RAVE_ERR_ARG, "unit " + k3.name + ": workspace query failed: " + rave_last_error());
     PlanOp& o = p.add(RAVE_OP_UNIT, u, label);
     rave_unit_args& U = *reinterpret_cast<rave_unit_args*>(o.op.u.raw);

@@ -1209,7 +1209,10 @@ static CoopLayout coop_layout(const rave_unit_args& a) {
     if (2 * ngp > RAVE_SPLITK_STATUS_WORD) return L;
     // a group's counters on a 128-byte line of their own where the words allow
     while (L.stride < 32 && 2 * L.stride * ngp <= RAVE_SPLITK_STATUS_WORD) L.stride *= 2;
-    const int rb = C / 128;
+    // group size: C / 128, or the wide group (coop_rb = 4 at C = 256: twice the CUs
+    // stream the slab's weights -- short inputs, where few slabs leave CUs idle)
+    const int rb = a.coop_rb == 4 && C == 256 ? 4 : C / 128;
+    if (a.coop_rb != 0 && a.coop_rb != rb) return L;      // (refused by residual_unit_split)
     L.groups = ng;
     L.xmax = RAVE_SPLITK_TICKETS;
     L.xch = L.xmax + ceil_div64(ngp * rb, 64) * 64;
@@ -1224,6 +1227,10 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
     if (!us_supported(C)) {
         set_error("residual_unit(split16): fused unit supports C in {64, 128, 256, 512}");
         return RAVE_ERR_UNSUPPORTED;
+    }
+    if (a.coop_rb != 0 && !((C == 256 && (a.coop_rb == 2 || a.coop_rb == 4)) || (C == 512 && a.coop_rb == 4))) {
+        set_error("residual_unit: coop_rb must be 0, or 2 / 4 at C = 256, 4 at C = 512");
+        return RAVE_ERR_ARG;
     }
     USArgs k{};
     k.x = a.x; k.y = a.y; k.w = a.weight;
@@ -1271,8 +1278,9 @@ int residual_unit_split(const rave_unit_args& a, void* stream) {
         k.xmax = a.workspace + L.xmax;
         k.xch = a.workspace + L.xch;
         k.xch_bytes = (int)((L.floats - L.xch) * 4);
-        const int rc = C == 256 ? go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<2>{})
-                                : go(IC<512>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<4>{});
+        const int rc = C == 512 ? go(IC<512>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<4>{})
+                       : L.rb == 4 ? go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<4>{})
+                                   : go(IC<256>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<1>{}, IC<2>{});
         if (rc != kCoopNoFit) return rc;
         // (a group does not fit one XCD: the one-workgroup form below)
     }

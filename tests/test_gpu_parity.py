@@ -986,12 +986,15 @@ def test_residual_unit_bf16x3_is_fp32_class(N, dev, case):
 
 
 COOP_CASES = [
-    # C, d, act, causal, B, T
+    # C, d, act, causal, B, T (C, rb: the wide group, coop_rb = 4 at C = 256, round 6)
     (256, 3, "leaky", False, 16, 256),
     (256, 9, "snake", True, 3, 77),
     (512, 3, "leaky", False, 16, 128),
     (512, 1, "snake", False, 2, 40),
     (512, 9, "leaky", True, 5, 333),
+    ((256, 4), 3, "leaky", False, 16, 256),
+    ((256, 4), 9, "snake", True, 3, 77),
+    ((256, 4), 1, "leaky", False, 1, 8),
 ]
 
 
@@ -1006,6 +1009,7 @@ def test_residual_unit_cooperative(N, dev, case, precision):
     gives up waiting (a give-up writes NaN)."""
     from oracle.rave_oracle import conv1d, leaky_relu, snake
     C, d, act, causal, B, T = case
+    C, rb = C if isinstance(C, tuple) else (C, 0)
     prec = N.PRECISION[precision]
     if precision == "f32_ring" and T % 4:
         pytest.skip("fp32 ring units need whole 16-byte rows")
@@ -1031,7 +1035,7 @@ def test_residual_unit_cooperative(N, dev, case, precision):
                           y_sb=C * T, y_sc=T, weight=packed.data_ptr(), bias1=dd["b1"].data_ptr(),
                           bias2=dd["b2"].data_ptr(), alpha0=dd["a0"].data_ptr() if act == "snake" else None,
                           alpha2=dd["a2"].data_ptr() if act == "snake" else None,
-                          workspace=ws.data_ptr() if ws is not None else None)
+                          workspace=ws.data_ptr() if ws is not None else None, coop_rb=rb)
     st = C_.c_void_p(torch.cuda.current_stream().cuda_stream)
     y1 = torch.full_like(xd, float("nan"))
     N.check(N.lib.rave_residual_unit(C_.byref(args(y1, None)), st))
@@ -1059,6 +1063,8 @@ CACHED_UNIT_CASES = [
     (256, 3, "snake", True, 1, 32, False),
     (256, 9, "leaky", True, 2, 64, True),
     (512, 1, "leaky", False, 1, 8, True),
+    (256, 3, "leaky", True, 1, 8, 4),             # the wide cooperative group (coop_rb = 4)
+    (256, 9, "snake", False, 1, 16, 4),
 ]
 
 
@@ -1102,7 +1108,8 @@ def test_residual_unit_cached_form(N, dev, case, precision):
                           y_sb=C * T, y_sc=T, weight=packed.data_ptr(), bias1=dd["b1"].data_ptr(),
                           bias2=dd["b2"].data_ptr(), alpha0=dd["a0"].data_ptr() if act == "snake" else None,
                           alpha2=dd["a2"].data_ptr() if act == "snake" else None,
-                          workspace=ws.data_ptr() if ws is not None else None, x_len=XL, res_shift=rs)
+                          workspace=ws.data_ptr() if ws is not None else None, x_len=XL, res_shift=rs,
+                          coop_rb=4 if coop == 4 else 0)
     ws = None
     if coop:
         nws = N.lib.rave_unit_workspace(C_.byref(args(None)))

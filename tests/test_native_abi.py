@@ -221,6 +221,17 @@ def test_unit_workspace_sizes():
     # more groups than the ticket words can count: no cooperative form
     assert ws(512, N.PREC_SPLIT16, B=512, T=4096) == 0
 
+    # the wide group (coop_rb = 4, C = 256 only, round 6): twice the members' maxima words
+    def wsr(ch, rb, B=1, T=8):
+        a = N.UnitArgs(channels=ch, batch=B, t_len=T, dilation=3, pad_left=3, act=N.ACT["leaky"],
+                       leaky_slope=0.2, precision=N.PREC_BF16X3, coop_rb=rb)
+        return N.lib.rave_unit_workspace(C.byref(a))
+    assert wsr(256, 4) >= wsr(256, 0) > 0 and wsr(256, 2) == wsr(256, 0)
+    assert wsr(512, 2) == 0                      # no such group: no cooperative form
+    a = N.UnitArgs(channels=256, batch=1, t_len=8, dilation=3, pad_left=3, act=N.ACT["leaky"], leaky_slope=0.2,
+                   precision=N.PREC_BF16X3, coop_rb=3, x=16, y=16, weight=16)
+    assert N.lib.rave_residual_unit(C.byref(a), None) == N.RAVE_ERR_ARG   # refused before any launch
+
 
 def test_edge_precision_and_f32_filter_images(golden):
     """rave_edge_args.precision is validated before any launch, and the fp32
