@@ -15,6 +15,7 @@
 //                   and every launch configuration, every unit fused against its
 //                   two convs, every stack against its units; the fastest wins.
 #include "engine.h"
+#include "shift_batch.h"
 
 #include <cstdlib>
 
@@ -2830,7 +2831,15 @@ extern "C" int rave_stream_launches(const rave_stream* h, int which) {
         if (which == 0 ? !s->has_enc() : !s->has_dec()) fail(RAVE_ERR_STATE, "stream has no such direction");
         hipGraph_t g = which == 0 ? s->enc_graph : s->dec_graph;
         if (!g) {
-            n = (int)(which == 0 ? s->enc : s->dec)->ops.size();
+            // eager: the plan's ops, with a run of history shifts going out as one
+            // launch per rave::kShiftBatch (rave_plan_run, capi.cpp)
+            const auto& ops = (which == 0 ? s->enc : s->dec)->ops;
+            for (size_t i = 0; i < ops.size();) {
+                int run = 0;
+                while (i + run < ops.size() && run < rave::kShiftBatch && ops[i + run].op.kind == RAVE_OP_SHIFT_HISTORY) ++run;
+                ++n;
+                i += run > 0 ? run : 1;
+            }
             return;
         }
         size_t cnt = 0;

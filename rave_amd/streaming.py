@@ -147,7 +147,8 @@ class StreamingRAVE:
 
     def launches(self, which: str = "decode") -> int:
         """Kernel launches of one block ("encode" or "decode"): the captured
-        graph's kernel nodes (graph mode) or the plan's ops (eager)."""
+        graph's kernel nodes (graph mode) or the plan's launches (eager: one
+        per op, a run of history shifts going out as one batched launch)."""
         n = int(N.lib.rave_stream_launches(self.handle, {"encode": 0, "decode": 1}[which]))
         if n < 0:
             N.check(n, "stream_launches")

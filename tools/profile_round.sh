@@ -21,7 +21,7 @@ ONLY=${2:-all}      # all | bf3 (the f32_bf3 headline's passes only)
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-QUIET="--no-cpu-baseline --pipeline 1"
+QUIET="--no-cpu-baseline --pipeline 1 --no-configs"
 timeout -k 10 300 python3 $R/bench.py --steps 10 --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
 echo "bench: $(head -c 400 $OUT/bench.json)"
 gemm_rows() {   # counter CSVs are large; keep the GEMM-family rows only
