@@ -261,41 +261,22 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
         __syncthreads();
     }
     const bool partial = a.S > 1;
+    // in-launch split-K combine (round 6): the slabs are stored write-through and
+    // the split drawing the tile's last ticket sums them in split order with sc1
+    // loads (bitwise the separate reduce launch; the form of conv_gemv.hip)
+    const bool inl = partial && a.inlaunch;
+    const bool fin = !partial || inl;                // this workgroup may finish the tile
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(
         partial ? a.partial + ((int64_t)split * a.B + b) * (int64_t)a.M * a.U : a.y,
         partial ? a.M * a.U * 4 : 0);
-    const __amdgpu_buffer_rsrc_t yrs = make_rsrc(a.y + (int64_t)b * a.y_sb, partial ? 0 : a.y_bytes);
-    const __amdgpu_buffer_rsrc_t brs = make_rsrc(a.bias ? a.bias : a.y, (a.bias && !partial) ? a.bias_rows * 4 : 0);
+    const __amdgpu_buffer_rsrc_t yrs = make_rsrc(a.y + (int64_t)b * a.y_sb, fin ? a.y_bytes : 0);
+    const __amdgpu_buffer_rsrc_t brs = make_rsrc(a.bias ? a.bias : a.y, (a.bias && fin) ? a.bias_rows * 4 : 0);
     const __amdgpu_buffer_rsrc_t rrs = make_rsrc(
-        a.res ? a.res + (int64_t)b * a.r_sb : a.y, (a.res && !partial) ? a.r_bytes : 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if constexpr (KS > 1) {
-            if (q % KS != kg) continue;            // uniform
-        }
+        a.res ? a.res + (int64_t)b * a.r_sb : a.y, (a.res && fin) ? a.r_bytes : 0);
+    // bias, residual, ConvT interleave and the output store of sub-tile q
+    auto finish = [&](int q, const float* v) __attribute__((always_inline)) {
         const int i = q >> 1, jj = q & 1;
         const int n = n0 + wn0 + jj * 32 + l32;
-        float v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if constexpr (KS > 1) {
-                float sum = 0.f;
-#pragma unroll
-                for (int g = 0; g < KS; ++g) sum += red[((g * NWT + wt) * 4096) + (q * 16 + r) * 64 + lane];
-                v[r] = sum;
-            } else {
-                v[r] = acc[i][jj][r];
-            }
-        }
-        if (partial) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const unsigned off = (m < a.M && n < a.U) ? (unsigned)(m * a.U + n) * 4u : kOOB;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), prs, off, 0, 0);
-            }
-            continue;
-        }
         float bv[16], rv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -324,6 +305,80 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r] + bv[r] + rv[r]),
                                                   yrs, off, 0, 0);
         }
+    };
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if constexpr (KS > 1) {
+            if (q % KS != kg) continue;            // uniform
+        }
+        const int i = q >> 1, jj = q & 1;
+        const int n = n0 + wn0 + jj * 32 + l32;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if constexpr (KS > 1) {
+                float sum = 0.f;
+#pragma unroll
+                for (int g = 0; g < KS; ++g) sum += red[((g * NWT + wt) * 4096) + (q * 16 + r) * 64 + lane];
+                v[r] = sum;
+            } else {
+                v[r] = acc[i][jj][r];
+            }
+        }
+        if (partial) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const unsigned off = (m < a.M && n < a.U) ? (unsigned)(m * a.U + n) * 4u : kOOB;
+                if (inl) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), prs, off, 0, 16);
+                else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), prs, off, 0, 0);
+            }
+            continue;
+        }
+        finish(q, v);
+    }
+    if (inl) {
+        // MI355X_MICROARCH.md hand-off table row 1 (the launch keeps one workgroup
+        // per CU): every slab byte stored sc1 and drained by its wave before the
+        // barrier behind which one lane adds to the tile's unsharded ticket; the
+        // last adder, told by the value its add returned, reads every slab sc1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        __shared__ int last_s;
+        const int tile = b * gxy + bxy;
+        if (tid == 0) {
+            const int prev = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = prev == a.S - 1;
+            if (last) __hip_atomic_store(a.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last_s = last;
+        }
+        __syncthreads();
+        if (!last_s) return;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if constexpr (KS > 1) {
+                if (q % KS != kg) continue;
+            }
+            const int i = q >> 1, jj = q & 1;
+            const int n = n0 + wn0 + jj * 32 + l32;
+            float v[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = 0.f;
+            for (int sp = 0; sp < a.S; ++sp) {
+                const __amdgpu_buffer_rsrc_t srs =
+                    make_rsrc(a.partial + ((int64_t)sp * a.B + b) * (int64_t)a.M * a.U, a.M * a.U * 4);
+                float t[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const unsigned off = (m < a.M && n < a.U) ? (unsigned)(m * a.U + n) * 4u : kOOB;
+                    t[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, off, 0, 16));
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] += t[r];
+            }
+            finish(q, v);
+        }
     }
 #ifdef RAVE_STAMPS
     stamp(3);
@@ -351,8 +406,10 @@ static int launch_k(ConvKArgs k, hipStream_t st) {
         set_error("conv1d: dilation too large for the staged window");
         return RAVE_ERR_UNSUPPORTED;
     }
-    const size_t lds = (size_t)std::max(2 * BUF, RED) * sizeof(float);
-    static_assert((size_t)std::max(2 * BUF, RED) * sizeof(float) <= 160 * 1024, "LDS budget");
+    size_t lds = (size_t)std::max(2 * BUF, RED) * sizeof(float);
+    static_assert((size_t)std::max(2 * BUF, RED) * sizeof(float) <= 150 * 1024, "LDS budget");
+    // an in-launch combine keeps one workgroup per CU (the sc1 hand-off's measured form)
+    if (k.inlaunch) lds = std::max(lds, (size_t)(80 * 1024 + 256));
     dim3 grid(ceil_div(k.U, BN), ceil_div(k.M, BM), k.B * k.S);
     auto kern = (k.act == RAVE_ACT_SNAKE) ? conv1d_mfma_kernel<BM, BN, KT, true>
                                            : conv1d_mfma_kernel<BM, BN, KT, false>;
@@ -362,7 +419,7 @@ static int launch_k(ConvKArgs k, hipStream_t st) {
         bool& d = done[k.act == RAVE_ACT_SNAKE];
         if (!d) {
             RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
             d = true;
         }
     }
@@ -524,6 +581,13 @@ static bool f32_tile_ok(int ti, int M, int split_row) {
 }
 
 // The launch configuration: args.config when set (validated), else the heuristic.
+// the in-launch combine of an fp32 MFMA tile: one ticket per output tile
+static bool f32_inl_ok(const ConvKArgs& k, int tile, int S) {
+    if (tile < 0 || tile >= 5) return false;
+    const int64_t tiles = (int64_t)ceil_div(k.M, kF32Tiles[tile][0]) * ceil_div(k.U, kF32Tiles[tile][1]) * k.B;
+    return S > 1 && tiles <= kSplitTicketsUsable;
+}
+
 static int resolve(const rave_conv1d_args& a, const ConvKArgs& k, int taps, LaunchCfg& c) {
     if (a.config == 0) {
         c = choose(k.M, k.U, k.B, k.nchunks, k.split_row);
@@ -540,10 +604,13 @@ static int resolve(const rave_conv1d_args& a, const ConvKArgs& k, int taps, Laun
         c.sep = cc.sep;
         return RAVE_OK;
     }
-    RAVE_CHECK_ARG(dec && cc.sep == 0 && f32_tile_ok(cc.tile, k.M, k.split_row) &&
-                       split_count_distinct(cc.S, k.nchunks),
+    // bit 9 on an fp32 MFMA tile: the K splits combined in-launch (its meaning for
+    // the gemv tiles is the opposite; both spellings predate the other's)
+    RAVE_CHECK_ARG(dec && (cc.sep == 0 || (cc.S > 1 && f32_inl_ok(k, cc.tile, cc.S))) &&
+                       f32_tile_ok(cc.tile, k.M, k.split_row) && split_count_distinct(cc.S, k.nchunks),
                    "conv1d: config not valid for these args (see rave_conv1d_configs)");
     c = {kF32Tiles[cc.tile][0], kF32Tiles[cc.tile][1], cc.S};
+    c.inl = cc.sep;
     return RAVE_OK;
 }
 
@@ -568,6 +635,10 @@ extern "C" int rave_conv1d_configs(const rave_conv1d_args* p, int32_t* cfgs, int
             if (S > 1 && (wg * S > 8192 || wg >= 1024)) continue;      // enough workgroups unsplit
             if (n < max_cfgs && cfgs) cfgs[n] = encode_config(ti, S, 0);
             ++n;
+            if (f32_inl_ok(k, ti, S)) {                                 // combined in-launch
+                if (n < max_cfgs && cfgs) cfgs[n] = encode_config(ti, S, 1);
+                ++n;
+            }
         }
     }
     // skinny-N (gemv) configurations: the smallest column width holding U
@@ -631,6 +702,9 @@ extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
 #ifdef RAVE_STAMPS
     k.stamps = p->stamps;
 #endif
+    k.tickets = reinterpret_cast<int*>(p->partial);
+    k.inlaunch = (k.S > 1 && c.inl && k.partial &&
+                  (int64_t)ceil_div(k.M, c.bm) * ceil_div(k.U, c.bn) * k.B <= kSplitTicketsUsable) ? 1 : 0;
     hipStream_t st = as_stream(stream);
     switch (taps) {
         case 1: rc = f32_launch_family<1>(k, c, st); break;
@@ -641,7 +715,7 @@ extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
         case 8: rc = f32_launch_family<8>(k, c, st); break;
         default: set_error("conv1d: unsupported kernel size"); return RAVE_ERR_UNSUPPORTED;
     }
-    if (rc != RAVE_OK || k.S <= 1) return rc;
+    if (rc != RAVE_OK || k.S <= 1 || k.inlaunch) return rc;
     int64_t total = (int64_t)k.B * k.M * k.U;
     int blocks = (int)std::min<int64_t>(ceil_div64(total, 256), 4096);
     launch(conv1d_splitk_reduce_kernel<0>, dim3(blocks), dim3(256), 0, st, k);

@@ -117,6 +117,7 @@ static inline int convt_group1_row(int c_out, int R, int q0) {
 struct LaunchCfg {
     int bm, bn, S;
     int sep = 0;          // gemv (bm == 0, bn = NMAX): the K-split slabs summed by a separate launch
+    int inl = 0;          // fp32 MFMA tiles (bm > 0, config bit 9, round 6): summed in-launch instead
 };
 
 // Skinny-N fp32 family (conv_gemv.hip): weights spread over the chip, all

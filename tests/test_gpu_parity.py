@@ -219,11 +219,19 @@ def test_conv_every_config(N, dev, case, precision):
                    alpha=16 if alpha is not None else None, residual=16 if res is not None else None)
     cfgs = N.conv_configs(a)
     assert cfgs, "no configurations listed"
+    outs = {}
     for cfg in cfgs:
         got = run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act, True,
                        N.PRECISION[precision], config=cfg)
         err = maxabs(got, ref)
         assert np.isfinite(got).all() and err <= 2e-5 * max(1.0, np.abs(ref).max()), (cfg, err)
+        outs[cfg] = got
+    if precision == "f32":
+        # exact-fp32 MFMA tiles (0..4): bit 9 = the in-launch combine (round 6),
+        # bitwise the separate reduce launch (both sum the splits in split order)
+        pairs = [(c, c + 512) for c in outs if (c - 1) & 15 < 5 and not ((c - 1) >> 9) & 1 and c + 512 in outs]
+        for c0, c1 in pairs:
+            assert np.array_equal(outs[c0], outs[c1]), (c0, c1)
 
 
 GEMV_CASES = [
@@ -263,11 +271,18 @@ def test_conv_gemv_configs(N, dev, case):
                    alpha=16 if alpha is not None else None, residual=16 if res is not None else None)
     gemv = [c for c in N.conv_configs(a) if 8 <= ((c - 1) & 15) <= 13]
     assert gemv, "no skinny-N configurations listed"
+    outs = {}
     for cfg in gemv:
         got = run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act, True,
                        N.PREC_F32, config=cfg)
         err = maxabs(got, ref)
         assert np.isfinite(got).all() and err <= 2e-5 * max(1.0, np.abs(ref).max()), (cfg, err)
+        outs[cfg] = got
+    # the in-launch combine (sc1 slabs, last arriver; round 6) sums the K splits in
+    # split order, as the separate reduce launch does: bitwise the same
+    pairs = [(c, c + 512) for c in outs if not ((c - 1) >> 9) & 1 and c + 512 in outs]
+    for c0, c1 in pairs:
+        assert np.array_equal(outs[c0], outs[c1]), (c0, c1)
 
 
 def test_conv_ring_refuses_unaligned(N, dev):

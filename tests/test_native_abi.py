@@ -138,6 +138,24 @@ def test_conv_configs_listing(precision):
     assert N.lib.rave_conv1d_workspace(C.byref(a)) == -1
 
 
+def test_conv_f32_inlaunch_configs():
+    """Exact-fp32 MFMA tiles (0..4) with K splits are listed twice (round 6): the
+    separate reduce launch and, bit 9 set, the in-launch combine; the launcher
+    accepts both and refuses the in-launch bit without K splits."""
+    a = N.ConvArgs(c_in=512, c_out=512, kernel=3, stride=1, dilation=1, pad_left=1, pad_right=1,
+                   batch=1, t_in=64, t_out=64, precision=N.PREC_F32, x=16, y=16, weight=16)
+    cfgs = N.conv_configs(a)
+    tile = lambda c: (c - 1) & 15
+    splits = lambda c: ((c - 1) >> 4 & 31) + 1
+    inl = [c for c in cfgs if tile(c) < 5 and ((c - 1) >> 9) & 1]
+    assert inl and all(splits(c) > 1 and c - 512 in cfgs for c in inl)
+    for c in inl:
+        a.config = c
+        assert N.lib.rave_conv1d_workspace(C.byref(a)) > 0
+    a.config = 1 + 4 + 512        # 64 x 64 tile, one K split, in-launch bit: nothing to combine
+    assert N.lib.rave_conv1d_workspace(C.byref(a)) == -1
+
+
 def test_plan_create_and_relocation_bounds():
     ops = (N.PlanOp * 1)()
     ops[0].kind = N.OP_FILL

@@ -1,82 +1,118 @@
 #!/usr/bin/env python3
-"""Per-kernel anatomy of one C3 streaming block (BASELINE configs[2]: v2 causal,
-B = 1, 2048-sample blocks), for rocprofv3 --kernel-trace.
+"""Where a C3 streaming block's time goes (BASELINE configs[2]: v2 causal,
+2048-sample blocks, B = 1), from a rocprofv3 kernel trace.
 
-    rocprofv3 --kernel-trace --output-format csv -d D -o run -- python3 tools/c3_trace.py run
-    python3 tools/c3_trace.py summarize D/.../run_kernel_trace.csv > c3_ops.json
+    run:      rocprofv3 --kernel-trace --output-format csv -d OUT -o run -- \
+                  python3 tools/c3_trace.py run --precision f32_bf3
+    analyse:  python3 tools/c3_trace.py analyse OUT/.../run_kernel_trace.csv
 
-``run`` builds the stream plans (autotuning launches happen here), then fires a
-marker kernel (torch cumsum of a 7-element tensor: a scan) and streams BLOCKS eager
-encode+decode blocks; ``summarize`` keeps the dispatches after the last marker
-and reports, per kernel name, launches per block and the mean duration, plus
-the first block's launch sequence with start-to-start gaps.
-"""
+``run`` builds the causal model with the committed launch choices
+(profiles/tuning/c3_<precision>.json, as bench.py's configs leg), replays
+``--blocks`` encode+decode blocks after 8 warm-up blocks with a synchronize
+around each (the latency measurement), and prints the host latencies as JSON.
+``analyse`` splits the trace into blocks at the host gaps and reports, per
+block: the span (first kernel start to last kernel end), the kernels' busy time
+and the gaps between them, plus each kernel's mean duration -- the part of the
+block latency the kernels themselves take against what the launches and the
+host add."""
+import argparse
 import csv
 import json
 import os
 import sys
+import time
 from collections import defaultdict
 
-BLOCKS = 40
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
 
 
-def run():
+def run(a):
+    import numpy as np
     import torch
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import _pinned
     from rave_amd import config as rcfg
     from rave_amd.model import RAVE
     from rave_amd.streaming import StreamingRAVE
     from rave_amd.weights import init_params, init_speaker
     dev = torch.device("cuda:0")
     cfg = rcfg.causal()
-    prec = os.environ.get("C3_PRECISION", "auto")
-    m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=prec)
-    s = StreamingRAVE(m, batch=1, block=2048, graph=False)
-    x = (0.2 * torch.randn(BLOCKS + 4, 1, 1, 2048, generator=torch.Generator().manual_seed(0))).to(dev)
-    for i in range(4):
-        s.forward(x[i])
-    torch.cuda.synchronize()
-    torch.arange(7, device=dev).cumsum(0)     # marker (a scan kernel: no rave kernel is one)
-    torch.cuda.synchronize()
-    for i in range(BLOCKS):
-        s.forward(x[4 + i])
+    tun, src = (None, "autotuned at plan build") if a.retune else _pinned("c3", a.precision)
+    m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=a.precision, tuning=tun)
+    blk, warm, nb = 2048, 8, a.blocks
+    x = (0.2 * torch.randn(warm + nb, 1, 1, blk, generator=torch.Generator().manual_seed(0))).to(dev)
+    s = StreamingRAVE(m, batch=1, block=blk, graph=True)
+    s.reset()
+    lat = []
+    for i in range(warm + nb):
         torch.cuda.synchronize()
-    print(json.dumps({"blocks": BLOCKS, "precision": prec}))
+        time.sleep(0.002)                       # a clear gap between blocks in the trace
+        t0 = time.perf_counter()
+        s.forward(x[i])
+        torch.cuda.synchronize()
+        if i >= warm:
+            lat.append((time.perf_counter() - t0) * 1e3)
+    lat = np.array(lat)
+    if a.save:
+        with open(a.save, "w") as fh:
+            json.dump(m.tuning(), fh, indent=0)
+    print(json.dumps({"precision": a.precision, "tuning": src, "blocks": nb,
+                      "launches": {"encode": s.launches("encode"), "decode": s.launches("decode")},
+                      "latency_ms_median": round(float(np.median(lat)), 4),
+                      "latency_ms_p99": round(float(np.percentile(lat, 99)), 4)}))
 
 
-def summarize(path):
-    with open(path, newline="") as fh:
-        rows = sorted(csv.DictReader(fh), key=lambda r: int(r["Start_Timestamp"]))
-    def is_marker(r):
-        k = r["Kernel_Name"].lower()
-        return "rave" not in k and ("scan" in k or "cumsum" in k)
-    last = max(i for i, r in enumerate(rows) if is_marker(r))
-    rows = rows[last + 1:]
-    name = lambda r: r["Kernel_Name"].split("(")[0].replace("void ", "")[:90]
-    tot, cnt = defaultdict(float), defaultdict(int)
+def analyse(a):
+    rows = []
+    with open(a.trace) as fh:
+        for r in csv.DictReader(fh):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    blocks, cur = [], []
     for r in rows:
-        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        tot[name(r)] += d
-        cnt[name(r)] += 1
-    per_block = len(rows) / BLOCKS
-    ker = sorted(tot, key=lambda k: -tot[k])
-    out = {"launches_per_block": per_block,
-           "busy_us_per_block": sum(tot.values()) / BLOCKS / 1e3,
-           "span_us_per_block": (int(rows[-1]["End_Timestamp"]) - int(rows[0]["Start_Timestamp"])) / BLOCKS / 1e3,
-           "kernels": [{"kernel": k, "per_block": cnt[k] / BLOCKS, "avg_us": tot[k] / cnt[k] / 1e3,
-                        "us_per_block": tot[k] / BLOCKS / 1e3} for k in ker]}
-    n = int(round(per_block))
-    seq, t_prev = [], None
-    for r in rows[:n]:
-        st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        seq.append({"kernel": name(r), "us": (en - st) / 1e3, "gap_us": (st - t_prev) / 1e3 if t_prev else 0.0})
-        t_prev = en
-    out["first_block"] = seq
+        if cur and r[0] - cur[-1][1] > a.gap_us * 1000:
+            blocks.append(cur)
+            cur = []
+        cur.append(r)
+    if cur:
+        blocks.append(cur)
+    # the timed blocks: the last ones of the modal kernel count (warm-up and plan
+    # building launch other kernels)
+    counts = defaultdict(int)
+    for b in blocks:
+        counts[len(b)] += 1
+    n_mode = max(counts, key=lambda k: (counts[k], k))
+    timed = [b for b in blocks if len(b) == n_mode][-a.blocks:]
+    spans = sorted((b[-1][1] - b[0][0]) / 1e3 for b in timed)
+    busy = sorted(sum(e - s for s, e, _ in b) / 1e3 for b in timed)
+    per = defaultdict(list)
+    for b in timed:
+        for i, (s, e, n) in enumerate(b):
+            per[(i, n)].append((e - s) / 1e3)
+    mid = len(timed) // 2
+    out = {"blocks": len(timed), "kernels_per_block": n_mode,
+           "span_us_median": round(spans[mid], 1), "busy_us_median": round(busy[mid], 1),
+           "gaps_us_median": round(spans[mid] - busy[mid], 1),
+           "kernels": [{"i": i, "name": n.split("(")[0][:90], "us": round(sorted(v)[len(v) // 2], 2)}
+                       for (i, n), v in sorted(per.items())]}
     print(json.dumps(out, indent=1))
 
 
+def main():
+    ap = argparse.ArgumentParser()
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    r = sub.add_parser("run")
+    r.add_argument("--precision", default="f32_bf3")
+    r.add_argument("--blocks", type=int, default=32)
+    r.add_argument("--retune", action="store_true", help="time every launch choice instead of the pins")
+    r.add_argument("--save", help="write the plan's launch choices (RAVE.tuning()) here")
+    an = sub.add_parser("analyse")
+    an.add_argument("trace")
+    an.add_argument("--blocks", type=int, default=32)
+    an.add_argument("--gap-us", type=float, default=500.0)
+    a = ap.parse_args()
+    run(a) if a.cmd == "run" else analyse(a)
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "run":
-        run()
-    else:
-        summarize(sys.argv[2])
+    main()
