@@ -46,7 +46,8 @@ def run(a):
     lat = []
     for i in range(warm + nb):
         torch.cuda.synchronize()
-        time.sleep(0.002)                       # a clear gap between blocks in the trace
+        if a.sleep_ms > 0:
+            time.sleep(a.sleep_ms / 1e3)        # a wider gap between blocks in the trace
         t0 = time.perf_counter()
         s.forward(x[i])
         torch.cuda.synchronize()
@@ -106,10 +107,12 @@ def main():
     r.add_argument("--blocks", type=int, default=32)
     r.add_argument("--retune", action="store_true", help="time every launch choice instead of the pins")
     r.add_argument("--save", help="write the plan's launch choices (RAVE.tuning()) here")
+    r.add_argument("--sleep-ms", type=float, default=0.0,
+                   help="host sleep before each block (the bench leg has none: clocks stay up)")
     an = sub.add_parser("analyse")
     an.add_argument("trace")
     an.add_argument("--blocks", type=int, default=32)
-    an.add_argument("--gap-us", type=float, default=500.0)
+    an.add_argument("--gap-us", type=float, default=15.0)
     a = ap.parse_args()
     run(a) if a.cmd == "run" else analyse(a)
 
