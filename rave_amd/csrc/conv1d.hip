@@ -266,6 +266,9 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
     // loads (bitwise the separate reduce launch; the form of conv_gemv.hip)
     const bool inl = partial && a.inlaunch;
     const bool fin = !partial || inl;                // this workgroup may finish the tile
+    const int ntl = gxy * a.B;                       // output tiles (in-launch slab layout)
+    const __amdgpu_buffer_rsrc_t irs = make_rsrc(
+        inl ? a.partial + ((int64_t)split * ntl + (b * gxy + bxy)) * (BM * BN) : a.y, inl ? BM * BN * 4 : 0);
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(
         partial ? a.partial + ((int64_t)split * a.B + b) * (int64_t)a.M * a.U : a.y,
         partial ? a.M * a.U * 4 : 0);
@@ -325,13 +328,23 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
                 v[r] = acc[i][jj][r];
             }
         }
+        if (inl) {
+            // the in-launch slab is private to the combine: lane-major 16-byte
+            // pieces [split][tile][wave tile][q][r / 4][lane] (whole-wave
+            // write-through stores, and the last arriver's loads, are 16 B)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(u32x4_t, f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]}), irs,
+                    (unsigned)((((wt * 4 + q) * 4 + g) * 64 + lane) * 16), 0, 16);
+            continue;
+        }
         if (partial) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 const unsigned off = (m < a.M && n < a.U) ? (unsigned)(m * a.U + n) * 4u : kOOB;
-                if (inl) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), prs, off, 0, 16);
-                else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), prs, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), prs, off, 0, 0);
             }
             continue;
         }
@@ -361,22 +374,36 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
             }
             const int i = q >> 1, jj = q & 1;
             const int n = n0 + wn0 + jj * 32 + l32;
-            float v[16];
+            (void)i;
+            (void)n;
+            f32x4 v4[4];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = 0.f;
-            for (int sp = 0; sp < a.S; ++sp) {
-                const __amdgpu_buffer_rsrc_t srs =
-                    make_rsrc(a.partial + ((int64_t)sp * a.B + b) * (int64_t)a.M * a.U, a.M * a.U * 4);
-                float t[16];
+            for (int g = 0; g < 4; ++g) v4[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+            // splits in order; SB splits' loads in flight per round trip
+            constexpr int SB = 4;
+            for (int sp0 = 0; sp0 < a.S; sp0 += SB) {
+                f32x4 t[SB][4];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const unsigned off = (m < a.M && n < a.U) ? (unsigned)(m * a.U + n) * 4u : kOOB;
-                    t[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, off, 0, 16));
+                for (int u = 0; u < SB; ++u) {
+                    const int sp = min(sp0 + u, a.S - 1);
+                    const __amdgpu_buffer_rsrc_t srs = make_rsrc(a.partial + ((int64_t)sp * ntl + tile) * (BM * BN),
+                                                                 BM * BN * 4);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        t[u][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                            srs, (unsigned)((((wt * 4 + q) * 4 + g) * 64 + lane) * 16), 0, 16));
                 }
 #pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] += t[r];
+                for (int u = 0; u < SB; ++u)
+                    if (sp0 + u < a.S)
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) v4[g] += t[u][g];
             }
+            float v[16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[4 * g + e] = v4[g][e];
             finish(q, v);
         }
     }
@@ -595,6 +622,14 @@ static int resolve(const rave_conv1d_args& a, const ConvKArgs& k, int taps, Laun
     }
     ConfigCode cc;
     const bool dec = decode_config(a.config, cc);
+    if (dec && (cc.tile == kRowsTile || cc.tile == kRowsTile8)) {   // row-sliced skinny-N (one launch, no K split)
+        RAVE_CHECK_ARG(cc.S == 1 && k.U <= kRowsMaxN && (cc.tile == kRowsTile || !cc.sep) &&
+                           gemv_rows_fits(taps, k.U, k.d, k.transposed != 0, k.nchunks, rows_nmax(k.U)),
+                       "conv1d: gemv rows config not valid for these args (see rave_conv1d_configs)");
+        c = {0, rows_nmax(k.U), 1};
+        c.rows = cc.tile == kRowsTile8 ? 8 : cc.sep ? 32 : 16;
+        return RAVE_OK;
+    }
     if (dec && is_gemv_tile(cc.tile)) {   // the skinny-N family (conv_gemv.hip)
         RAVE_CHECK_ARG(split_count_distinct(cc.S, k.nchunks) && (cc.S > 1 || !cc.sep) &&
                            gemv_fits(taps, k.U, k.d, k.transposed != 0, ceil_div(k.nchunks, cc.S),
@@ -660,6 +695,14 @@ extern "C" int rave_conv1d_configs(const rave_conv1d_args* p, int32_t* cfgs, int
             }
         }
     }
+    // the row-sliced skinny-N form: 8, 16 and 32 rows per workgroup, no K split
+    if (k.U <= kRowsMaxN && gemv_rows_fits(taps, k.U, k.d, k.transposed != 0, k.nchunks, rows_nmax(k.U)))
+        for (int v = 0; v < 3; ++v) {
+            const int rt = v == 0 ? 8 : v == 1 ? 16 : 32;
+            if (k.transposed && k.split_row < k.M && k.split_row % rt != 0) continue;
+            if (n < max_cfgs && cfgs) cfgs[n] = v == 0 ? encode_config(kRowsTile8, 1, 0) : encode_config(kRowsTile, 1, v - 1);
+            ++n;
+        }
     return n;
 }
 
@@ -673,6 +716,8 @@ extern "C" int64_t rave_conv1d_workspace(const rave_conv1d_args* p) {
     LaunchCfg c;
     if (resolve(*p, k, taps, c) != RAVE_OK) return -1;
     if (c.S <= 1) return 0;
+    if (c.inl && c.bm > 0)   // the in-launch combine's private slabs: one whole tile per split and tile
+        return kSplitTickets + (int64_t)c.S * ceil_div(k.M, c.bm) * ceil_div(k.U, c.bn) * k.B * c.bm * c.bn;
     return kSplitTickets + (int64_t)c.S * k.B * (int64_t)k.M * k.U;   // same layout as the split path
 }
 
@@ -691,6 +736,7 @@ extern "C" int rave_conv1d(const rave_conv1d_args* p, void* stream) {
     k.cps = ceil_div(k.nchunks, c.S);
     k.S = ceil_div(k.nchunks, k.cps);                 // no empty splits
     k.partial = p->partial ? p->partial + kSplitTickets : nullptr;   // slabs after the counters
+    if (c.rows) return conv1d_gemv_rows(k, taps, c.bn, c.rows, as_stream(stream));
     if (c.bm == 0) {                                  // skinny-N family (tickets ahead of the slabs)
         k.tickets = reinterpret_cast<int*>(p->partial);
         if (!gemv_fits(taps, k.U, k.d, k.transposed != 0, k.cps, c.bn)) {

@@ -268,6 +268,201 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
         if (n0 + n < U) store_out(a, b, m, n0 + n, v[n]);
 }
 
+// ---------------------------------------------------------------- row-sliced form
+// Skinny-N conv with no K split (round 6): the C3 stream plans pay 4-5 us per
+// launch whatever its work, and a K-split conv is two launches (or an in-launch
+// combine of about the same cost).  Here a workgroup owns RT = 8, 16 or 32 output
+// rows over the WHOLE K, so a conv is one launch with M / RT workgroups per
+// batch item and nothing to combine:
+//   * lane = kl * ML + ml: ML = RT / 4 lanes along the rows (4 consecutive rows
+//     each, one 16-byte load per K-row: a wave instruction reads KL = 64 / ML
+//     K-rows x RT * 4 contiguous bytes), KL lanes along K; the 4 waves take
+//     interleaved K-row groups;
+//   * the input window of every channel is staged once in LDS, activation
+//     applied (as conv1d_gemv_kernel);
+//   * each lane keeps 4 x NMAX fp32 sums; the KL lanes of one row group are
+//     summed by a fixed xor-shuffle tree, the 4 waves through LDS in wave
+//     order: deterministic, no atomics, no slabs.
+constexpr int kRowsStage = 24576;                  // staged window floats (96 KiB)
+// the wave-sum area after the window (+ slack: lanes read NMAX columns per row)
+__host__ __device__ inline int rows_red_off(int window, int slack) { return ((window + 3) & ~3) + slack + 16; }
+
+template <int KT, int NMAX, int RT, bool SNAKE>
+__global__ __launch_bounds__(256) void conv1d_gemv_rows_kernel(ConvKArgs a) {
+    constexpr int CIT = GFam<KT>::CIT, ST = GFam<KT>::ST;
+    constexpr int ML = RT / 4, KL = 64 / ML, KRW = KT * CIT, QB = NMAX <= 8 ? 16 : 8;
+    constexpr unsigned kOOB = 0xFFFFFFF0u;
+    extern __shared__ __attribute__((aligned(16))) float gsm[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ml = lane % ML, kl = lane / ML;
+    const int MT = ceil_div(a.M, RT);
+    const int tile = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    const int mt = tile % MT, b = tile / MT;
+    const int m0 = mt * RT;
+    const int nch = a.nchunks * CIT;                 // staged channels (all of K)
+    const int U = a.U, XW = a.XW;
+    const int t0 = -a.pad_l;
+    const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
+
+    // ---------------------------------------------------------------- window
+    constexpr int WB = 32;                           // the whole window is read: keep it in flight
+    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);
+    for (int e0 = tid; e0 < nch * XW; e0 += 256 * WB) {
+        float rv[WB];
+#pragma unroll
+        for (int i = 0; i < WB; ++i) {
+            const int e = e0 + i * 256;
+            const int ci = e / XW, w = e - ci * XW, t = t0 + w;
+            const bool ok = e < nch * XW && ci < a.c_in && t >= 0 && t < a.t_in;
+            rv[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                xrs, ok ? (unsigned)(ci * a.x_sc + t) * 4u : kOOB, 0, 0));
+        }
+#pragma unroll
+        for (int i = 0; i < WB; ++i) {
+            const int e = e0 + i * 256;
+            if (e >= nch * XW) break;
+            const int ci = e / XW, w = e - ci * XW, t = t0 + w;
+            const bool ok = ci < a.c_in && t >= 0 && t < a.t_in;
+            float v = rv[i];
+            if constexpr (SNAKE) {
+                const float al = a.alpha[min(ci, a.c_in - 1)];
+                v = v + (1.0f / (al + 1e-9f)) * sin_squared(al * v);
+            } else {
+                v = v > 0.f ? v : v * slope;
+            }
+            gsm[e] = ok ? v : 0.f;
+        }
+    }
+    __syncthreads();
+
+    // ---------------------------------------------------------------- K loop
+    // K-row kr of the packed image ([chunk][tap][channel][Mpad]) = (chunk, tap j,
+    // channel cl): x of column n at window (chunk * CIT + cl, goff + j d + n ST)
+    const int mrow = m0 + 4 * ml;
+    const int goff = (a.transposed && m0 >= a.split_row) ? 1 : 0;   // (RT | 64: no straddle)
+    const bool rows_ok = mrow < a.Mpad;
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, a.w_bytes);
+    const int nq = a.nchunks * KRW;
+    float acc[4][NMAX];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n) acc[r][n] = 0.f;
+    constexpr int KS = 4 * KL;                       // K-rows per workgroup step
+    for (int k0 = wave * KL + kl; k0 < nq; k0 += KS * QB) {
+        f32x4 wv[QB];
+        int xo[QB];
+#pragma unroll
+        for (int i = 0; i < QB; ++i) {
+            const int kr = k0 + i * KS;
+            const bool ok = kr < nq && rows_ok;
+            const unsigned off = ok ? ((unsigned)kr * (unsigned)a.Mpad + (unsigned)mrow) * 4u : kOOB;
+            wv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
+            const int c = kr / KRW, rem = kr - c * KRW, j = rem / CIT, cl = rem - j * CIT;
+            xo[i] = kr < nq ? (c * CIT + cl) * XW + goff + j * a.d : 0;   // (past nq: zero weights)
+        }
+#pragma unroll
+        for (int i = 0; i < QB; ++i) {
+            const float* xr = gsm + xo[i];
+#pragma unroll
+            for (int n = 0; n < NMAX; ++n) {
+                const float xv = xr[n * ST];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[r][n] = fmaf(wv[i][r], xv, acc[r][n]);
+            }
+        }
+    }
+
+    // ---------------------------------------------------------------- sums (fixed order)
+#pragma unroll
+    for (int off = ML; off < 64; off *= 2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int n = 0; n < NMAX; ++n) acc[r][n] += __shfl_xor(acc[r][n], off);
+    float* red = gsm + rows_red_off(nch * XW, NMAX * ST);   // [wave][RT rows][NMAX]
+    if (kl == 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int n = 0; n < NMAX; ++n) red[(wave * RT + 4 * ml + r) * NMAX + n] = acc[r][n];
+    __syncthreads();
+    for (int e = tid; e < RT * NMAX; e += 256) {
+        const int row = e / NMAX, n = e - row * NMAX;
+        const float v = ((red[row * NMAX + n] + red[(RT + row) * NMAX + n]) + red[(2 * RT + row) * NMAX + n]) +
+                        red[(3 * RT + row) * NMAX + n];
+        const int m = m0 + row;
+        if (n < U && m < a.M) store_out(a, b, m, n, v);
+    }
+}
+
+template <int KT, int NMAX, int RT>
+static int rows_go(ConvKArgs k, hipStream_t st) {
+    const int grid = ceil_div(k.M, RT) * k.B;
+    const size_t lds = (size_t)(rows_red_off(k.nchunks * GFam<KT>::CIT * k.XW, NMAX * GFam<KT>::ST) + 4 * RT * NMAX) * 4;
+    auto kern = k.act == RAVE_ACT_SNAKE ? conv1d_gemv_rows_kernel<KT, NMAX, RT, true>
+                                        : conv1d_gemv_rows_kernel<KT, NMAX, RT, false>;
+    static bool done[2] = {false, false};
+    bool& d = done[k.act == RAVE_ACT_SNAKE];
+    if (!d) {
+        RAVE_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+        d = true;
+    }
+    launch(kern, dim3(grid), dim3(256), (uint32_t)lds, st, k);
+    return launch_status("conv1d_gemv_rows_kernel");
+}
+
+template <int KT, int RT>
+static int rows_family(const ConvKArgs& k, int nmax, hipStream_t st) {
+    switch (nmax) {
+        case 4: return rows_go<KT, 4, RT>(k, st);
+        case 8: return rows_go<KT, 8, RT>(k, st);
+        case 16: return rows_go<KT, 16, RT>(k, st);
+        default: return rows_go<KT, 32, RT>(k, st);
+    }
+}
+
+bool gemv_rows_fits(int taps, int U, int d, bool transposed, int nchunks, int nmax) {
+    if (U > nmax || nmax > kRowsMaxN) return false;
+    const int cit = taps == 1 || taps == 2 ? 32 : taps == 3 || taps == 4 ? 16 : 8;
+    const int st = taps == 4 ? 2 : taps == 8 ? 4 : 1;
+    return (int64_t)nchunks * cit * gemv_xw(taps, st, U, d, transposed) <= kRowsStage;
+}
+
+int conv1d_gemv_rows(ConvKArgs k, int taps, int nmax, int rt, hipStream_t st) {
+    const int stv = taps == 4 ? 2 : taps == 8 ? 4 : 1;
+    k.XW = gemv_xw(taps, stv, k.U, k.d, k.transposed != 0);
+    if (!gemv_rows_fits(taps, k.U, k.d, k.transposed != 0, k.nchunks, nmax) || (rt != 8 && rt != 16 && rt != 32) ||
+        (k.transposed && k.split_row < k.M && k.split_row % rt != 0)) {
+        set_error("conv1d(gemv rows): window exceeds the staging area, or too many columns");
+        return RAVE_ERR_UNSUPPORTED;
+    }
+    k.S = 1;
+    switch (taps * 64 + rt) {
+        case 1 * 64 + 8: return rows_family<1, 8>(k, nmax, st);
+        case 2 * 64 + 8: return rows_family<2, 8>(k, nmax, st);
+        case 3 * 64 + 8: return rows_family<3, 8>(k, nmax, st);
+        case 4 * 64 + 8: return rows_family<4, 8>(k, nmax, st);
+        case 7 * 64 + 8: return rows_family<7, 8>(k, nmax, st);
+        case 8 * 64 + 8: return rows_family<8, 8>(k, nmax, st);
+        case 1 * 64 + 16: return rows_family<1, 16>(k, nmax, st);
+        case 1 * 64 + 32: return rows_family<1, 32>(k, nmax, st);
+        case 2 * 64 + 16: return rows_family<2, 16>(k, nmax, st);
+        case 2 * 64 + 32: return rows_family<2, 32>(k, nmax, st);
+        case 3 * 64 + 16: return rows_family<3, 16>(k, nmax, st);
+        case 3 * 64 + 32: return rows_family<3, 32>(k, nmax, st);
+        case 4 * 64 + 16: return rows_family<4, 16>(k, nmax, st);
+        case 4 * 64 + 32: return rows_family<4, 32>(k, nmax, st);
+        case 7 * 64 + 16: return rows_family<7, 16>(k, nmax, st);
+        case 7 * 64 + 32: return rows_family<7, 32>(k, nmax, st);
+        case 8 * 64 + 16: return rows_family<8, 16>(k, nmax, st);
+        case 8 * 64 + 32: return rows_family<8, 32>(k, nmax, st);
+        default: set_error("conv1d(gemv rows): unsupported kernel size"); return RAVE_ERR_UNSUPPORTED;
+    }
+}
+
 template <int KT, int NMAX>
 static int gemv_go(ConvKArgs k, hipStream_t st) {
     const int MT = ceil_div(k.M, GR<NMAX>::BM);

@@ -118,6 +118,7 @@ struct LaunchCfg {
     int bm, bn, S;
     int sep = 0;          // gemv (bm == 0, bn = NMAX): the K-split slabs summed by a separate launch
     int inl = 0;          // fp32 MFMA tiles (bm > 0, config bit 9, round 6): summed in-launch instead
+    int rows = 0;         // row-sliced skinny-N (tile 14, round 6): rows per workgroup (16 / 32), no K split
 };
 
 // Skinny-N fp32 family (conv_gemv.hip): weights spread over the chip, all
@@ -129,6 +130,13 @@ inline int gemv_rows(int nmax) { return nmax <= 32 ? 256 : nmax == 64 ? 128 : 64
 inline int gemv_nmax(int t) { return 4 << (t - 8); }
 bool gemv_fits(int taps, int U, int d, bool transposed, int cps, int nmax);
 int conv1d_gemv(ConvKArgs k, int taps, int nmax, int sep, hipStream_t st);
+// Row-sliced skinny-N form (conv_gemv.hip, round 6): config tile 14 (bit 9 = 32
+// rows per workgroup, else 16) or 15 (8 rows), one K split; NMAX the smallest
+// of 4..32 holding U
+constexpr int kRowsTile = 14, kRowsTile8 = 15, kRowsMaxN = 32;
+bool gemv_rows_fits(int taps, int U, int d, bool transposed, int nchunks, int nmax);
+int conv1d_gemv_rows(ConvKArgs k, int taps, int nmax, int rt, hipStream_t st);
+inline int rows_nmax(int U) { int n = 4; while (n < U) n *= 2; return n; }
 
 // rave_conv1d_args.config: 0 = heuristic, else 1 + tile + 16 (S - 1) + 512 sep
 // (tile: index into the precision's tile table; S: K-splits; sep: split-K

@@ -269,8 +269,10 @@ def test_conv_gemv_configs(N, dev, case):
                    transposed=transposed, out_shift=s // 2 if transposed else 0, act=N.ACT[act],
                    batch=B, t_in=T, t_out=t_out, precision=N.PREC_F32, x=16, y=16, weight=16,
                    alpha=16 if alpha is not None else None, residual=16 if res is not None else None)
-    gemv = [c for c in N.conv_configs(a) if 8 <= ((c - 1) & 15) <= 13]
+    # tiles 8..13: K-split over workgroups; 14 / 15: row-sliced, whole K per workgroup (round 6)
+    gemv = [c for c in N.conv_configs(a) if 8 <= ((c - 1) & 15) <= 15]
     assert gemv, "no skinny-N configurations listed"
+    assert T > 32 or {(c - 1) & 15 for c in gemv} >= {14, 15}, "no row-sliced configuration listed"
     outs = {}
     for cfg in gemv:
         got = run_conv(N, dev, x, w, b, alpha, res, c_in, c_out, k, s, d, pad, transposed, act, True,
@@ -280,7 +282,7 @@ def test_conv_gemv_configs(N, dev, case):
         outs[cfg] = got
     # the in-launch combine (sc1 slabs, last arriver; round 6) sums the K splits in
     # split order, as the separate reduce launch does: bitwise the same
-    pairs = [(c, c + 512) for c in outs if not ((c - 1) >> 9) & 1 and c + 512 in outs]
+    pairs = [(c, c + 512) for c in outs if (c - 1) & 15 < 14 and not ((c - 1) >> 9) & 1 and c + 512 in outs]
     for c0, c1 in pairs:
         assert np.array_equal(outs[c0], outs[c1]), (c0, c1)
 

@@ -156,6 +156,27 @@ def test_conv_f32_inlaunch_configs():
     assert N.lib.rave_conv1d_workspace(C.byref(a)) == -1
 
 
+def test_conv_gemv_rows_configs():
+    """The row-sliced skinny-N form (tiles 14 / 15, round 6: 8, 16 or 32 rows
+    per workgroup over the whole K, one launch) is listed for up to 32 output
+    columns, with one K split only."""
+    def args(T, c_in=512):
+        return N.ConvArgs(c_in=c_in, c_out=512, kernel=3, stride=1, dilation=1, pad_left=2, pad_right=0,
+                          batch=1, t_in=T, t_out=T, precision=N.PREC_F32, x=16, y=16, weight=16)
+    rows = lambda a: [c for c in N.conv_configs(a) if (c - 1) & 15 >= 14]
+    a = args(8)
+    assert sorted(rows(a)) == [15, 16, 15 + 512]                 # 16, 8 and 32 rows per workgroup
+    for c in rows(a):
+        a.config = c
+        assert N.lib.rave_conv1d_workspace(C.byref(a)) == 0      # nothing to combine
+    a.config = 15 + 16                                            # two K splits: refused
+    assert N.lib.rave_conv1d_workspace(C.byref(a)) == -1
+    a.config = 16 + 512                                           # tile 15 has no bit-9 form
+    assert N.lib.rave_conv1d_workspace(C.byref(a)) == -1
+    assert not rows(args(33))                                     # more columns than the form holds
+    assert not rows(args(32, c_in=4096))                          # window beyond the staging area
+
+
 def test_plan_create_and_relocation_bounds():
     ops = (N.PlanOp * 1)()
     ops[0].kind = N.OP_FILL

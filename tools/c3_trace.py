@@ -38,6 +38,9 @@ def run(a):
     dev = torch.device("cuda:0")
     cfg = rcfg.causal()
     tun, src = (None, "autotuned at plan build") if a.retune else _pinned("c3", a.precision)
+    if a.tuning:
+        with open(a.tuning) as fh:
+            tun, src = json.load(fh), a.tuning
     m = RAVE(cfg, init_params(cfg, 0), init_speaker(cfg, 0), device=dev, precision=a.precision, tuning=tun)
     blk, warm, nb = 2048, 8, a.blocks
     x = (0.2 * torch.randn(warm + nb, 1, 1, blk, generator=torch.Generator().manual_seed(0))).to(dev)
@@ -107,6 +110,7 @@ def main():
     r.add_argument("--blocks", type=int, default=32)
     r.add_argument("--retune", action="store_true", help="time every launch choice instead of the pins")
     r.add_argument("--save", help="write the plan's launch choices (RAVE.tuning()) here")
+    r.add_argument("--tuning", help="launch choices to replay instead of the committed pins")
     r.add_argument("--sleep-ms", type=float, default=0.0,
                    help="host sleep before each block (the bench leg has none: clocks stay up)")
     an = sub.add_parser("analyse")
