@@ -305,8 +305,35 @@ __global__ __launch_bounds__(256) void conv1d_gemv_rows_kernel(ConvKArgs a) {
     const int t0 = -a.pad_l;
     const float slope = a.act == RAVE_ACT_LEAKY ? a.slope : 1.0f;
 
+    // K-row kr of the packed image ([chunk][tap][channel][Mpad]) = (chunk, tap j,
+    // channel cl): x of column n at window (chunk * CIT + cl, goff + j d + n ST)
+    const int mrow = m0 + 4 * ml;
+    const int goff = (a.transposed && m0 >= a.split_row) ? 1 : 0;   // (RT | 64: no straddle)
+    const bool rows_ok = mrow < a.Mpad;
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, a.w_bytes);
+    const int nq = a.nchunks * KRW;
+    constexpr int KS = 4 * KL;                       // K-rows per workgroup step
+    // one batch: QB K-rows' weights (16 B per lane each) and window offsets
+    auto load_batch = [&](int k0, f32x4* wv, int* xo) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < QB; ++i) {
+            const int kr = k0 + i * KS;
+            const bool ok = kr < nq && rows_ok;
+            const unsigned off = ok ? ((unsigned)kr * (unsigned)a.Mpad + (unsigned)mrow) * 4u : kOOB;
+            wv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
+            const int c = kr / KRW, rem = kr - c * KRW, j = rem / CIT, cl = rem - j * CIT;
+            xo[i] = kr < nq ? (c * CIT + cl) * XW + goff + j * a.d : 0;   // (past nq: zero weights)
+        }
+    };
+    // the first batch's weights are in flight while the window is staged (they
+    // do not depend on it); each later batch is loaded under the previous one's FMAs
+    const int kfirst = wave * KL + kl;
+    f32x4 wv[QB];
+    int xo[QB];
+    load_batch(kfirst, wv, xo);
+
     // ---------------------------------------------------------------- window
-    constexpr int WB = 32;                           // the whole window is read: keep it in flight
+    constexpr int WB = 8;
     const __amdgpu_buffer_rsrc_t xrs = make_rsrc(a.x + (int64_t)b * a.x_sb, a.x_bytes);
     for (int e0 = tid; e0 < nch * XW; e0 += 256 * WB) {
         float rv[WB];
@@ -337,31 +364,16 @@ __global__ __launch_bounds__(256) void conv1d_gemv_rows_kernel(ConvKArgs a) {
     __syncthreads();
 
     // ---------------------------------------------------------------- K loop
-    // K-row kr of the packed image ([chunk][tap][channel][Mpad]) = (chunk, tap j,
-    // channel cl): x of column n at window (chunk * CIT + cl, goff + j d + n ST)
-    const int mrow = m0 + 4 * ml;
-    const int goff = (a.transposed && m0 >= a.split_row) ? 1 : 0;   // (RT | 64: no straddle)
-    const bool rows_ok = mrow < a.Mpad;
-    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, a.w_bytes);
-    const int nq = a.nchunks * KRW;
     float acc[4][NMAX];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int n = 0; n < NMAX; ++n) acc[r][n] = 0.f;
-    constexpr int KS = 4 * KL;                       // K-rows per workgroup step
-    for (int k0 = wave * KL + kl; k0 < nq; k0 += KS * QB) {
-        f32x4 wv[QB];
-        int xo[QB];
-#pragma unroll
-        for (int i = 0; i < QB; ++i) {
-            const int kr = k0 + i * KS;
-            const bool ok = kr < nq && rows_ok;
-            const unsigned off = ok ? ((unsigned)kr * (unsigned)a.Mpad + (unsigned)mrow) * 4u : kOOB;
-            wv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
-            const int c = kr / KRW, rem = kr - c * KRW, j = rem / CIT, cl = rem - j * CIT;
-            xo[i] = kr < nq ? (c * CIT + cl) * XW + goff + j * a.d : 0;   // (past nq: zero weights)
-        }
+    // (the batch loop runs per wave: its K-rows start at wave * KL, wave-uniform)
+    for (int kw = wave * KL; kw < nq; kw += KS * QB) {
+        f32x4 wn[QB];
+        int xn[QB];
+        if (kw + KS * QB < nq) load_batch(kw + KS * QB + kl, wn, xn);
 #pragma unroll
         for (int i = 0; i < QB; ++i) {
             const float* xr = gsm + xo[i];
@@ -372,7 +384,15 @@ __global__ __launch_bounds__(256) void conv1d_gemv_rows_kernel(ConvKArgs a) {
                 for (int r = 0; r < 4; ++r) acc[r][n] = fmaf(wv[i][r], xv, acc[r][n]);
             }
         }
+        if (kw + KS * QB < nq) {
+#pragma unroll
+            for (int i = 0; i < QB; ++i) {
+                wv[i] = wn[i];
+                xo[i] = xn[i];
+            }
+        }
     }
+    (void)kfirst;
 
     // ---------------------------------------------------------------- sums (fixed order)
 #pragma unroll
