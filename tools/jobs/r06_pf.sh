@@ -3,4 +3,4 @@
 # bench line, rocprofv3 kernel trace + stats, FETCH_SIZE / WRITE_SIZE and MFMA-busy
 # passes of the same command (tools/profile_round.sh, bf3 passes only).
 set -o pipefail
-timeout -k 10 1500 bash tools/profile_round.sh ${1:-r06_pf} bf3
+timeout -k 10 1100 bash tools/profile_round.sh ${1:-r06_pf} bf3
