@@ -372,10 +372,6 @@ __global__ __launch_bounds__(kThreads) void conv1d_mfma_kernel(ConvKArgs a) {
             if constexpr (KS > 1) {
                 if (q % KS != kg) continue;
             }
-            const int i = q >> 1, jj = q & 1;
-            const int n = n0 + wn0 + jj * 32 + l32;
-            (void)i;
-            (void)n;
             f32x4 v4[4];
 #pragma unroll
             for (int g = 0; g < 4; ++g) v4[g] = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -392,7 +392,6 @@ __global__ __launch_bounds__(256) void conv1d_gemv_rows_kernel(ConvKArgs a) {
             }
         }
     }
-    (void)kfirst;
 
     // ---------------------------------------------------------------- sums (fixed order)
 #pragma unroll
