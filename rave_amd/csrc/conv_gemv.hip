@@ -284,6 +284,9 @@ __global__ __launch_bounds__(256) void conv1d_gemv_kernel(ConvKArgs a) {
 //     summed by a fixed xor-shuffle tree, the 4 waves through LDS in wave
 //     order: deterministic, no atomics, no slabs.
 constexpr int kRowsStage = 24576;                  // staged window floats (96 KiB)
+#ifndef RAVE_ROWS_XCD
+#define RAVE_ROWS_XCD 1                            // 0: plain block order (A/B builds)
+#endif
 // the wave-sum area after the window (+ slack: lanes read NMAX columns per row)
 __host__ __device__ inline int rows_red_off(int window, int slack) { return ((window + 3) & ~3) + slack + 16; }
 
@@ -297,7 +300,10 @@ __global__ __launch_bounds__(256) void conv1d_gemv_rows_kernel(ConvKArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ml = lane % ML, kl = lane / ML;
     const int MT = ceil_div(a.M, RT);
-    const int tile = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    // neighbouring row tiles (which read the same 128-byte weight lines at RT < 32)
+    // on one XCD: blocks are dealt round-robin over the 8 XCDs (common.h xcd_major)
+    const int tile = __builtin_amdgcn_readfirstlane(RAVE_ROWS_XCD ? xcd_major((int)blockIdx.x, (int)gridDim.x)
+                                                                   : (int)blockIdx.x);
     const int mt = tile % MT, b = tile / MT;
     const int m0 = mt * RT;
     const int nch = a.nchunks * CIT;                 // staged channels (all of K)
