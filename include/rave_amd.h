@@ -800,10 +800,11 @@ int rave_stream_encode_codes(rave_stream* s, const float* x, int64_t* idx, void*
 int rave_stream_decode_codes(rave_stream* s, const int64_t* idx, float* y, const float* noise_u, void* stream);
 int rave_stream_delay(const rave_stream* s);
 /* Kernel launches one block issues (which 0 = encode, 1 = decode): the kernel
- * nodes of the captured graph (RAVE_STREAM_GRAPH; the staging copies around a
- * replay are not counted) or the plan's launches (eager: one per op, a run of
- * history shifts batched into one launch as rave_plan_run issues it).
- * Negative = status. */
+ * nodes of the captured graph (RAVE_STREAM_GRAPH; the copies around a replay are
+ * not counted: the call copies the block's input straight into the history
+ * buffer and the output out of a staging buffer) or the plan's launches (eager:
+ * one per op, a run of history shifts batched into one launch as rave_plan_run
+ * issues it).  Negative = status. */
 int rave_stream_launches(const rave_stream* s, int which);
 
 #ifdef __cplusplus

@@ -139,10 +139,25 @@ int plan_patch(rave_plan* plan, int op, int offset, const void* data, int n) {
 }
 }  // namespace rave
 
+namespace rave {
+int plan_run_from(rave_plan* plan, void* const* slots, int n_slots, void* stream, int first);
+}
+
 extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, void* stream) {
+    return rave::plan_run_from(plan, slots, n_slots, stream, 0);
+}
+
+namespace rave {
+// Engine-internal: run ops [first, size) of the plan (a stream graph whose input
+// copy the host does itself is captured from op 1; unprofiled when first > 0).
+int plan_run_from(rave_plan* plan, void* const* slots, int n_slots, void* stream, int first) {
     if (!plan) {
         rave::set_error("plan_run: null plan");
         return RAVE_ERR_STATE;
+    }
+    if (first < 0 || first > (int)plan->ops.size()) {
+        rave::set_error("plan_run: bad first op");
+        return RAVE_ERR_ARG;
     }
     // The relocated op list is per call and per host thread (the plan itself is
     // read-only here), so threads may run one plan concurrently on their own
@@ -157,9 +172,9 @@ extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, v
         char* base = static_cast<char*>(slots[r.slot]) + r.byte_offset;
         std::memcpy(scratch[r.op].u.raw + r.field_offset, &base, sizeof(void*));
     }
-    const bool prof = plan->runs < plan->runs_cap;   // armed and not yet full
+    const bool prof = first == 0 && plan->runs < plan->runs_cap;   // armed and not yet full
     hipEvent_t* ev = prof ? plan->ev.data() + (size_t)2 * scratch.size() * plan->runs : nullptr;
-    for (size_t i = 0; i < scratch.size(); ++i) {
+    for (size_t i = (size_t)first; i < scratch.size(); ++i) {
         const rave_plan_op& op = scratch[i];
         int rc;
         if (prof) rave::g_op_events = {ev[2 * i], ev[2 * i + 1]};
@@ -219,3 +234,4 @@ extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, v
     if (prof) ++plan->runs;
     return RAVE_OK;
 }
+}  // namespace rave

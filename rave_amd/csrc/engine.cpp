@@ -2564,13 +2564,42 @@ static int64_t latent_bytes(const Stream& s, bool dec_side) {
     return (int64_t)s.B * (dec_side ? s.m->dec_in : c.latent_size + c.speaker_size) * s.Fz * 4;
 }
 
-static void capture(Stream& s, Plan& p, void* const* slots, int n, hipGraph_t& g, hipGraphExec_t& e) {
+// the plan's first op when it is the block's input copy into a history buffer
+// whose rows the host can fill with one 2-D copy (graph mode, Stream::Direct)
+static Stream::Direct direct_input(const Plan& p) {
+    Stream::Direct d;
+    static const bool on = [] {
+        const char* e = std::getenv("RAVE_STREAM_DIRECT");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || p.ops.empty() || p.ops[0].kind != RAVE_OP_COPY) return d;
+    rave_copy_args c;
+    std::memcpy(&c, p.ops[0].op.u.raw, sizeof(c));
+    const int yoff = (int)offsetof(rave_copy_args, y);
+    for (auto& fp : p.ops[0].ptrs)
+        if (fp.first == yoff && fp.second.kind == PRef::WS) d.dst = (float*)((char*)p.ws_dev + fp.second.off);
+    if (!d.dst) return Stream::Direct{};
+    if (c.channels == 1) {
+        d.pitch = c.y_sb;
+        d.rows = c.batch;
+    } else if (c.y_sb == (int64_t)c.channels * c.y_sc) {
+        d.pitch = c.y_sc;
+        d.rows = (int64_t)c.batch * c.channels;
+    } else {
+        return Stream::Direct{};
+    }
+    d.width = c.t_len;
+    return d;
+}
+
+static void capture(Stream& s, Plan& p, void* const* slots, int n, hipGraph_t& g, hipGraphExec_t& e,
+                    int first = 0) {
     if (e) (void)hipGraphExecDestroy(e);
     if (g) (void)hipGraphDestroy(g);
     e = nullptr;
     g = nullptr;
     RAVE_HIP_OR_THROW(hipStreamBeginCapture(s.cap, hipStreamCaptureModeThreadLocal));
-    const int rc = rave_plan_run(p.handle, slots, n, s.cap);
+    const int rc = plan_run_from(p.handle, slots, n, s.cap, first);
     hipGraph_t graph = nullptr;
     const hipError_t ec = hipStreamEndCapture(s.cap, &graph);
     if (rc != RAVE_OK) {
@@ -2585,11 +2614,11 @@ static void capture(Stream& s, Plan& p, void* const* slots, int n, hipGraph_t& g
 static void recapture(Stream& s) {
     if (s.has_enc()) {
         void* es[2] = {s.x_st, s.z_st};
-        capture(s, *s.enc, es, 2, s.enc_graph, s.enc_exec);
+        capture(s, *s.enc, es, 2, s.enc_graph, s.enc_exec, s.enc_in.dst ? 1 : 0);
     }
     if (s.has_dec()) {
         void* ds[3] = {s.zi_st, s.y_st, s.u_st ? (void*)s.u_st : (void*)s.y_st};
-        capture(s, *s.dec, ds, 3, s.dec_graph, s.dec_exec);
+        capture(s, *s.dec, ds, 3, s.dec_graph, s.dec_exec, s.dec_in.dst ? 1 : 0);
     }
 }
 
@@ -2711,6 +2740,8 @@ extern "C" int rave_stream_create(rave_model* mh, int batch, int block, int flag
             if (s.has_dec()) RAVE_HIP_OR_THROW(hipMemset(s.dec->ws_dev, 0, (size_t)s.dec->ws_floats * 4));
         }
         if (flags & RAVE_STREAM_GRAPH) {
+            if (s.has_enc()) s.enc_in = direct_input(*s.enc);
+            if (s.has_dec()) s.dec_in = direct_input(*s.dec);
             RAVE_HIP_OR_THROW(hipStreamCreateWithFlags(&s.cap, hipStreamNonBlocking));
             recapture(s);
         }
@@ -2734,12 +2765,19 @@ extern "C" int rave_stream_reset(rave_stream* h, void* stream) {
 }
 
 namespace rave {
+// graph mode: the block's input rows straight into the history buffer (Stream::Direct)
+static void direct_copy(const Stream::Direct& d, const void* src, hipStream_t st) {
+    RAVE_HIP_OR_THROW(hipMemcpy2DAsync(d.dst, (size_t)d.pitch * 4, src, (size_t)d.width * 4, (size_t)d.width * 4,
+                                       (size_t)d.rows, hipMemcpyDeviceToDevice, st));
+}
+
 // one encoder block: audio (B, 1, block) -> latents or indices (latent_bytes)
 static void stream_enc(Stream* s, const void* x, void* out, hipStream_t st) {
     if (!s->has_enc()) fail(RAVE_ERR_STATE, "stream was created RAVE_STREAM_DECODE_ONLY");
     sync_adain(*s);
     if (s->flags & RAVE_STREAM_GRAPH) {
-        RAVE_HIP_OR_THROW(hipMemcpyAsync(s->x_st, x, (size_t)s->B * s->block * 4, hipMemcpyDeviceToDevice, st));
+        if (s->enc_in.dst) direct_copy(s->enc_in, x, st);
+        else RAVE_HIP_OR_THROW(hipMemcpyAsync(s->x_st, x, (size_t)s->B * s->block * 4, hipMemcpyDeviceToDevice, st));
         RAVE_HIP_OR_THROW(hipGraphLaunch(s->enc_exec, st));
         RAVE_HIP_OR_THROW(hipMemcpyAsync(out, s->z_st, (size_t)latent_bytes(*s, false), hipMemcpyDeviceToDevice, st));
     } else {
@@ -2769,7 +2807,8 @@ static void stream_dec(Stream* s, const void* in, float* y, const float* noise_u
         }
     }
     if (s->flags & RAVE_STREAM_GRAPH) {
-        RAVE_HIP_OR_THROW(hipMemcpyAsync(s->zi_st, in, (size_t)latent_bytes(*s, true), hipMemcpyDeviceToDevice, st));
+        if (s->dec_in.dst) direct_copy(s->dec_in, in, st);
+        else RAVE_HIP_OR_THROW(hipMemcpyAsync(s->zi_st, in, (size_t)latent_bytes(*s, true), hipMemcpyDeviceToDevice, st));
         RAVE_HIP_OR_THROW(hipGraphLaunch(s->dec_exec, st));
         RAVE_HIP_OR_THROW(hipMemcpyAsync(y, s->y_st, (size_t)s->B * s->block * 4, hipMemcpyDeviceToDevice, st));
     } else {

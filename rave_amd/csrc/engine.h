@@ -34,6 +34,7 @@ inline void check_rc(int rc, const std::string& what) {
     } while (0)
 
 int plan_patch(rave_plan* plan, int op, int offset, const void* data, int n);   // capi.cpp
+int plan_run_from(rave_plan* plan, void* const* slots, int n_slots, void* stream, int first);   // capi.cpp
 
 // ------------------------------------------------------------------ graph
 // One convolution (or transposed convolution) of the reference module tree,
@@ -185,6 +186,14 @@ struct Stream {
     hipGraphExec_t enc_exec = nullptr, dec_exec = nullptr;
     hipGraph_t enc_graph = nullptr, dec_graph = nullptr;
     hipStream_t cap = nullptr;
+    // graph mode: the block's input goes straight into the history buffer's new
+    // columns (a 2-D copy by the host call) instead of staging + the plan's copy
+    // op, which the captured graph then skips (op 0): rows of `width` floats,
+    // `rows` of them at `pitch` floats (RAVE_STREAM_DIRECT=0 keeps the staging)
+    struct Direct {
+        float* dst = nullptr;
+        int64_t pitch = 0, rows = 0, width = 0;
+    } enc_in, dec_in;
     int delay = 0;
     int ad_mode = -1;                              // AdaIN mode baked into the plans
     int ad_row0 = 0;                               // AdaIN buffer row baked into the plans

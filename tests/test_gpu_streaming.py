@@ -242,11 +242,12 @@ def test_stream_direction_flags_and_row0(dev):
     torch.cuda.synchronize()
     assert torch.equal(full.decode(full.encode(x)), y)
     # rave_stream_launches (ABI 18): kernels per block; graph-captured kernel
-    # nodes cover the plan's ops (an op can add a split-K reduce), and a
-    # direction the stream lacks is refused
+    # nodes cover the plan's ops (an op can add a split-K reduce) except the
+    # block's input copy, which a graph-mode call does itself straight into the
+    # history buffer (round 6); a direction the stream lacks is refused
     eager = StreamingRAVE(m, batch=1, block=2048, graph=False)
     for w in ("encode", "decode"):
-        assert full.launches(w) >= eager.launches(w) >= 5
+        assert full.launches(w) >= eager.launches(w) - 1 >= 4
     assert se.launches("encode") == full.launches("encode")
     with pytest.raises(Exception):
         se.launches("decode")
