@@ -802,7 +802,9 @@ int rave_stream_delay(const rave_stream* s);
 /* Kernel launches one block issues (which 0 = encode, 1 = decode): the kernel
  * nodes of the captured graph (RAVE_STREAM_GRAPH; the copies around a replay are
  * not counted: the call copies the block's input straight into the history
- * buffer and the output out of a staging buffer) or the plan's launches (eager:
+ * buffer and the output out of a staging buffer, and fills the latents' speaker
+ * channels outside the graph once per rave_model_set_speaker) or the plan's
+ * launches (eager:
  * one per op, a run of history shifts batched into one launch as rave_plan_run
  * issues it).  Negative = status. */
 int rave_stream_launches(const rave_stream* s, int which);

@@ -140,23 +140,26 @@ int plan_patch(rave_plan* plan, int op, int offset, const void* data, int n) {
 }  // namespace rave
 
 namespace rave {
-int plan_run_from(rave_plan* plan, void* const* slots, int n_slots, void* stream, int first);
+int plan_run_from(rave_plan* plan, void* const* slots, int n_slots, void* stream, int first, int end, int skip);
 }
 
 extern "C" int rave_plan_run(rave_plan* plan, void* const* slots, int n_slots, void* stream) {
-    return rave::plan_run_from(plan, slots, n_slots, stream, 0);
+    return rave::plan_run_from(plan, slots, n_slots, stream, 0, -1, -1);
 }
 
 namespace rave {
-// Engine-internal: run ops [first, size) of the plan (a stream graph whose input
-// copy the host does itself is captured from op 1; unprofiled when first > 0).
-int plan_run_from(rave_plan* plan, void* const* slots, int n_slots, void* stream, int first) {
+// Engine-internal: run ops [first, end) of the plan (end < 0: to the last op),
+// leaving out op `skip` (< 0: none).  A stream graph whose input copy the host
+// does itself is captured from op 1, and its speaker fill runs only when the
+// speaker changes.  Unprofiled unless it is the whole plan.
+int plan_run_from(rave_plan* plan, void* const* slots, int n_slots, void* stream, int first, int end, int skip) {
     if (!plan) {
         rave::set_error("plan_run: null plan");
         return RAVE_ERR_STATE;
     }
-    if (first < 0 || first > (int)plan->ops.size()) {
-        rave::set_error("plan_run: bad first op");
+    if (end < 0) end = (int)plan->ops.size();
+    if (first < 0 || first > end || end > (int)plan->ops.size()) {
+        rave::set_error("plan_run: bad op range");
         return RAVE_ERR_ARG;
     }
     // The relocated op list is per call and per host thread (the plan itself is
@@ -172,9 +175,11 @@ int plan_run_from(rave_plan* plan, void* const* slots, int n_slots, void* stream
         char* base = static_cast<char*>(slots[r.slot]) + r.byte_offset;
         std::memcpy(scratch[r.op].u.raw + r.field_offset, &base, sizeof(void*));
     }
-    const bool prof = first == 0 && plan->runs < plan->runs_cap;   // armed and not yet full
+    const bool prof = first == 0 && end == (int)plan->ops.size() && skip < 0 &&
+                      plan->runs < plan->runs_cap;   // armed and not yet full
     hipEvent_t* ev = prof ? plan->ev.data() + (size_t)2 * scratch.size() * plan->runs : nullptr;
-    for (size_t i = (size_t)first; i < scratch.size(); ++i) {
+    for (size_t i = (size_t)first; i < (size_t)end; ++i) {
+        if ((int)i == skip) continue;
         const rave_plan_op& op = scratch[i];
         int rc;
         if (prof) rave::g_op_events = {ev[2 * i], ev[2 * i + 1]};
@@ -190,7 +195,7 @@ int plan_run_from(rave_plan* plan, void* const* slots, int n_slots, void* stream
                 // one launch, timed on the first op; the rest record empty intervals
                 const rave_shift_args* batch[rave::kShiftBatch];
                 int n = 0;
-                while (n < rave::kShiftBatch && i + n < scratch.size() &&
+                while (n < rave::kShiftBatch && i + n < (size_t)end && (int)(i + n) != skip &&
                        scratch[i + n].kind == RAVE_OP_SHIFT_HISTORY) {
                     batch[n] = &scratch[i + n].u.shift;
                     ++n;

@@ -351,6 +351,7 @@ struct Model {
     std::map<std::string, int> ad_index;
     bool learn_x = false, learn_y = false, touched = false;
     int row0 = 0;
+    int spk_version = 0;               // bumped by rave_model_set_speaker (stream graphs refill)
     // autotuner choices: key -> (choice, ms)
     std::map<std::string, std::pair<int64_t, double>> tuned;
     std::map<std::string, std::unique_ptr<Plan>> plans;
@@ -2122,6 +2123,7 @@ extern "C" int rave_model_set_speaker(rave_model* h, const float* speaker, void*
         // before every later encode/decode (and streaming graph replay) on it
         RAVE_HIP_OR_THROW(hipMemcpyAsync(m->arena + m->spk_off, speaker, sizeof(float) * m->cfg.speaker_size,
                                          hipMemcpyDefault, as_stream(stream)));
+        ++m->spk_version;
     });
 }
 
@@ -2592,14 +2594,36 @@ static Stream::Direct direct_input(const Plan& p) {
     return d;
 }
 
+// the encoder plan's speaker fill when it writes only the staged latents (slot
+// 1), which nothing else in the graph touches: outside the graph, run once per
+// speaker (RAVE_STREAM_SPK_ONCE=0 keeps it in the graph)
+static int speaker_fill_op(const Stream& s) {
+    static const bool on = [] {
+        const char* e = std::getenv("RAVE_STREAM_SPK_ONCE");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || s.codes) return -1;
+    const Plan& p = *s.enc;
+    int found = -1;
+    for (int i = 0; i < (int)p.ops.size(); ++i) {
+        if (p.ops[i].kind != RAVE_OP_FILL) continue;
+        if (found >= 0) return -1;                   // one fill only
+        const int yoff = (int)offsetof(rave_fill_args, y);
+        for (auto& fp : p.ops[i].ptrs)
+            if (fp.first == yoff && fp.second.kind == PRef::IO && fp.second.slot == 1) found = i;
+        if (found != i) return -1;
+    }
+    return found;
+}
+
 static void capture(Stream& s, Plan& p, void* const* slots, int n, hipGraph_t& g, hipGraphExec_t& e,
-                    int first = 0) {
+                    int first = 0, int skip = -1) {
     if (e) (void)hipGraphExecDestroy(e);
     if (g) (void)hipGraphDestroy(g);
     e = nullptr;
     g = nullptr;
     RAVE_HIP_OR_THROW(hipStreamBeginCapture(s.cap, hipStreamCaptureModeThreadLocal));
-    const int rc = plan_run_from(p.handle, slots, n, s.cap, first);
+    const int rc = plan_run_from(p.handle, slots, n, s.cap, first, -1, skip);
     hipGraph_t graph = nullptr;
     const hipError_t ec = hipStreamEndCapture(s.cap, &graph);
     if (rc != RAVE_OK) {
@@ -2614,7 +2638,7 @@ static void capture(Stream& s, Plan& p, void* const* slots, int n, hipGraph_t& g
 static void recapture(Stream& s) {
     if (s.has_enc()) {
         void* es[2] = {s.x_st, s.z_st};
-        capture(s, *s.enc, es, 2, s.enc_graph, s.enc_exec, s.enc_in.dst ? 1 : 0);
+        capture(s, *s.enc, es, 2, s.enc_graph, s.enc_exec, s.enc_in.dst ? 1 : 0, s.enc_fill);
     }
     if (s.has_dec()) {
         void* ds[3] = {s.zi_st, s.y_st, s.u_st ? (void*)s.u_st : (void*)s.y_st};
@@ -2740,7 +2764,10 @@ extern "C" int rave_stream_create(rave_model* mh, int batch, int block, int flag
             if (s.has_dec()) RAVE_HIP_OR_THROW(hipMemset(s.dec->ws_dev, 0, (size_t)s.dec->ws_floats * 4));
         }
         if (flags & RAVE_STREAM_GRAPH) {
-            if (s.has_enc()) s.enc_in = direct_input(*s.enc);
+            if (s.has_enc()) {
+                s.enc_in = direct_input(*s.enc);
+                s.enc_fill = speaker_fill_op(s);
+            }
             if (s.has_dec()) s.dec_in = direct_input(*s.dec);
             RAVE_HIP_OR_THROW(hipStreamCreateWithFlags(&s.cap, hipStreamNonBlocking));
             recapture(s);
@@ -2778,6 +2805,11 @@ static void stream_enc(Stream* s, const void* x, void* out, hipStream_t st) {
     if (s->flags & RAVE_STREAM_GRAPH) {
         if (s->enc_in.dst) direct_copy(s->enc_in, x, st);
         else RAVE_HIP_OR_THROW(hipMemcpyAsync(s->x_st, x, (size_t)s->B * s->block * 4, hipMemcpyDeviceToDevice, st));
+        if (s->enc_fill >= 0 && s->spk_seen != s->m->spk_version) {
+            void* es[2] = {s->x_st, s->z_st};
+            check_rc(plan_run_from(s->enc->handle, es, 2, st, s->enc_fill, s->enc_fill + 1), "speaker fill");
+            s->spk_seen = s->m->spk_version;
+        }
         RAVE_HIP_OR_THROW(hipGraphLaunch(s->enc_exec, st));
         RAVE_HIP_OR_THROW(hipMemcpyAsync(out, s->z_st, (size_t)latent_bytes(*s, false), hipMemcpyDeviceToDevice, st));
     } else {

@@ -34,7 +34,8 @@ inline void check_rc(int rc, const std::string& what) {
     } while (0)
 
 int plan_patch(rave_plan* plan, int op, int offset, const void* data, int n);   // capi.cpp
-int plan_run_from(rave_plan* plan, void* const* slots, int n_slots, void* stream, int first);   // capi.cpp
+int plan_run_from(rave_plan* plan, void* const* slots, int n_slots, void* stream, int first, int end = -1,
+                  int skip = -1);   // capi.cpp
 
 // ------------------------------------------------------------------ graph
 // One convolution (or transposed convolution) of the reference module tree,
@@ -194,6 +195,10 @@ struct Stream {
         float* dst = nullptr;
         int64_t pitch = 0, rows = 0, width = 0;
     } enc_in, dec_in;
+    // graph mode: the encoder plan's speaker fill (op index, -1: none) writes the
+    // constant speaker channels of the staged latents; it runs outside the graph,
+    // once per speaker (Model::spk_version)
+    int enc_fill = -1, spk_seen = -1;
     int delay = 0;
     int ad_mode = -1;                              // AdaIN mode baked into the plans
     int ad_row0 = 0;                               // AdaIN buffer row baked into the plans

@@ -244,10 +244,11 @@ def test_stream_direction_flags_and_row0(dev):
     # rave_stream_launches (ABI 18): kernels per block; graph-captured kernel
     # nodes cover the plan's ops (an op can add a split-K reduce) except the
     # block's input copy, which a graph-mode call does itself straight into the
-    # history buffer (round 6); a direction the stream lacks is refused
+    # history buffer, and the encoder's speaker fill, run once per speaker
+    # (round 6); a direction the stream lacks is refused
     eager = StreamingRAVE(m, batch=1, block=2048, graph=False)
     for w in ("encode", "decode"):
-        assert full.launches(w) >= eager.launches(w) - 1 >= 4
+        assert full.launches(w) >= eager.launches(w) - (2 if w == "encode" else 1) >= 3
     assert se.launches("encode") == full.launches("encode")
     with pytest.raises(Exception):
         se.launches("decode")
@@ -280,3 +281,39 @@ def test_noise_frames_must_divide(dev):
         else:                            # 1 frame * 64 / 16 = 4 band frames, not a multiple of 8
             with pytest.raises(ValueError):
                 m.decode(z)
+
+
+def test_stream_graph_speaker_change(dev):
+    """A graph-mode stream fills the latents' speaker channels outside its graph,
+    once per speaker (round 6): a speaker change between blocks reaches the
+    next block's latents and output exactly as in an eager stream."""
+    from rave_amd import config as rcfg
+    from rave_amd.model import RAVE
+    from rave_amd.streaming import StreamingRAVE
+    from rave_amd.weights import init_params, init_speaker
+    cfg = rcfg.causal(capacity=8)
+    p = init_params(cfg, 21)
+    spk = [init_speaker(cfg, 21), init_speaker(cfg, 22)]
+    gen = torch.Generator().manual_seed(21)
+    xs = [(0.3 * torch.randn(1, 1, 2048, generator=gen)).to(dev) for _ in range(4)]
+    outs = []
+    for graph in (True, False):
+        m = RAVE(cfg, p, spk[0], device=dev)
+        s = StreamingRAVE(m, batch=1, block=2048, graph=graph)
+        zs, ys = [], []
+        for i, x in enumerate(xs):
+            if i == 2:
+                m.set_speaker(spk[1])
+            z = s.encode(x)
+            zs.append(z.clone())
+            ys.append(s.decode(z).clone())
+        torch.cuda.synchronize()
+        outs.append((zs, ys))
+    (zg, yg), (ze, ye) = outs
+    lat = cfg.latent_size
+    for i in range(4):
+        assert torch.equal(zg[i], ze[i]), i
+        assert torch.equal(yg[i], ye[i]), i
+    # the speaker channels follow the change
+    assert not torch.equal(zg[1][:, lat:], zg[2][:, lat:])
+    assert torch.equal(zg[2][:, lat:], zg[3][:, lat:])
